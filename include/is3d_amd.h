@@ -1,0 +1,138 @@
+/*
+ * is3d_amd.h -- C ABI of the MI355X Cooper-Frye continuous-spectra engine
+ * (libis3d_amd.so).  Plain pointers and sizes only; no torch / HIP types.
+ *
+ * This is the drop-in boundary for iS3D2's operation = 1 hot path.  Each entry
+ * point replaces one piece of the reference's EmissionFunctionArray /
+ * Deltaf_Data / IS3D plug-in surface (reference = xyw2016/iS3D2 @ 2025-01-17):
+ *
+ *   is3d_create / is3d_destroy        EmissionFunctionArray ctor / dtor        (EmissionFunction.cpp:114-399)
+ *   is3d_set_params                   ParameterReader flags read by the ctor   (EmissionFunction.cpp:140-205)
+ *   is3d_set_species                  chosen particle arrays                    (EmissionFunction.cpp:997-1021, 339-390)
+ *   is3d_set_pdg                      full PDG arrays (PTMA, PTB Jonah table)   (EmissionFunction.cpp:1025-1036)
+ *   is3d_set_momentum_grid            pT/phi/y/eta Tables                      (iS3D.cpp:254-257, MomentumSpectra.cpp:49-91)
+ *   is3d_set_gauss_laguerre           Gauss_Laguerre::load_roots_and_weights   (readindata.cpp:26-61)
+ *   is3d_set_df_tables                Deltaf_Data::load_df_coefficient_data +  (DeltafData.cpp:65-321)
+ *                                     construct_cubic_splines + compute_jonah_coefficients
+ *   is3d_set_surface                  FO_surf[] -> SoA unpack                  (EmissionFunction.cpp:1049-1161)
+ *   is3d_calculate_spectra            calculate_spectra, operation = 1         (EmissionFunction.cpp:1198-1226)
+ *   is3d_evaluate_df_coefficients     Deltaf_Data::evaluate_df_coefficients    (DeltafData.cpp:501-519)
+ *   is3d_surface_averages             ds_max-weighted averages (Plasma)        (readindata.cpp:316-366, iS3D.cpp:184-219)
+ *
+ * Conventions: caller-owned host buffers in and out; the engine owns its HBM
+ * buffers.  Errors are return codes (never exit()); is3d_last_error() gives the
+ * message the reference would have printed before aborting.  One engine per
+ * host thread per GPU; an engine is not re-entrant.  Output layout is the
+ * reference's dN_pTdpTdphidy[ipart][ipT][iphi][iy] (MomentumSpectra.cpp:252-295).
+ */
+#ifndef IS3D_AMD_H
+#define IS3D_AMD_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define IS3D_ABI_VERSION 1
+
+enum {
+  IS3D_OK = 0,
+  IS3D_ERR_ARG = 1,          /* bad argument / inconsistent setup */
+  IS3D_ERR_STATE = 2,        /* missing setup step */
+  IS3D_ERR_DEVICE = 3,       /* HIP runtime error */
+  IS3D_ERR_DF_RANGE = 4,     /* df coefficient spline/table evaluated out of range (reference: GSL abort / exit) */
+  IS3D_ERR_UNSUPPORTED = 5   /* combination the reference rejects (e.g. PTB + baryon) */
+};
+
+typedef struct is3d_engine is3d_engine;
+
+typedef struct {
+  int operation;                  /* must be 1 (continuous spectra) */
+  int dimension;                  /* 2 = boost-invariant (eta quadrature), 3 = 3+1d (y grid) */
+  int df_mode;                    /* 1 Grad, 2 RTA-CE, 3 PTM, 4 PTB, 5 PTMA */
+  int include_baryon;
+  int include_bulk_deltaf;
+  int include_shear_deltaf;
+  int include_baryondiff_deltaf;
+  int regulate_deltaf;
+  int outflow;
+  int famod_chains;               /* PTMA warm-start chains (= reference OpenMP thread count);
+                                     0 = every cell solved independently (= threads >= cells) */
+  double deta_min;
+  double mass_pion0;
+} is3d_params;
+
+/* Freeze-out surface as structure-of-arrays, reference units after the reader's
+ * conversion (GeV, fm): tau x y eta | dsigma_mu (covariant) | u^x u^y u^eta |
+ * E T P | pi^xx pi^xy pi^xeta pi^yy pi^yeta | Pi | muB nB V^x V^y V^eta.
+ * The baryon arrays may be NULL when include_baryon = 0.  (readindata.h:79-91) */
+typedef struct {
+  const double *tau, *x, *y, *eta;
+  const double *dat, *dax, *day, *dan;
+  const double *ux, *uy, *un;
+  const double *E, *T, *P;
+  const double *pixx, *pixy, *pixn, *piyy, *piyn;
+  const double *bulkPi;
+  const double *muB, *nB, *Vx, *Vy, *Vn;
+} is3d_surface;
+
+typedef struct {
+  long cells;                     /* cells processed in the last call */
+  long breakdown;                 /* feqmod / famod breakdown cells */
+  long pl_negative;               /* cells with p_L < 0 (p_L or p_T < 0 for PTMA) */
+  long recon_fail;                /* PTMA reconstruction failures */
+  long iterations;                /* PTMA total Newton iterations */
+  double ms_prepass, ms_spectra, ms_total;   /* device time of the last call (HIP events) */
+} is3d_stats;
+
+int is3d_abi_version(void);
+is3d_engine *is3d_create(int device);
+void is3d_destroy(is3d_engine *e);
+const char *is3d_last_error(const is3d_engine *e);
+
+int is3d_set_params(is3d_engine *e, const is3d_params *p);
+int is3d_set_species(is3d_engine *e, int n, const double *mass, const double *sign,
+                     const double *degeneracy, const double *baryon);
+int is3d_set_pdg(is3d_engine *e, int n, const double *mass, const double *sign,
+                 const double *degeneracy, const double *baryon);
+int is3d_set_momentum_grid(is3d_engine *e, int npT, const double *pT, int nphi, const double *phi,
+                           int ny, const double *y, int neta, const double *eta, const double *eta_weight);
+/* roots/weights[alpha][points], as in tables/gauss/gla_roots_weights.txt */
+int is3d_set_gauss_laguerre(is3d_engine *e, int alpha, int points, const double *roots, const double *weights);
+/* tables[10][nmuB][nT] in file order c0 c1 c2 c3 c4 F G betabulk betaV betapi;
+ * T_avg = Plasma::temperature (surface average after the 15-digit file round trip),
+ * used only for the PTB (Jonah) table. */
+int is3d_set_df_tables(is3d_engine *e, int nT, int nmuB, const double *T, const double *muB,
+                       const double *tables, double T_avg);
+
+/* Copies n_cells cells (host pointers) into engine-owned HBM. */
+int is3d_set_surface(is3d_engine *e, long n_cells, const is3d_surface *s);
+/* Same, but the 25 field arrays are already in device memory on the engine's GPU
+ * (field-major: dev[f * n_cells + c], f in is3d_surface order).  Not copied. */
+int is3d_set_surface_device(is3d_engine *e, long n_cells, const double *dev_fields);
+
+/* Full call: kernels + device->host copy of dN/(pT dpT dphi dy) into dN_out. */
+int is3d_calculate_spectra(is3d_engine *e, double *dN_out);
+
+/* Split call for resident benchmarking / multi-GPU reduction: launch the whole
+ * hot path on `stream` (a hipStream_t, NULL = default) writing the spectra into
+ * the device buffer dev_out (npart*npT*nphi*ny doubles on the engine's GPU);
+ * is3d_finish() synchronises and reports device-side errors. */
+int is3d_launch(is3d_engine *e, double *dev_out, void *stream);
+int is3d_finish(is3d_engine *e);
+int is3d_get_stats(const is3d_engine *e, is3d_stats *out);
+long is3d_output_size(const is3d_engine *e);
+
+/* Test hooks mirroring reference services. out[15] = c0 c1 c2 c3 c4 shear14 F G
+ * betabulk betaV betapi lambda z delta_lambda delta_z (evaluated on the GPU). */
+int is3d_evaluate_df_coefficients(is3d_engine *e, double T, double muB, double E, double P,
+                                  double bulkPi, double *out15);
+/* out[5] = T, E, P, muB, nB averages (after the setprecision(15) round trip). */
+int is3d_surface_averages(long n_cells, const is3d_surface *s, int include_baryon, double *out5);
+/* Jonah table the engine built: lambda^2, z, bulkPi/P (301 each) and the max. */
+int is3d_get_jonah_table(const is3d_engine *e, double *lambda2, double *z, double *bulk_over_P,
+                         double *bulk_over_P_max);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,79 @@
+"""ctypes binding of libis3d_amd.so (include/is3d_amd.h).
+
+The library is built in-tree by is3d_amd/csrc/Makefile (or __graft_entry__.build()).
+There is no fallback: if the HIP library is missing, importing the engine fails.
+"""
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libis3d_amd.so")
+
+SURFACE_FIELDS = ["tau", "x", "y", "eta", "dat", "dax", "day", "dan", "ux", "uy", "un", "E", "T", "P",
+                  "pixx", "pixy", "pixn", "piyy", "piyn", "bulkPi", "muB", "nB", "Vx", "Vy", "Vn"]
+
+IS3D_OK, IS3D_ERR_ARG, IS3D_ERR_STATE, IS3D_ERR_DEVICE, IS3D_ERR_DF_RANGE, IS3D_ERR_UNSUPPORTED = range(6)
+
+# every symbol include/is3d_amd.h declares
+EXPORTS = ["is3d_abi_version", "is3d_create", "is3d_destroy", "is3d_last_error", "is3d_set_params",
+           "is3d_set_species", "is3d_set_pdg", "is3d_set_momentum_grid", "is3d_set_gauss_laguerre",
+           "is3d_set_df_tables", "is3d_set_surface", "is3d_set_surface_device", "is3d_calculate_spectra",
+           "is3d_launch", "is3d_finish", "is3d_get_stats", "is3d_output_size", "is3d_evaluate_df_coefficients",
+           "is3d_surface_averages", "is3d_get_jonah_table"]
+
+
+class Params(C.Structure):
+    _fields_ = [("operation", C.c_int), ("dimension", C.c_int), ("df_mode", C.c_int), ("include_baryon", C.c_int),
+                ("include_bulk_deltaf", C.c_int), ("include_shear_deltaf", C.c_int),
+                ("include_baryondiff_deltaf", C.c_int), ("regulate_deltaf", C.c_int), ("outflow", C.c_int),
+                ("famod_chains", C.c_int), ("deta_min", C.c_double), ("mass_pion0", C.c_double)]
+
+
+class Surface(C.Structure):
+    _fields_ = [(k, C.POINTER(C.c_double)) for k in SURFACE_FIELDS]
+
+
+class Stats(C.Structure):
+    _fields_ = [("cells", C.c_long), ("breakdown", C.c_long), ("pl_negative", C.c_long), ("recon_fail", C.c_long),
+                ("iterations", C.c_long), ("ms_prepass", C.c_double), ("ms_spectra", C.c_double),
+                ("ms_total", C.c_double)]
+
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("libis3d_amd.so not built (run `make -C is3d_amd/csrc` or __graft_entry__.build())")
+    lib = C.CDLL(LIB_PATH)
+    P = C.POINTER
+    d = C.c_double
+    pd = P(C.c_double)
+    lib.is3d_abi_version.restype = C.c_int
+    lib.is3d_create.restype = C.c_void_p
+    lib.is3d_create.argtypes = [C.c_int]
+    lib.is3d_destroy.argtypes = [C.c_void_p]
+    lib.is3d_last_error.restype = C.c_char_p
+    lib.is3d_last_error.argtypes = [C.c_void_p]
+    lib.is3d_set_params.argtypes = [C.c_void_p, P(Params)]
+    lib.is3d_set_species.argtypes = [C.c_void_p, C.c_int, pd, pd, pd, pd]
+    lib.is3d_set_pdg.argtypes = [C.c_void_p, C.c_int, pd, pd, pd, pd]
+    lib.is3d_set_momentum_grid.argtypes = [C.c_void_p, C.c_int, pd, C.c_int, pd, C.c_int, pd, C.c_int, pd, pd]
+    lib.is3d_set_gauss_laguerre.argtypes = [C.c_void_p, C.c_int, C.c_int, pd, pd]
+    lib.is3d_set_df_tables.argtypes = [C.c_void_p, C.c_int, C.c_int, pd, pd, pd, d]
+    lib.is3d_set_surface.argtypes = [C.c_void_p, C.c_long, P(Surface)]
+    lib.is3d_set_surface_device.argtypes = [C.c_void_p, C.c_long, C.c_void_p]
+    lib.is3d_calculate_spectra.argtypes = [C.c_void_p, pd]
+    lib.is3d_launch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.is3d_finish.argtypes = [C.c_void_p]
+    lib.is3d_get_stats.argtypes = [C.c_void_p, P(Stats)]
+    lib.is3d_output_size.restype = C.c_long
+    lib.is3d_output_size.argtypes = [C.c_void_p]
+    lib.is3d_evaluate_df_coefficients.argtypes = [C.c_void_p, d, d, d, d, d, pd]
+    lib.is3d_surface_averages.argtypes = [C.c_long, P(Surface), C.c_int, pd]
+    lib.is3d_get_jonah_table.argtypes = [C.c_void_p, pd, pd, pd, pd]
+    _lib = lib
+    return lib

@@ -1,0 +1,701 @@
+// cf_math.h -- Cooper-Frye math shared by the HIP kernels (and, for tests only,
+// by a host harness that runs the same functions serially against the oracle).
+//
+// The reference evaluates, for every (cell, species, pT, phi, y, eta) point, one
+// exp + sinh + sqrt + 1-2 divisions (MomentumSpectra.cpp:302-361).  Here the
+// integrand is factorised along the momentum grid axes:
+//
+//   p^tau = mT ch,  p^eta = mT sh / tau,  p^x = pT cos(phi),  p^y = pT sin(phi)
+//   u.p      = mT A_q - pT B_j              A_q = ch ut - sh (tau u^eta),  B_j = cos ux + sin uy
+//   p.dsigma = mT D_q + pT Dp_j             D_q = ch dat + sh dan/tau,      Dp_j = cos dax + sin day
+//   pi.pp    = mT^2 Q1_q + mT pT (ch Pt_j + sh Pn_j) + pT^2 Q3_j
+//   V.p      = mT W_q - pT Wp_j
+//   exp(u.p/T - chem) = exp(mT A_q/T - chem) * exp(-pT B_j/T)
+//
+// so that the per-point work is a handful of FMAs plus one reciprocal; the
+// exponentials move to per-(cell,y/eta) ("y-terms", q index) and per-(cell,phi)
+// ("phi-terms", j index) tables.  For the modified distributions (PTM/PTB/PTMA)
+// p_mod = A^{-1} p_LRF is linear in (mT ch, mT sh, pT cos, pT sin), so
+//   p_mod = mT (ch Uc + sh Us) + pT (cos Vc + sin Vs)
+// with four 3-vectors per cell (Uc = A^{-1}(-Xt,0,-Zt), Us = A^{-1}(tau Xn,0,tau Zn),
+// Vc = A^{-1}(Xx,Yx,0), Vs = A^{-1}(Xy,Yy,0)).  The reference's iterative
+// refinement of A p_mod = p_LRF (<=5 steps, residual 1e-16) only removes rounding
+// from that same linear solve, so it is not repeated.
+#pragma once
+#include <math.h>
+
+#if defined(__HIPCC__) || defined(__HIP__)
+#define IS3D_HD __host__ __device__ inline
+#else
+#define IS3D_HD inline
+#endif
+
+namespace is3d {
+
+enum DfMode : int { GRAD = 1, CE = 2, PTM = 3, PTB = 4, PTMA = 5 };
+
+static constexpr double kHbarC = 0.197327053;            // iS3D.h:14
+
+// ---------------------------------------------------------------------------
+// Per-cell record (output of the prepass, input of the spectra kernel), SoA.
+// ---------------------------------------------------------------------------
+enum Rec : int {
+  R_KIND = 0,   // 0 skip (u.dsigma<=0), 1 separable (Grad/CE or breakdown), 2 modified
+  R_T, R_CHEM,  // T (GeV) and alphaB entering feq (chem = baryon * R_CHEM)
+  R_INVTM, R_CHEMM,  // 1/T_mod (1/lambda for PTMA) and alphaB_mod (upsilonB)
+  R_TAU, R_ETA,
+  R_UT, R_TAUUN, R_UX, R_UY,
+  R_DAT, R_DANT, R_DAX, R_DAY,
+  R_PITT, R_T2PINN, R_TPITN, R_PITX, R_PITY, R_TPIXN, R_TPIYN, R_PIXX, R_PIXY, R_PIYY,
+  R_VT, R_TVN, R_VX, R_VY,
+  R_SHEAR, R_BULK0, R_BULK1, R_BULK2, R_DIFF0, R_DIFF1, R_DLAM, R_DZ,
+  R_ETASCALE, R_DET, R_NARROW, R_RENORM, R_ZB, R_VB,
+  R_UCX, R_UCY, R_UCZ, R_USX, R_USY, R_USZ, R_VCX, R_VCY, R_VCZ, R_VSX, R_VSY, R_VSZ,
+  NREC
+};
+
+// y-term (per cell, q) and phi-term (per cell, j) layouts
+enum YT : int { Y_A = 0, Y_D, Y_Q1, Y_CH, Y_SH, Y_W, Y_WT, Y_MUX, Y_MUY, Y_MUZ, Y_MD, Y_NARROW, NYT };
+enum PT : int { P_Z = 0, P_B, P_PTB, P_PTDP, P_PT, P_PN, P_Q3, P_WP, P_VX, P_VY, P_VZ, NPT };
+
+// surface field order (include/is3d_amd.h, is3d_surface)
+enum Surf : int {
+  S_TAU = 0, S_X, S_Y, S_ETA, S_DAT, S_DAX, S_DAY, S_DAN, S_UX, S_UY, S_UN, S_E, S_T, S_P,
+  S_PIXX, S_PIXY, S_PIXN, S_PIYY, S_PIYN, S_BULKPI, S_MUB, S_NB, S_VX, S_VY, S_VN, NSURF
+};
+
+// ---------------------------------------------------------------------------
+// delta-f coefficient tables (DeltafData.cpp)
+// ---------------------------------------------------------------------------
+enum Spl : int { SP_C0 = 0, SP_C2, SP_C3, SP_F, SP_BB, SP_BV, SP_BP, NSPL };
+
+struct DfTables {
+  int df_mode, include_baryon;
+  int nT, nmuB;
+  const double *T, *muB, *tab;           // tab[10][nmuB][nT]
+  double T_min, muB_min, dT, dmuB;
+  const double *sy[NSPL], *sc[NSPL];     // spline knot values / second-derivative coefficients (x = T)
+  int nj;                                // Jonah table (PTB)
+  const double *jx, *jl2, *jl2c, *jz, *jzc;
+  double bulk_over_P_max;
+};
+
+struct DfCoef {
+  double c0, c1, c2, c3, c4, shear14, F, G, betabulk, betaV, betapi, lambda, z, dlambda, dz;
+};
+
+enum DfErr : int { DF_OK = 0, DF_SPLINE_RANGE = 1, DF_BAD_MODE = 2, DF_TABLE_RANGE = 3, DF_PTB_BARYON = 4 };
+
+// gsl_spline_eval for gsl_interp_cspline: range check, binary search, coeff_calc
+IS3D_HD double spline_eval(const double* x, const double* y, const double* c, int n, double xv, int* err) {
+  if (xv < x[0] || xv > x[n - 1]) { *err = DF_SPLINE_RANGE; return 0.0; }
+  int lo = 0, hi = n - 1;
+  while (hi > lo + 1) { int i = (hi + lo) >> 1; if (x[i] > xv) hi = i; else lo = i; }
+  const double dx = x[lo + 1] - x[lo];
+  if (!(dx > 0.0)) return 0.0;
+  const double dy = y[lo + 1] - y[lo], delx = xv - x[lo];
+  const double ci = c[lo], cip1 = c[lo + 1];
+  const double b = (dy / dx) - dx * (cip1 + 2.0 * ci) / 3.0;
+  const double d = (cip1 - ci) / (3.0 * dx);
+  return y[lo] + delx * (b + delx * (ci + delx * d));
+}
+
+IS3D_HD double tabv(const DfTables& t, int k, int iB, int iT) { return t.tab[((long)k * t.nmuB + iB) * t.nT + iT]; }
+
+IS3D_HD double bilinear(const DfTables& t, int k, double T, double muB, double TL, double TR, double mL, double mR,
+                        int iTL, int iTR, int imL, int imR) {
+  const double fLL = tabv(t, k, imL, iTL), fLR = tabv(t, k, imR, iTL), fRL = tabv(t, k, imL, iTR), fRR = tabv(t, k, imR, iTR);
+  return ((fLL * (TR - T) + fRL * (T - TL)) * (mR - muB) + (fLR * (TR - T) + fRR * (T - TL)) * (muB - mL)) / (t.dT * t.dmuB);
+}
+
+// Deltaf_Data::evaluate_df_coefficients (DeltafData.cpp:324-519)
+IS3D_HD int df_eval(const DfTables& t, double T, double muB, double E, double P, double bulkPi, DfCoef& df) {
+  df = DfCoef{0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  int err = DF_OK;
+  const double T4 = T * T * T * T;
+  if (!t.include_baryon) {
+    switch (t.df_mode) {
+      case GRAD:
+        df.c0 = spline_eval(t.T, t.sy[SP_C0], t.sc[SP_C0], t.nT, T, &err) / T4;
+        df.c2 = spline_eval(t.T, t.sy[SP_C2], t.sc[SP_C2], t.nT, T, &err) / T4;
+        df.shear14 = 2.0 * T * T * (E + P);
+        break;
+      case CE: case PTM: case PTMA:
+        df.F = spline_eval(t.T, t.sy[SP_F], t.sc[SP_F], t.nT, T, &err) * T;
+        df.betabulk = spline_eval(t.T, t.sy[SP_BB], t.sc[SP_BB], t.nT, T, &err) * T4;
+        df.betaV = 1.0;
+        df.betapi = spline_eval(t.T, t.sy[SP_BP], t.sc[SP_BP], t.nT, T, &err) * T4;
+        break;
+      case PTB: {
+        const double l2 = spline_eval(t.jx, t.jl2, t.jl2c, t.nj, bulkPi / P, &err);
+        df.lambda = 0.0;  // reference leaves lambda uninitialised when bulkPi == 0
+        if (bulkPi < 0.0) df.lambda = -sqrt(l2);
+        else if (bulkPi > 0.0) df.lambda = sqrt(l2);
+        df.z = spline_eval(t.jx, t.jz, t.jzc, t.nj, bulkPi / P, &err);
+        df.betapi = spline_eval(t.T, t.sy[SP_BP], t.sc[SP_BP], t.nT, T, &err) * T4;
+        df.dlambda = bulkPi / (5.0 * df.betapi - 3.0 * P * (E + P) / E);
+        df.dz = -3.0 * df.dlambda * P / E;
+        break;
+      }
+      default: return DF_BAD_MODE;
+    }
+    return err;
+  }
+  const int iTL = (int)floor((T - t.T_min) / t.dT), iTR = iTL + 1;
+  const int imL = (int)floor((muB - t.muB_min) / t.dmuB), imR = imL + 1;
+  if (!(iTL >= 0 && iTR < t.nT) || !(imL >= 0 && imR < t.nmuB)) return DF_TABLE_RANGE;
+  const double TL = t.T[iTL], TR = t.T[iTR], mL = t.muB[imL], mR = t.muB[imR];
+  const double T3 = T * T * T, T5 = T4 * T;
+  switch (t.df_mode) {
+    case GRAD:
+      df.c0 = bilinear(t, 0, T, muB, TL, TR, mL, mR, iTL, iTR, imL, imR) / T4;
+      df.c1 = bilinear(t, 1, T, muB, TL, TR, mL, mR, iTL, iTR, imL, imR) / T3;
+      df.c2 = bilinear(t, 2, T, muB, TL, TR, mL, mR, iTL, iTR, imL, imR) / T4;
+      df.c3 = bilinear(t, 3, T, muB, TL, TR, mL, mR, iTL, iTR, imL, imR) / T4;
+      df.c4 = bilinear(t, 4, T, muB, TL, TR, mL, mR, iTL, iTR, imL, imR) / T5;
+      df.shear14 = 2.0 * T * T * (E + P);
+      break;
+    case CE: case PTM: case PTMA:
+      df.F = bilinear(t, 5, T, muB, TL, TR, mL, mR, iTL, iTR, imL, imR) * T;
+      df.G = bilinear(t, 6, T, muB, TL, TR, mL, mR, iTL, iTR, imL, imR);
+      df.betabulk = bilinear(t, 7, T, muB, TL, TR, mL, mR, iTL, iTR, imL, imR) * T4;
+      df.betaV = bilinear(t, 8, T, muB, TL, TR, mL, mR, iTL, iTR, imL, imR) * T3;
+      df.betapi = bilinear(t, 9, T, muB, TL, TR, mL, mR, iTL, iTR, imL, imR) * T4;
+      break;
+    case PTB: return DF_PTB_BARYON;
+    default: return DF_BAD_MODE;
+  }
+  return DF_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Gauss-Laguerre thermal integrals (GaussThermal.cpp:7-78)
+// ---------------------------------------------------------------------------
+IS3D_HD double gt_neq(const double* r, const double* w, int n, double mbar, double alphaB, double baryon, double sign) {
+  double s = 0.0;
+  for (int k = 0; k < n; k++) {
+    const double p = r[k], Eb = sqrt(p * p + mbar * mbar);
+    s += w[k] * (p * exp(p) / (exp(Eb - baryon * alphaB) + sign));
+  }
+  return s;
+}
+IS3D_HD double gt_J10(const double* r, const double* w, int n, double mbar, double alphaB, double baryon, double sign) {
+  double s = 0.0;
+  for (int k = 0; k < n; k++) {
+    const double p = r[k], Eb = sqrt(p * p + mbar * mbar), q = exp(Eb - baryon * alphaB) + sign;
+    s += w[k] * (p * exp(p + Eb - baryon * alphaB) / (q * q));
+  }
+  return s;
+}
+IS3D_HD double gt_J20(const double* r, const double* w, int n, double mbar, double alphaB, double baryon, double sign) {
+  double s = 0.0;
+  for (int k = 0; k < n; k++) {
+    const double p = r[k], Eb = sqrt(p * p + mbar * mbar), q = exp(Eb - baryon * alphaB) + sign;
+    s += w[k] * (Eb * exp(p + Eb - baryon * alphaB) / (q * q));
+  }
+  return s;
+}
+
+// ---------------------------------------------------------------------------
+// 3x3 helpers: LU with partial pivoting (gsl_linalg_LU_decomp/_solve/_invert)
+// ---------------------------------------------------------------------------
+IS3D_HD void lu3_decomp(double* A, int* perm) {
+  perm[0] = 0; perm[1] = 1; perm[2] = 2;
+  for (int j = 0; j < 3; j++) {
+    int piv = j; double mx = fabs(A[3 * j + j]);
+    for (int i = j + 1; i < 3; i++) if (fabs(A[3 * i + j]) > mx) { mx = fabs(A[3 * i + j]); piv = i; }
+    if (piv != j) {
+      for (int k = 0; k < 3; k++) { const double t = A[3 * j + k]; A[3 * j + k] = A[3 * piv + k]; A[3 * piv + k] = t; }
+      const int t = perm[j]; perm[j] = perm[piv]; perm[piv] = t;
+    }
+    const double ajj = A[3 * j + j];
+    if (ajj != 0.0) {
+      for (int i = j + 1; i < 3; i++) {
+        const double aij = A[3 * i + j] / ajj;
+        A[3 * i + j] = aij;
+        for (int k = j + 1; k < 3; k++) A[3 * i + k] -= aij * A[3 * j + k];
+      }
+    }
+  }
+}
+
+IS3D_HD void lu3_solve(const double* LU, const int* perm, const double* b, double* x) {
+  double y[3];
+  for (int i = 0; i < 3; i++) y[i] = b[perm[i]];
+  for (int i = 0; i < 3; i++) { double s = y[i]; for (int k = 0; k < i; k++) s -= LU[3 * i + k] * y[k]; y[i] = s; }
+  for (int i = 2; i >= 0; i--) { double s = y[i]; for (int k = i + 1; k < 3; k++) s -= LU[3 * i + k] * x[k]; x[i] = s / LU[3 * i + i]; }
+}
+
+// A^{-1} applied to the four LRF basis directions -> Uc, Us, Vc, Vs (written to rec R_UCX..R_VSZ)
+IS3D_HD void modified_directions(const double* Asym, double tau, double Xt, double Xx, double Xy, double Xn,
+                                 double Yx, double Yy, double Zt, double Zn, double* rec_u /* 12 */) {
+  double LU[9]; int perm[3];
+  for (int i = 0; i < 9; i++) LU[i] = Asym[i];
+  lu3_decomp(LU, perm);
+  const double dirs[4][3] = {{-Xt, 0.0, -Zt}, {tau * Xn, 0.0, tau * Zn}, {Xx, Yx, 0.0}, {Xy, Yy, 0.0}};
+  for (int d = 0; d < 4; d++) lu3_solve(LU, perm, dirs[d], rec_u + 3 * d);
+}
+
+// ---------------------------------------------------------------------------
+// Milne basis / LRF boosts (LocalRestFrame.cpp:12-41, 133-154)
+// ---------------------------------------------------------------------------
+struct Milne { double Xt, Xx, Xy, Xn, Yx, Yy, Zt, Zn; };
+
+IS3D_HD Milne milne_basis(double ut, double ux, double uy, double un, double uperp, double utperp, double tau) {
+  Milne b;
+  const double sinhL = tau * un / utperp, coshL = ut / utperp;
+  b.Xt = uperp * coshL; b.Xx = 1; b.Xy = 0; b.Xn = uperp * sinhL / tau;
+  b.Yx = 0; b.Yy = 1; b.Zt = sinhL; b.Zn = coshL / tau;
+  if (uperp > 1.e-5) {
+    b.Xx = utperp * ux / uperp; b.Xy = utperp * uy / uperp;
+    b.Yx = -uy / uperp; b.Yy = ux / uperp;
+  }
+  return b;
+}
+
+struct PiLRF { double xx, xy, xz, yy, yz, zz; };
+
+IS3D_HD PiLRF boost_pi(const Milne& b, double tau2, double pitt, double pitx, double pity, double pitn, double pixx,
+                       double pixy, double pixn, double piyy, double piyn, double pinn) {
+  PiLRF r;
+  const double Xt = b.Xt, Xx = b.Xx, Xy = b.Xy, Xn = b.Xn, Yx = b.Yx, Yy = b.Yy, Zt = b.Zt, Zn = b.Zn;
+  r.xx = pitt * Xt * Xt + pixx * Xx * Xx + piyy * Xy * Xy + tau2 * tau2 * pinn * Xn * Xn +
+         2.0 * (-Xt * (pitx * Xx + pity * Xy) + pixy * Xx * Xy + tau2 * Xn * (pixn * Xx + piyn * Xy - pitn * Xt));
+  r.xy = Yx * (-pitx * Xt + pixx * Xx + pixy * Xy + tau2 * pixn * Xn) + Yy * (-pity * Xt + pixy * Xx + piyy * Xy + tau2 * piyn * Xn);
+  r.xz = Zt * (pitt * Xt - pitx * Xx - pity * Xy - tau2 * pitn * Xn) - tau2 * Zn * (pitn * Xt - pixn * Xx - piyn * Xy - tau2 * pinn * Xn);
+  r.yy = pixx * Yx * Yx + 2.0 * pixy * Yx * Yy + piyy * Yy * Yy;
+  r.yz = -Zt * (pitx * Yx + pity * Yy) + tau2 * Zn * (pixn * Yx + piyn * Yy);
+  r.zz = -(r.xx + r.yy);
+  return r;
+}
+
+// ---------------------------------------------------------------------------
+// Run-level constants for the prepass
+// ---------------------------------------------------------------------------
+struct PrepConsts {
+  int df_mode, dim, include_baryon, include_bulk, include_shear, include_diff;
+  double deta_min, mass_pion0;
+  int gla_pts;
+  const double *gla_r1, *gla_w1, *gla_r2, *gla_w2;
+  double two_pi2_hbarC3;
+};
+
+// common fields for every record
+IS3D_HD void rec_common(double* R, double tau, double eta, double ut, double un, double ux, double uy, double dat,
+                        double dax, double day, double dan, double T) {
+  R[R_TAU] = tau; R[R_ETA] = eta; R[R_UT] = ut; R[R_TAUUN] = tau * un; R[R_UX] = ux; R[R_UY] = uy;
+  R[R_DAT] = dat; R[R_DANT] = dan / tau; R[R_DAX] = dax; R[R_DAY] = day; R[R_T] = T;
+  R[R_ZB] = sqrt(ux * ux + uy * uy) / T;
+}
+
+IS3D_HD void rec_pi(double* R, double tau, double pitt, double pitx, double pity, double pitn, double pixx, double pixy,
+                    double pixn, double piyy, double piyn, double pinn) {
+  R[R_PITT] = pitt; R[R_T2PINN] = tau * tau * pinn; R[R_TPITN] = tau * pitn; R[R_PITX] = pitx; R[R_PITY] = pity;
+  R[R_TPIXN] = tau * pixn; R[R_TPIYN] = tau * piyn; R[R_PIXX] = pixx; R[R_PIXY] = pixy; R[R_PIYY] = piyy;
+}
+
+// --- Grad / RTA-CE prologue (MomentumSpectra.cpp:109-246) ---
+IS3D_HD int prep_grad_ce(const PrepConsts& k, const DfTables& tb, const double* s, double* R) {
+  for (int f = 0; f < NREC; f++) R[f] = 0.0;
+  const double tau = s[S_TAU], tau2 = tau * tau;
+  const double eta = (k.dim == 3) ? s[S_ETA] : 0.0;
+  const double dat = s[S_DAT], dax = s[S_DAX], day = s[S_DAY], dan = s[S_DAN];
+  const double ux = s[S_UX], uy = s[S_UY], un = s[S_UN];
+  const double ux2 = ux * ux, uy2 = uy * uy, utperp = sqrt(1.0 + ux2 + uy2), tau2_un = tau2 * un;
+  const double ut = sqrt(utperp * utperp + tau2_un * un), ut2 = ut * ut;
+  if (ut * dat + ux * dax + uy * day + un * dan <= 0.0) { R[R_KIND] = 0.0; return DF_OK; }
+  const double T = s[S_T], P = s[S_P], E = s[S_E];
+  double pitt = 0, pitx = 0, pity = 0, pitn = 0, pixx = 0, pixy = 0, pixn = 0, piyy = 0, piyn = 0, pinn = 0;
+  if (k.include_shear) {
+    pixx = s[S_PIXX]; pixy = s[S_PIXY]; pixn = s[S_PIXN]; piyy = s[S_PIYY]; piyn = s[S_PIYN];
+    pinn = (pixx * (ux2 - ut2) + piyy * (uy2 - ut2) + 2.0 * (pixy * ux * uy + tau2_un * (pixn * ux + piyn * uy))) / (tau2 * utperp * utperp);
+    pitn = (pixn * ux + piyn * uy + tau2_un * pinn) / ut;
+    pity = (pixy * ux + piyy * uy + tau2_un * piyn) / ut;
+    pitx = (pixx * ux + pixy * uy + tau2_un * pixn) / ut;
+    pitt = (pitx * ux + pity * uy + tau2_un * pitn) / ut;
+  }
+  const double bulkPi = k.include_bulk ? s[S_BULKPI] : 0.0;
+  double muB = 0, alphaB = 0, nB = 0, Vt = 0, Vx = 0, Vy = 0, Vn = 0, ber = 0;
+  if (k.include_baryon && k.include_diff) {
+    muB = s[S_MUB]; nB = s[S_NB]; Vx = s[S_VX]; Vy = s[S_VY]; Vn = s[S_VN];
+    Vt = (Vx * ux + Vy * uy + Vn * tau2_un) / ut;
+    alphaB = muB / T;
+    ber = nB / (E + P);
+  }
+  DfCoef df;
+  const int err = df_eval(tb, T, muB, E, P, bulkPi, df);
+  if (err) return err;
+  rec_common(R, tau, eta, ut, un, ux, uy, dat, dax, day, dan, T);
+  rec_pi(R, tau, pitt, pitx, pity, pitn, pixx, pixy, pixn, piyy, piyn, pinn);
+  R[R_VT] = Vt; R[R_TVN] = tau * Vn; R[R_VX] = Vx; R[R_VY] = Vy;
+  R[R_CHEM] = alphaB;
+  if (k.df_mode == GRAD) {
+    R[R_SHEAR] = 1.0 / df.shear14;
+    R[R_BULK0] = (df.c0 - df.c2) * bulkPi; R[R_BULK1] = df.c1 * bulkPi; R[R_BULK2] = (4. * df.c2 - df.c0) * bulkPi;
+    R[R_DIFF0] = df.c3; R[R_DIFF1] = df.c4;
+  } else {
+    R[R_SHEAR] = 0.5 / (df.betapi * T);
+    R[R_BULK0] = df.F / (T * T * df.betabulk) * bulkPi; R[R_BULK1] = df.G / df.betabulk * bulkPi;
+    R[R_BULK2] = bulkPi / (3.0 * T * df.betabulk);
+    R[R_DIFF0] = ber / df.betaV; R[R_DIFF1] = 1.0 / df.betaV;
+  }
+  R[R_ETASCALE] = 1.0;
+  R[R_KIND] = 1.0;
+  return DF_OK;
+}
+
+// --- PTM / PTB prologue (MomentumSpectra.cpp:516-773 + EmissionFunction.cpp:65-109) ---
+// stats[0] += breakdown, stats[1] += pl<0.  renorm_base: PTM -> 1/den (species factor from the
+// renorm kernel), PTB -> z/den.  aux[0..3] = T, T_mod, alphaB, alphaB_mod and aux[4..6] = F, G,
+// betabulk and aux[7] bulkPi (for the PTM renorm kernel).
+IS3D_HD int prep_feqmod(const PrepConsts& k, const DfTables& tb, const double* s, double* R, double* aux, int* flags) {
+  for (int f = 0; f < NREC; f++) R[f] = 0.0;
+  flags[0] = flags[1] = 0;
+  const double tau = s[S_TAU], tau2 = tau * tau;
+  const double eta = (k.dim == 3) ? s[S_ETA] : 0.0;
+  const double dat = s[S_DAT], dax = s[S_DAX], day = s[S_DAY], dan = s[S_DAN];
+  const double ux = s[S_UX], uy = s[S_UY], un = s[S_UN];
+  const double ut = sqrt(1.0 + ux * ux + uy * uy + tau2 * un * un);
+  if (ut * dat + ux * dax + uy * day + un * dan <= 0.0) { R[R_KIND] = 0.0; return DF_OK; }
+  const double ut2 = ut * ut, ux2 = ux * ux, uy2 = uy * uy;
+  const double uperp = sqrt(ux * ux + uy * uy), utperp = sqrt(1.0 + ux * ux + uy * uy);
+  const double T = s[S_T], P = s[S_P], E = s[S_E];
+  double pitt = 0, pitx = 0, pity = 0, pitn = 0, pixx = 0, pixy = 0, pixn = 0, piyy = 0, piyn = 0, pinn = 0;
+  if (k.include_shear) {
+    pixx = s[S_PIXX]; pixy = s[S_PIXY]; pixn = s[S_PIXN]; piyy = s[S_PIYY]; piyn = s[S_PIYN];
+    pinn = (pixx * (ux2 - ut2) + piyy * (uy2 - ut2) + 2.0 * (pixy * ux * uy + tau2 * un * (pixn * ux + piyn * uy))) / (tau2 * utperp * utperp);
+    pitn = (pixn * ux + piyn * uy + tau2 * pinn * un) / ut;
+    pity = (pixy * ux + piyy * uy + tau2 * piyn * un) / ut;
+    pitx = (pixx * ux + pixy * uy + tau2 * pixn * un) / ut;
+    pitt = (pitx * ux + pity * uy + tau2 * pitn * un) / ut;
+  }
+  double bulkPi = k.include_bulk ? s[S_BULKPI] : 0.0;
+  double muB = 0, alphaB = 0, nB = 0, Vt = 0, Vx = 0, Vy = 0, Vn = 0, ber = 0;
+  if (k.include_baryon && k.include_diff) {
+    muB = s[S_MUB]; nB = s[S_NB]; Vx = s[S_VX]; Vy = s[S_VY]; Vn = s[S_VN];
+    Vt = (Vx * ux + Vy * uy + tau2 * Vn * un) / ut;
+    alphaB = muB / T;
+    ber = nB / (E + P);
+  }
+  if (k.df_mode == PTB) {
+    if (bulkPi < -P) bulkPi = -(1.0 - 1.e-5) * P;
+    else if (bulkPi / P > tb.bulk_over_P_max) bulkPi = P * (tb.bulk_over_P_max - 1.e-5);
+  }
+  const double zt = tau * un / utperp, zn = ut / (tau * utperp);
+  const double pl = P + bulkPi + zt * zt * pitt + tau2 * tau2 * zn * zn * pinn + 2. * tau2 * zt * zn * pitn;
+  if (pl < 0) flags[1] = 1;
+  DfCoef df;
+  const int err = df_eval(tb, T, muB, E, P, bulkPi, df);
+  if (err) return err;
+  const double F = df.F, G = df.G, betabulk = df.betabulk, betaV = df.betaV, betapi = df.betapi;
+  const Milne b = milne_basis(ut, ux, uy, un, uperp, utperp, tau);
+  const PiLRF pl_ = boost_pi(b, tau2, pitt, pitx, pity, pitn, pixx, pixy, pixn, piyy, piyn, pinn);
+  double T_mod = T, alphaB_mod = alphaB;
+  if (k.df_mode == PTM) { T_mod = T + bulkPi * F / betabulk; alphaB_mod = alphaB + bulkPi * G / betabulk; }
+  const double shear_coeff = 0.5 / (betapi * T);
+  const double shear_mod = 0.5 / betapi;
+  double bulk_mod = bulkPi / (3.0 * betabulk);
+  if (k.df_mode == PTB) bulk_mod = df.lambda;
+  const double Axx = 1.0 + pl_.xx * shear_mod + bulk_mod, Axy = pl_.xy * shear_mod, Axz = pl_.xz * shear_mod;
+  const double Ayy = 1.0 + pl_.yy * shear_mod + bulk_mod, Ayz = pl_.yz * shear_mod, Azz = 1.0 + pl_.zz * shear_mod + bulk_mod;
+  const double detA = Axx * (Ayy * Azz - Ayz * Ayz) - Axy * (Axy * Azz - Ayz * Axz) + Axz * (Axy * Ayz - Ayy * Axz);
+  const double detA_b23 = pow(1.0 + bulk_mod, 2);
+  const double A[9] = {Axx, Axy, Axz, Axy, Ayy, Ayz, Axz, Ayz, Azz};
+  // breakdown test (EmissionFunction.cpp:65-109, fast = 0)
+  int breaks = 0;
+  if (k.df_mode == PTM) {
+    const double mbar = k.mass_pion0 / T;
+    const double neq_fact = T * T * T / k.two_pi2_hbarC3, J20_fact = T * neq_fact;
+    const double neq = neq_fact * gt_neq(k.gla_r1, k.gla_w1, k.gla_pts, mbar, 0., 0., -1.);
+    const double J20 = J20_fact * gt_J20(k.gla_r2, k.gla_w2, k.gla_pts, mbar, 0., 0., -1.);
+    const double dn = bulkPi * (neq + J20 * F / T / T) / betabulk;
+    breaks = (detA <= k.deta_min || (neq + dn < 0.0));
+  } else {
+    breaks = (detA <= k.deta_min || df.z < 0.0);
+  }
+  flags[0] = breaks;
+  double eta_scale = 1.0;
+  if (detA > k.deta_min && k.dim == 2) eta_scale = detA / detA_b23;
+  const double den = (k.dim == 2) ? detA_b23 : detA;
+  double renorm_base = 1.0;
+  if (k.include_bulk && k.df_mode == PTB) renorm_base = df.z;
+  rec_common(R, tau, eta, ut, un, ux, uy, dat, dax, day, dan, T);
+  rec_pi(R, tau, pitt, pitx, pity, pitn, pixx, pixy, pixn, piyy, piyn, pinn);
+  R[R_VT] = Vt; R[R_TVN] = tau * Vn; R[R_VX] = Vx; R[R_VY] = Vy;
+  R[R_CHEM] = (k.df_mode == PTB) ? 0.0 : alphaB;   // PTB breakdown feq has no chemical potential (:913)
+  R[R_INVTM] = 1.0 / T_mod; R[R_CHEMM] = alphaB_mod;
+  R[R_SHEAR] = shear_coeff;
+  if (k.df_mode == PTM) {   // linearised CE fallback (:887-909): same shape as CE
+    R[R_BULK0] = F / (T * T * betabulk) * bulkPi; R[R_BULK1] = G / betabulk * bulkPi;
+    R[R_BULK2] = 1.0 / (3.0 * T * betabulk) * bulkPi;
+    R[R_DIFF0] = ber / betaV; R[R_DIFF1] = 1.0 / betaV;
+  } else {
+    R[R_DLAM] = df.dlambda; R[R_DZ] = df.dz;
+  }
+  R[R_ETASCALE] = eta_scale; R[R_DET] = detA;
+  R[R_NARROW] = (k.dim == 3 && detA < 0.01) ? 1.0 : 0.0;
+  R[R_RENORM] = renorm_base / den;
+  modified_directions(A, tau, b.Xt, b.Xx, b.Xy, b.Xn, b.Yx, b.Yy, b.Zt, b.Zn, R + R_UCX);
+  R[R_VB] = sqrt(R[R_VCX] * R[R_VCX] + R[R_VCY] * R[R_VCY] + R[R_VCZ] * R[R_VCZ]) +
+            sqrt(R[R_VSX] * R[R_VSX] + R[R_VSY] * R[R_VSY] + R[R_VSZ] * R[R_VSZ]);
+  aux[0] = T; aux[1] = T_mod; aux[2] = alphaB; aux[3] = alphaB_mod; aux[4] = F; aux[5] = G; aux[6] = betabulk; aux[7] = bulkPi;
+  aux[8] = den;
+  R[R_KIND] = breaks ? 1.0 : 2.0;
+  return DF_OK;
+}
+
+// PTM per-(cell, species) renormalisation (MomentumSpectra.cpp:790-832); NaN => species skipped.
+IS3D_HD double ptm_renorm(const PrepConsts& k, const double* aux, double mass, double sign, double degeneracy, double baryon) {
+  const double T = aux[0], T_mod = aux[1], alphaB = aux[2], alphaB_mod = aux[3], F = aux[4], G = aux[5];
+  const double betabulk = aux[6], bulkPi = aux[7], den = aux[8];
+  double renorm = 1.0;
+  if (k.include_bulk) {
+    const double neq_fact = T * T * T / k.two_pi2_hbarC3;
+    const double dn_fact = bulkPi / betabulk, J20_fact = T * neq_fact, N10_fact = neq_fact;
+    const double nmod_fact = T_mod * T_mod * T_mod / k.two_pi2_hbarC3;
+    const double mbar = mass / T, mbar_mod = mass / T_mod;
+    const double neq = neq_fact * degeneracy * gt_neq(k.gla_r1, k.gla_w1, k.gla_pts, mbar, alphaB, baryon, sign);
+    const double N10 = baryon * N10_fact * degeneracy * gt_J10(k.gla_r1, k.gla_w1, k.gla_pts, mbar, alphaB, baryon, sign);
+    const double J20 = J20_fact * degeneracy * gt_J20(k.gla_r2, k.gla_w2, k.gla_pts, mbar, alphaB, baryon, sign);
+    const double n_linear = neq + dn_fact * (neq + N10 * G + J20 * F / T / T);
+    const double n_mod = nmod_fact * degeneracy * gt_neq(k.gla_r1, k.gla_w1, k.gla_pts, mbar_mod, alphaB_mod, baryon, sign);
+    renorm = n_linear / n_mod;
+  }
+  renorm /= den;
+  return renorm;
+}
+
+// --- PTMA prologue part A (MomentumSpectra.cpp:1159-1285): everything up to the Newton solve.
+// aniso_in: E, pl, pt, T (initial lambda), piTxx, piTxy, piTyy, WTzx, WTzy ; returns kind (0 skip)
+IS3D_HD int prep_famod_a(const PrepConsts& k, const double* s, double* R, double* ain) {
+  for (int f = 0; f < NREC; f++) R[f] = 0.0;
+  const double tau = s[S_TAU], tau2 = tau * tau;
+  const double eta = (k.dim == 3) ? s[S_ETA] : 0.0;
+  const double dat = s[S_DAT], dax = s[S_DAX], day = s[S_DAY], dan = s[S_DAN];
+  const double ux = s[S_UX], uy = s[S_UY], un = s[S_UN];
+  const double ut = sqrt(1. + ux * ux + uy * uy + tau2 * un * un);
+  if (ut * dat + ux * dax + uy * day + un * dan <= 0) { R[R_KIND] = 0.0; return 0; }
+  const double ut2 = ut * ut, ux2 = ux * ux, uy2 = uy * uy;
+  const double uperp = sqrt(ux * ux + uy * uy), utperp = sqrt(1. + ux * ux + uy * uy);
+  const double T = s[S_T], P = s[S_P], E = s[S_E];
+  const double pixx = s[S_PIXX], pixy = s[S_PIXY], pixn = s[S_PIXN], piyy = s[S_PIYY], piyn = s[S_PIYN];
+  const double pinn = (pixx * (ux2 - ut2) + piyy * (uy2 - ut2) + 2. * (pixy * ux * uy + tau2 * un * (pixn * ux + piyn * uy))) / (tau2 * utperp * utperp);
+  const double pitn = (pixn * ux + piyn * uy + tau2 * pinn * un) / ut;
+  const double pity = (pixy * ux + piyy * uy + tau2 * piyn * un) / ut;
+  const double pitx = (pixx * ux + pixy * uy + tau2 * pixn * un) / ut;
+  const double pitt = (pitx * ux + pity * uy + tau2 * pitn * un) / ut;
+  const double bulkPi = s[S_BULKPI];
+  const double muB = k.include_baryon ? s[S_MUB] : 0.0;
+  const double alphaB = muB / T;
+  const Milne b = milne_basis(ut, ux, uy, un, uperp, utperp, tau);
+  const PiLRF pl_ = boost_pi(b, tau2, pitt, pitx, pity, pitn, pixx, pixy, pixn, piyy, piyn, pinn);
+  const double pl = P + bulkPi + pl_.zz, pt = P + bulkPi - pl_.zz / 2.;
+  double piTxx = 0, piTxy = 0, piTyy = 0, WTzx = 0, WTzy = 0;
+  if (k.include_shear) {
+    piTxx = (pl_.xx - pl_.yy) / 2.; piTxy = pl_.xy; piTyy = -(piTxx);
+    WTzx = pl_.xz; WTzy = pl_.yz;
+  }
+  rec_common(R, tau, eta, ut, un, ux, uy, dat, dax, day, dan, T);
+  // PTMA's feq fallback has no delta-f; pi / V fields stay zero in the record
+  R[R_CHEM] = alphaB; R[R_CHEMM] = alphaB;   // upsilonB = alphaB (:1292)
+  // basis for the modified directions (stashed in the U/V slots until part B)
+  R[R_UCX] = b.Xt; R[R_UCY] = b.Xx; R[R_UCZ] = b.Xy; R[R_USX] = b.Xn; R[R_USY] = b.Yx; R[R_USZ] = b.Yy;
+  R[R_VCX] = b.Zt; R[R_VCY] = b.Zn;
+  ain[0] = E; ain[1] = pl; ain[2] = pt; ain[3] = T;
+  ain[4] = piTxx; ain[5] = piTxy; ain[6] = piTyy; ain[7] = WTzx; ain[8] = WTzy;
+  R[R_KIND] = 2.0;
+  return 1;
+}
+
+// --- PTMA prologue part B (MomentumSpectra.cpp:1372-1481), after the Newton solve.
+// sol: lambda, aT, aL, broken(0/1), betapiperp, betaWperp
+IS3D_HD void prep_famod_b(const PrepConsts& k, double* R, const double* ain, const double* sol, int* breakdown_out) {
+  const double tau = R[R_TAU];
+  const double Xt = R[R_UCX], Xx = R[R_UCY], Xy = R[R_UCZ], Xn = R[R_USX], Yx = R[R_USY], Yy = R[R_USZ];
+  const double Zt = R[R_VCX], Zn = R[R_VCY];
+  const double piTxx = ain[4], piTxy = ain[5], piTyy = ain[6], WTzx = ain[7], WTzy = ain[8];
+  const double lambda = sol[0], aT = sol[1], aL = sol[2];
+  int broken = (int)sol[3];
+  const double shear_coeff = 0.5 / sol[4], diff_coeff = 1. / sol[5];
+  const double Axx = aT, Ayy = aT, Azz = aL, detA = Axx * Ayy * Azz;
+  const double Cxx = 1. + shear_coeff * piTxx, Cxy = shear_coeff * piTxy, Cxz = diff_coeff * WTzx * aT / (aT + aL);
+  const double Cyx = Cxy, Cyy = 1. + shear_coeff * piTyy, Cyz = diff_coeff * WTzy * aT / (aT + aL);
+  const double Czx = diff_coeff * WTzx * aL / (aT + aL), Czy = diff_coeff * WTzy * aL / (aT + aL), Czz = 1.;
+  const double detC = Cxx * (Cyy * Czz - Cyz * Czy) - Cxy * (Cyx * Czz - Cyz * Czx) + Cxz * (Cyx * Czy - Cyy * Czx);
+  const double Bxx = Axx + aT * shear_coeff * piTxx, Bxy = aT * shear_coeff * piTxy, Bxz = diff_coeff * WTzx * aT * aL / (aT + aL);
+  const double Byy = Ayy + aT * shear_coeff * piTyy, Byz = diff_coeff * WTzy * aT * aL / (aT + aL), Bzz = Azz;
+  const double detB = detC * detA;
+  const double detB_b23 = (2. * aT + aL) * (2. * aT + aL) / 9.;
+  const double B[9] = {Bxx, Bxy, Bxz, Bxy, Byy, Byz, Bxz, Byz, Bzz};
+  if (detB <= k.deta_min) broken = 1;
+  double eta_scale = 1;
+  if (detB > k.deta_min && k.dim == 2) eta_scale = detB / detB_b23;
+  const double renorm = eta_scale / detC;
+  if (isnan(renorm) || isinf(renorm)) broken = 1;
+  modified_directions(B, tau, Xt, Xx, Xy, Xn, Yx, Yy, Zt, Zn, R + R_UCX);
+  R[R_VB] = sqrt(R[R_VCX] * R[R_VCX] + R[R_VCY] * R[R_VCY] + R[R_VCZ] * R[R_VCZ]) +
+            sqrt(R[R_VSX] * R[R_VSX] + R[R_VSY] * R[R_VSY] + R[R_VSZ] * R[R_VSZ]);
+  R[R_INVTM] = 1.0 / lambda;
+  R[R_ETASCALE] = eta_scale; R[R_DET] = detB;
+  R[R_NARROW] = (k.dim == 3 && detB < 0.01) ? 1.0 : 0.0;
+  R[R_RENORM] = fabs(renorm);
+  *breakdown_out = broken;
+  R[R_KIND] = broken ? 1.0 : 2.0;
+}
+
+// ---------------------------------------------------------------------------
+// y-terms and phi-terms
+// ---------------------------------------------------------------------------
+// variant flags for the separable path
+enum SepFlavor : int { SEP_GRAD = 0, SEP_CE = 1, SEP_PTB = 2, SEP_FEQ = 3 };
+
+// mode -> (separable flavour, use cosh() instead of sqrt(1+sinh^2), w_eta only on the non-eta part of p.dsigma)
+IS3D_HD int sep_flavor(int mode) { return mode == GRAD ? SEP_GRAD : (mode == CE || mode == PTM) ? SEP_CE : mode == PTB ? SEP_PTB : SEP_FEQ; }
+IS3D_HD int quirk_pds(int mode) { return (mode == PTM || mode == PTB) ? 1 : 0; }
+
+// y-terms for (cell R, rapidity y, space-time rapidity eta, weight w)
+IS3D_HD void yterms(int mode, const double* R, double y, double eta, double w, double* Y) {
+  const int quirk = quirk_pds(mode);
+  // separable part: p^tau = mT cosh(y-eta) (Grad/CE: sqrt(1+sinh^2), :307-308)
+  const double sh = sinh(y - eta);
+  const double ch = (mode <= CE) ? sqrt(1.0 + sh * sh) : cosh(y - eta);
+  Y[Y_A] = ch * R[R_UT] - sh * R[R_TAUUN];
+  Y[Y_D] = quirk ? (w * ch * R[R_DAT] + sh * R[R_DANT]) : w * (ch * R[R_DAT] + sh * R[R_DANT]);
+  Y[Y_Q1] = R[R_PITT] * ch * ch + R[R_T2PINN] * sh * sh - 2.0 * R[R_TPITN] * ch * sh;
+  Y[Y_CH] = ch; Y[Y_SH] = sh;
+  Y[Y_W] = R[R_VT] * ch - R[R_TVN] * sh;
+  Y[Y_WT] = w;
+  if (mode >= PTM) {
+    const double es = R[R_ETASCALE];
+    const double shm = sinh(y - es * eta), chm = cosh(y - es * eta);
+    Y[Y_MUX] = chm * R[R_UCX] + shm * R[R_USX];
+    Y[Y_MUY] = chm * R[R_UCY] + shm * R[R_USY];
+    Y[Y_MUZ] = chm * R[R_UCZ] + shm * R[R_USZ];
+    Y[Y_MD] = quirk ? (w * chm * R[R_DAT] + shm * R[R_DANT]) : w * (chm * R[R_DAT] + shm * R[R_DANT]);
+    Y[Y_NARROW] = (R[R_NARROW] != 0.0 && fabs(y - eta) < R[R_DET]) ? 1.0 : 0.0;
+  } else {
+    Y[Y_MUX] = Y[Y_MUY] = Y[Y_MUZ] = Y[Y_MD] = Y[Y_NARROW] = 0.0;
+  }
+}
+
+// phi-terms for (cell R, pT, phi)
+IS3D_HD void phiterms(int mode, const double* R, double pT, double c, double s, double* PH) {
+  const double B = c * R[R_UX] + s * R[R_UY];
+  PH[P_PTB] = pT * B;
+  PH[P_Z] = PH[P_PTB] / R[R_T];
+  PH[P_B] = exp(-PH[P_Z]);
+  PH[P_PTDP] = pT * (c * R[R_DAX] + s * R[R_DAY]);
+  PH[P_PT] = pT * (-2.0 * (R[R_PITX] * c + R[R_PITY] * s));
+  PH[P_PN] = pT * (2.0 * (R[R_TPIXN] * c + R[R_TPIYN] * s));
+  PH[P_Q3] = pT * pT * (R[R_PIXX] * c * c + R[R_PIYY] * s * s + 2.0 * R[R_PIXY] * c * s);
+  PH[P_WP] = pT * (R[R_VX] * c + R[R_VY] * s);
+  if (mode >= PTM) {
+    PH[P_VX] = pT * (c * R[R_VCX] + s * R[R_VSX]);
+    PH[P_VY] = pT * (c * R[R_VCY] + s * R[R_VSY]);
+    PH[P_VZ] = pT * (c * R[R_VCZ] + s * R[R_VSZ]);
+  } else {
+    PH[P_VX] = PH[P_VY] = PH[P_VZ] = 0.0;
+  }
+}
+
+// exp(x) overflows above this; 1/(inf + sign) == 0 exactly as in the reference
+static constexpr double kExpMax = 709.782712893384;
+static constexpr double kFastMax = 700.0;
+
+// ---------------------------------------------------------------------------
+// Lane state for one (cell, species, pT, q) and the per-phi integrand.
+// ---------------------------------------------------------------------------
+struct SepLane {
+  double EA, x, a, mTD, w, q1, mch, msh, mW, c0, b1b, d0b;   // see sep_setup
+  double sign, m2, baryon;
+  int skip, fast;
+};
+
+// Per-(cell, q, species) setup for the separable integrand.  Returns skip=1 when every
+// phi point underflows (exp argument > 709.78 for all phi: contributes exactly 0).
+IS3D_HD void sep_setup(int flavor, const double* R, const double* Y, double mT, double m2, double pT, double sign,
+                       double baryon, SepLane& L) {
+  const double T = R[R_T];
+  L.sign = sign; L.m2 = m2; L.baryon = baryon;
+  L.EA = mT * Y[Y_A];
+  L.x = L.EA / T - baryon * R[R_CHEM];
+  const double zb = pT * R[R_ZB];                 // >= max_j |pT B_j / T|
+  L.skip = (L.x - zb > kExpMax) ? 1 : 0;
+  L.fast = (fabs(L.x) <= kFastMax && zb <= kFastMax) ? 1 : 0;
+  L.a = L.fast ? exp(L.x) : 0.0;
+  L.mTD = mT * Y[Y_D];
+  L.w = Y[Y_WT];
+  const double shear = R[R_SHEAR];
+  L.q1 = shear * mT * mT * Y[Y_Q1];
+  L.mch = shear * mT * Y[Y_CH];
+  L.msh = shear * mT * Y[Y_SH];
+  L.mW = mT * Y[Y_W];
+  if (flavor == SEP_GRAD) {
+    L.c0 = R[R_BULK0] * m2; L.b1b = R[R_BULK1] * baryon; L.d0b = R[R_DIFF0] * baryon;
+  } else if (flavor == SEP_CE) {
+    L.c0 = 0.0; L.b1b = R[R_BULK1] * baryon; L.d0b = R[R_DIFF1] * baryon;
+  } else {
+    L.c0 = R[R_DZ] - 3.0 * R[R_DLAM]; L.b1b = 0.0; L.d0b = 0.0;
+  }
+}
+
+// one separable integrand point; returns w * p.dsigma * f (0 when outflow-cut)
+IS3D_HD double sep_point(int flavor, const double* R, const SepLane& L, const double* PH, int regulate, int outflow) {
+  const double E = L.EA - PH[P_PTB];
+  const double pds = L.mTD + L.w * PH[P_PTDP];
+  const double den = L.fast ? (L.a * PH[P_B] + L.sign) : (exp(L.x - PH[P_Z]) + L.sign);
+  const double feq = 1.0 / den;
+  double f;
+  if (flavor == SEP_FEQ) {
+    f = feq;
+  } else {
+    const double fbar = 1.0 - L.sign * feq;
+    const double ppp = L.q1 + L.mch * PH[P_PT] + L.msh * PH[P_PN] + R[R_SHEAR] * PH[P_Q3];
+    double dfv;
+    if (flavor == SEP_GRAD) {
+      const double Vp = L.mW - PH[P_WP];
+      const double S = ppp + L.c0 + (L.b1b + R[R_BULK2] * E) * E + (L.d0b + R[R_DIFF1] * E) * Vp;
+      dfv = fbar * S;
+    } else if (flavor == SEP_CE) {
+      const double Vp = L.mW - PH[P_WP];
+      const double iE = 1.0 / E;
+      const double S = ppp * iE + R[R_BULK0] * E + L.b1b + R[R_BULK2] * (E - L.m2 * iE) + (R[R_DIFF0] - L.d0b * iE) * Vp;
+      dfv = fbar * S;
+    } else {   // PTB linearised (:920-923)
+      const double iE = 1.0 / E;
+      dfv = fbar * ppp * iE + L.c0 + fbar * R[R_DLAM] * (E - L.m2 * iE) / R[R_T];
+    }
+    if (regulate) dfv = fmax(-1.0, fmin(dfv, 1.0));
+    f = feq * (1.0 + dfv);
+  }
+  const double r = pds * f;
+  return (outflow && pds <= 0.0) ? 0.0 : r;
+}
+
+struct ModLane {
+  double mUx, mUy, mUz, mTD, w, m2, invTm, chemm, rn, sign;
+  int skip;
+};
+
+IS3D_HD void mod_setup(const double* R, const double* Y, double mT, double m2, double pT, double sign, double baryon,
+                       double renorm_abs, ModLane& L) {
+  L.mUx = mT * Y[Y_MUX]; L.mUy = mT * Y[Y_MUY]; L.mUz = mT * Y[Y_MUZ];
+  L.mTD = mT * Y[Y_MD]; L.w = Y[Y_WT]; L.m2 = m2; L.sign = sign;
+  L.invTm = R[R_INVTM]; L.chemm = baryon * R[R_CHEMM]; L.rn = renorm_abs;
+  // E_mod >= | |mT U| - pT |V|max |; if even that overflows exp, every phi point is exactly 0
+  const double mu = sqrt(L.mUx * L.mUx + L.mUy * L.mUy + L.mUz * L.mUz);
+  const double lo = mu - pT * R[R_VB];
+  const double emin = (lo > 0.0) ? sqrt(m2 + lo * lo) * (1.0 - 1e-12) : 0.0;
+  L.skip = (emin * L.invTm - L.chemm > kExpMax + 1.0) ? 1 : 0;
+}
+
+IS3D_HD double mod_point(const ModLane& L, const double* PH, int outflow) {
+  const double qx = L.mUx + PH[P_VX], qy = L.mUy + PH[P_VY], qz = L.mUz + PH[P_VZ];
+  const double Emod = sqrt(L.m2 + qx * qx + qy * qy + qz * qz);
+  const double f = L.rn / (exp(Emod * L.invTm - L.chemm) + L.sign);
+  const double pds = L.mTD + L.w * PH[P_PTDP];
+  const double r = pds * f;
+  return (outflow && pds <= 0.0) ? 0.0 : r;
+}
+
+}  // namespace is3d

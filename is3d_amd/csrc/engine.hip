@@ -1,0 +1,852 @@
+// engine.hip -- MI355X (gfx950) Cooper-Frye continuous-spectra engine behind the
+// C ABI of include/is3d_amd.h.
+//
+// Hot path (reference MomentumSpectra.cpp:32-1682, dispatched from
+// EmissionFunction.cpp:1198-1226):
+//   k_prep_*      one thread per freeze-out cell: u^tau, pi^{mu nu} reconstruction,
+//                 delta-f coefficients (GSL-equivalent spline / bilinear table on
+//                 device), LRF basis, A^{-1} (PTM/PTB), breakdown tests -> cell record
+//   k_aniso       PTMA only: one wavefront per warm-start chain (or per cell),
+//                 Newton solve for (lambda, aT, aL) + famod coefficients
+//   k_renorm      PTM only: per (cell, species) renormalisation n_linear / n_mod
+//   k_spectra     the (cell x species x pT x phi x y [x eta]) integral: workgroup =
+//                 one pT value x 256 (species, y) lanes x a cell range; each lane keeps
+//                 32 phi accumulators in VGPRs; per cell tile the per-(cell,phi) and
+//                 per-(cell,y/eta) factors are built cooperatively in LDS (see
+//                 cf_math.h for the factorisation); no atomics, fixed summation order
+//   k_reduce      sum of the cell-split partial slabs x (2 pi hbarc)^-3 x g
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/is3d_amd.h"
+#include "aniso_math.h"
+#include "cf_math.h"
+#include "spline_host.h"
+
+using namespace is3d;
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kJmax = 32;     // phi accumulators per lane
+constexpr int kTile = 4;      // cells per LDS tile
+
+struct DevTables {            // device copy of the delta-f tables (pointers into one blob)
+  DfTables tb;
+};
+
+// ------------------------------------------------------------------------------------------
+// prepass kernels
+// ------------------------------------------------------------------------------------------
+struct PrepArgs {
+  PrepConsts k;
+  DfTables tb;
+  const double* surf;   // [NSURF][n]
+  double* rec;          // [NREC][n]
+  double* aux;          // PTM/PTB: [9][n]; PTMA: [9][n] Newton inputs
+  long n;
+  int* err;
+  unsigned long long* cnt;  // [0] breakdown [1] pl<0 [2] recon fail [3] iterations
+};
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k_prep(PrepArgs A) {
+  const long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= A.n) return;
+  double s[NSURF];
+#pragma unroll
+  for (int f = 0; f < NSURF; f++) s[f] = A.surf[(long)f * A.n + c];
+  double R[NREC];
+  int err = DF_OK;
+  if (MODE == GRAD || MODE == CE) {
+    err = prep_grad_ce(A.k, A.tb, s, R);
+  } else if (MODE == PTM || MODE == PTB) {
+    double aux[9];
+    int flags[2];
+    err = prep_feqmod(A.k, A.tb, s, R, aux, flags);
+    if (!err) {
+#pragma unroll
+      for (int f = 0; f < 9; f++) A.aux[(long)f * A.n + c] = aux[f];
+      if (flags[0] && R[R_KIND] != 0.0) atomicAdd(&A.cnt[0], 1ull);
+      if (flags[1]) atomicAdd(&A.cnt[1], 1ull);
+    }
+  } else {
+    double ain[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+    prep_famod_a(A.k, s, R, ain);
+#pragma unroll
+    for (int f = 0; f < 9; f++) A.aux[(long)f * A.n + c] = ain[f];
+  }
+  if (err) { atomicMax(A.err, err); R[R_KIND] = 0.0; }
+#pragma unroll
+  for (int f = 0; f < NREC; f++) A.rec[(long)f * A.n + c] = R[f];
+}
+
+struct WaveSum {
+  __device__ double operator()(double v) const {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+  }
+};
+
+struct AnisoArgs {
+  const double* rec; const double* ain; double* sol;   // sol [6][n]
+  long n, chains;
+  Hadrons h;
+  double fp2;
+  unsigned long long* cnt;
+};
+
+// one wavefront per warm-start chain: cells chain, chain + C, chain + 2C, ... (MomentumSpectra.cpp:98-107)
+__global__ __launch_bounds__(64) void k_aniso(AnisoArgs A) {
+  const long chain = blockIdx.x;
+  const int lane = threadIdx.x;
+  double state[4] = {0.0, 0.0, 0.0, 0.0};
+  long cnt[3] = {0, 0, 0};
+  for (long c = chain; c < A.n; c += A.chains) {
+    if (A.rec[(long)R_KIND * A.n + c] == 0.0) continue;
+    double ain[4];
+#pragma unroll
+    for (int f = 0; f < 4; f++) ain[f] = A.ain[(long)f * A.n + c];
+    double out[6];
+    aniso_cell(ain, A.h, lane, 64, WaveSum(), A.fp2, state, out, cnt);
+    if (lane == 0) {
+#pragma unroll
+      for (int f = 0; f < 6; f++) A.sol[(long)f * A.n + c] = out[f];
+    }
+  }
+  if (lane == 0) {
+    if (cnt[0]) atomicAdd(&A.cnt[1], (unsigned long long)cnt[0]);
+    if (cnt[1]) atomicAdd(&A.cnt[2], (unsigned long long)cnt[1]);
+    if (cnt[2]) atomicAdd(&A.cnt[3], (unsigned long long)cnt[2]);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_famod_b(PrepArgs A, const double* sol) {
+  const long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= A.n) return;
+  if (A.rec[(long)R_KIND * A.n + c] == 0.0) return;
+  double R[NREC], ain[9], so[6];
+#pragma unroll
+  for (int f = 0; f < NREC; f++) R[f] = A.rec[(long)f * A.n + c];
+#pragma unroll
+  for (int f = 0; f < 9; f++) ain[f] = A.aux[(long)f * A.n + c];
+#pragma unroll
+  for (int f = 0; f < 6; f++) so[f] = sol[(long)f * A.n + c];
+  int broken = 0;
+  prep_famod_b(A.k, R, ain, so, &broken);
+  if (broken) atomicAdd(&A.cnt[0], 1ull);
+#pragma unroll
+  for (int f = 0; f < NREC; f++) A.rec[(long)f * A.n + c] = R[f];
+}
+
+struct RenormArgs {
+  PrepConsts k;
+  const double* rec; const double* aux; double* renorm;   // renorm[c][s_sorted]
+  const double *mass, *sign, *degen, *baryon;              // sorted species
+  long n; int npart;
+};
+
+__global__ __launch_bounds__(256) void k_renorm(RenormArgs A) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= A.n * A.npart) return;
+  const long c = idx / A.npart;
+  const int s = (int)(idx % A.npart);
+  if (A.rec[(long)R_KIND * A.n + c] == 0.0) { A.renorm[idx] = 0.0; return; }
+  double aux[9];
+#pragma unroll
+  for (int f = 0; f < 9; f++) aux[f] = A.aux[(long)f * A.n + c];
+  A.renorm[idx] = ptm_renorm(A.k, aux, A.mass[s], A.sign[s], A.degen[s], A.baryon[s]);
+}
+
+// ------------------------------------------------------------------------------------------
+// spectra kernel
+// ------------------------------------------------------------------------------------------
+struct SpecArgs {
+  const double* rec; long n;
+  const double* renorm;       // PTM: [c][s_sorted]
+  double* slab; long outsize;
+  const double *smass, *ssign, *sbaryon; const int* sorig;
+  const double *pT, *cphi, *sphi, *yv, *etav, *etaw;
+  int npart, npT, nphi, ny_out, nk, nl, nq, njb;
+  long ntask;
+  long cells_per_split;
+  int regulate, outflow, dim;
+};
+
+template <int MODE, bool FAST>
+__device__ __forceinline__ void sep_phi_loop(const SpecArgs& A, const double* R, const SepLane& L, const double* PHc,
+                                             int j0, int nj, double* acc) {
+  constexpr int FL = (MODE == GRAD) ? SEP_GRAD : (MODE == CE || MODE == PTM) ? SEP_CE : (MODE == PTB) ? SEP_PTB : SEP_FEQ;
+  SepLane Lf = L;
+  Lf.fast = FAST ? 1 : 0;
+#pragma unroll
+  for (int jj = 0; jj < kJmax; jj++) {
+    if (jj < nj) acc[jj] += sep_point(FL, R, Lf, PHc + (j0 + jj) * NPT, A.regulate, A.outflow);
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_spectra(SpecArgs A) {
+  extern __shared__ double smem[];
+  double* s_rec = smem;                                   // [kTile][NREC]
+  double* s_phi = s_rec + kTile * NREC;                   // [kTile][nphi][NPT]
+  double* s_y = s_phi + (long)kTile * A.nphi * NPT;       // [kTile][nq][NYT]
+
+  const int tid = threadIdx.x;
+  const int ipt = blockIdx.y;
+  const double pT = A.pT[ipt];
+  const long task = (long)blockIdx.x * kBlock + tid;
+  const bool active = task < A.ntask;
+  int s = 0, k = 0, jb = 0;
+  if (active) {
+    s = (int)(task % A.npart);
+    const long r = task / A.npart;
+    k = (int)(r % A.nk);
+    jb = (int)(r / A.nk);
+  }
+  const int j0 = jb * kJmax;
+  const int nj = min(kJmax, A.nphi - j0);
+  const double mass = A.smass[s], m2 = mass * mass, sign = A.ssign[s], baryon = A.sbaryon[s];
+  const double mT = sqrt(m2 + pT * pT);
+
+  double acc[kJmax];
+#pragma unroll
+  for (int jj = 0; jj < kJmax; jj++) acc[jj] = 0.0;
+
+  const long c_begin = (long)blockIdx.z * A.cells_per_split;
+  const long c_end = min(A.n, c_begin + A.cells_per_split);
+
+  for (long cb = c_begin; cb < c_end; cb += kTile) {
+    const int nt = (int)min((long)kTile, c_end - cb);
+    for (int idx = tid; idx < kTile * NREC; idx += kBlock) {
+      const int f = idx / kTile, t = idx % kTile;
+      s_rec[t * NREC + f] = (t < nt) ? A.rec[(long)f * A.n + cb + t] : 0.0;
+    }
+    __syncthreads();
+    for (int idx = tid; idx < nt * A.nphi; idx += kBlock) {
+      const int t = idx / A.nphi, j = idx % A.nphi;
+      const double* R = s_rec + t * NREC;
+      if (R[R_KIND] != 0.0) phiterms(MODE, R, pT, A.cphi[j], A.sphi[j], s_phi + ((long)t * A.nphi + j) * NPT);
+    }
+    for (int idx = tid; idx < nt * A.nq; idx += kBlock) {
+      const int t = idx / A.nq, q = idx % A.nq;
+      const double* R = s_rec + t * NREC;
+      if (R[R_KIND] != 0.0) {
+        const int kk = q / A.nl, l = q % A.nl;
+        const double y = (A.dim == 3) ? A.yv[kk] : 0.0;
+        const double eta = (A.dim == 3) ? R[R_ETA] : A.etav[l];
+        const double w = (A.dim == 3) ? 1.0 : A.etaw[l];
+        yterms(MODE, R, y, eta, w, s_y + ((long)t * A.nq + q) * NYT);
+      }
+    }
+    __syncthreads();
+    if (active) {
+      for (int t = 0; t < nt; t++) {
+        const double* R = s_rec + t * NREC;
+        const double kind = R[R_KIND];
+        if (kind == 0.0) continue;
+        double rn_abs = R[R_RENORM];
+        if (MODE == PTM || MODE == PTB) {
+          const double rn = (MODE == PTM) ? A.renorm[(cb + t) * A.npart + s] : R[R_RENORM];
+          if (!isfinite(rn)) continue;    // species skipped (MomentumSpectra.cpp:828-832)
+          rn_abs = fabs(rn);
+        }
+        const double* PHc = s_phi + (long)t * A.nphi * NPT;
+        for (int l = 0; l < A.nl; l++) {
+          const int q = k * A.nl + l;
+          const double* Y = s_y + ((long)t * A.nq + q) * NYT;
+          const bool sep = (MODE <= CE) || kind == 1.0 || Y[Y_NARROW] != 0.0;
+          if (sep) {
+            SepLane L;
+            sep_setup(sep_flavor(MODE), R, Y, mT, m2, pT, sign, baryon, L);
+            if (L.skip) continue;
+            if (L.fast) sep_phi_loop<MODE, true>(A, R, L, PHc, j0, nj, acc);
+            else sep_phi_loop<MODE, false>(A, R, L, PHc, j0, nj, acc);
+          } else if (MODE >= PTM) {
+            ModLane M;
+            mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, M);
+            if (M.skip) continue;
+#pragma unroll
+            for (int jj = 0; jj < kJmax; jj++) {
+              if (jj < nj) acc[jj] += mod_point(M, PHc + (j0 + jj) * NPT, A.outflow);
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (active) {
+    double* out = A.slab + (long)blockIdx.z * A.outsize;
+    const long base = ((long)A.sorig[s] * A.npT + ipt) * A.nphi;
+#pragma unroll
+    for (int jj = 0; jj < kJmax; jj++) {
+      if (jj < nj) out[(base + j0 + jj) * A.ny_out + k] = acc[jj];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_reduce(const double* slab, long outsize, int nsplit, const double* degen_orig,
+                                                long per_species, double prefactor, double* out) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= outsize) return;
+  double acc = 0.0;
+  for (int z = 0; z < nsplit; z++) acc += slab[(long)z * outsize + idx];
+  out[idx] = prefactor * degen_orig[idx / per_species] * acc;
+}
+
+__global__ void k_df_eval(DfTables tb, double T, double muB, double E, double P, double bulkPi, double* out, int* err) {
+  DfCoef df;
+  *err = df_eval(tb, T, muB, E, P, bulkPi, df);
+  const double o[15] = {df.c0, df.c1, df.c2, df.c3, df.c4, df.shear14, df.F, df.G, df.betabulk, df.betaV, df.betapi,
+                        df.lambda, df.z, df.dlambda, df.dz};
+  for (int i = 0; i < 15; i++) out[i] = o[i];
+}
+
+template <class T>
+T* dalloc(size_t count) {
+  void* p = nullptr;
+  if (count == 0) count = 1;
+  if (hipMalloc(&p, count * sizeof(T)) != hipSuccess) return nullptr;
+  return (T*)p;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------
+// engine
+// ------------------------------------------------------------------------------------------
+struct is3d_engine {
+  int device = 0;
+  std::string err;
+  bool have_params = false, have_species = false, have_pdg = false, have_grid = false, have_gla = false, have_df = false;
+  is3d_params p{};
+  // species (original order) and mass-sorted permutation
+  std::vector<double> mass, sign, degen, baryon;
+  std::vector<int> order;
+  std::vector<double> pdg_mass, pdg_sign, pdg_degen, pdg_baryon;
+  std::vector<double> pT, phi, y, eta, eta_w;
+  int gla_alpha = 0, gla_pts = 0;
+  std::vector<double> gla_r, gla_w;
+  int nT = 0, nmuB = 0;
+  std::vector<double> Tarr, muBarr, tab;
+  double T_avg = 0.0;
+  // derived host tables
+  std::vector<double> jl2, jz, jx, jl2c, jzc;
+  double bp_max = -1.0;
+  bool tables_dirty = true;
+  // device
+  double* d_tables = nullptr; size_t tables_len = 0;
+  DfTables dtb{};
+  double* d_const = nullptr; size_t const_len = 0;    // species, grids, gla, pdg
+  const double *d_smass = nullptr, *d_ssign = nullptr, *d_sbaryon = nullptr, *d_sdegen = nullptr, *d_degen_orig = nullptr;
+  const double *d_pT = nullptr, *d_cphi = nullptr, *d_sphi = nullptr, *d_y = nullptr, *d_eta = nullptr, *d_etaw = nullptr;
+  const double *d_gla = nullptr;
+  const double *d_pdg = nullptr;
+  int* d_sorig = nullptr;
+  double* d_surf = nullptr; bool surf_owned = false; long ncell = 0; long surf_cap = 0;
+  double *d_rec = nullptr, *d_aux = nullptr, *d_sol = nullptr, *d_renorm = nullptr, *d_slab = nullptr, *d_out = nullptr;
+  long rec_cap = 0, aux_cap = 0, sol_cap = 0, renorm_cap = 0, slab_cap = 0, out_cap = 0;
+  int* d_err = nullptr;
+  unsigned long long* d_cnt = nullptr;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  is3d_stats st{};
+  bool launched = false;
+
+  int fail(int code, const std::string& msg) { err = msg; return code; }
+};
+
+static int hip_fail(is3d_engine* e, hipError_t h, const char* what) {
+  return e->fail(IS3D_ERR_DEVICE, std::string(what) + ": " + hipGetErrorString(h));
+}
+#define HIPCHK(e, x)                                           \
+  do {                                                         \
+    hipError_t h_ = (x);                                       \
+    if (h_ != hipSuccess) return hip_fail((e), h_, #x);        \
+  } while (0)
+
+static void dfree(void* p) { if (p) (void)hipFree(p); }
+
+extern "C" int is3d_abi_version(void) { return IS3D_ABI_VERSION; }
+
+extern "C" is3d_engine* is3d_create(int device) {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || device < 0 || device >= ndev) return nullptr;
+  if (hipSetDevice(device) != hipSuccess) return nullptr;
+  is3d_engine* e = new is3d_engine();
+  e->device = device;
+  if (hipMalloc(&e->d_err, sizeof(int)) != hipSuccess || hipMalloc(&e->d_cnt, 8 * sizeof(unsigned long long)) != hipSuccess) {
+    delete e;
+    return nullptr;
+  }
+  for (auto& v : e->ev) (void)hipEventCreate(&v);
+  return e;
+}
+
+extern "C" void is3d_destroy(is3d_engine* e) {
+  if (!e) return;
+  (void)hipSetDevice(e->device);
+  (void)hipDeviceSynchronize();
+  dfree(e->d_tables); dfree(e->d_const);
+  if (e->surf_owned) dfree(e->d_surf);
+  dfree(e->d_rec); dfree(e->d_aux); dfree(e->d_sol); dfree(e->d_renorm); dfree(e->d_slab); dfree(e->d_out);
+  dfree(e->d_err); dfree(e->d_cnt);
+  for (auto& v : e->ev) if (v) (void)hipEventDestroy(v);
+  delete e;
+}
+
+extern "C" const char* is3d_last_error(const is3d_engine* e) { return e ? e->err.c_str() : "null engine"; }
+
+extern "C" int is3d_set_params(is3d_engine* e, const is3d_params* p) {
+  if (!e || !p) return IS3D_ERR_ARG;
+  if (p->operation != 1) return e->fail(IS3D_ERR_UNSUPPORTED, "calculate_spectra: only operation = 1 (continuous spectra) is on this path");
+  if (p->dimension != 2 && p->dimension != 3) return e->fail(IS3D_ERR_ARG, "EmissionFunctionArray error: need to set dimension = (2,3)");
+  if (p->df_mode < 1 || p->df_mode > 5) return e->fail(IS3D_ERR_ARG, "EmissionFunctionArray error: need to set df_mode = (1,2,3,4,5)");
+  if (p->df_mode == PTB && p->include_baryon) return e->fail(IS3D_ERR_UNSUPPORTED, "Bilinear interpolation error: Jonah df doesn't work for nonzero muB. Exiting..");
+  if (p->famod_chains < 0) return e->fail(IS3D_ERR_ARG, "famod_chains must be >= 0");
+  e->p = *p;
+  e->have_params = true;
+  e->tables_dirty = true;
+  return IS3D_OK;
+}
+
+extern "C" int is3d_set_species(is3d_engine* e, int n, const double* mass, const double* sign, const double* degeneracy,
+                                const double* baryon) {
+  if (!e || n <= 0 || !mass || !sign || !degeneracy || !baryon) return e ? e->fail(IS3D_ERR_ARG, "bad species arrays") : IS3D_ERR_ARG;
+  e->mass.assign(mass, mass + n); e->sign.assign(sign, sign + n); e->degen.assign(degeneracy, degeneracy + n);
+  e->baryon.assign(baryon, baryon + n);
+  e->order.resize(n);
+  for (int i = 0; i < n; i++) e->order[i] = i;
+  // lanes of a wavefront take consecutive species: sort by mass so that whole wavefronts hit the
+  // exp-underflow early-out together (output order is unchanged)
+  std::stable_sort(e->order.begin(), e->order.end(), [&](int a, int b) { return e->mass[a] < e->mass[b]; });
+  e->have_species = true;
+  e->tables_dirty = true;
+  return IS3D_OK;
+}
+
+extern "C" int is3d_set_pdg(is3d_engine* e, int n, const double* mass, const double* sign, const double* degeneracy,
+                            const double* baryon) {
+  if (!e || n <= 0 || !mass || !sign || !degeneracy || !baryon) return e ? e->fail(IS3D_ERR_ARG, "bad pdg arrays") : IS3D_ERR_ARG;
+  e->pdg_mass.assign(mass, mass + n); e->pdg_sign.assign(sign, sign + n); e->pdg_degen.assign(degeneracy, degeneracy + n);
+  e->pdg_baryon.assign(baryon, baryon + n);
+  e->have_pdg = true;
+  e->tables_dirty = true;
+  return IS3D_OK;
+}
+
+extern "C" int is3d_set_momentum_grid(is3d_engine* e, int npT, const double* pT, int nphi, const double* phi, int ny,
+                                      const double* y, int neta, const double* eta, const double* eta_weight) {
+  if (!e) return IS3D_ERR_ARG;
+  if (npT <= 0 || nphi <= 0 || !pT || !phi) return e->fail(IS3D_ERR_ARG, "empty pT/phi table");
+  e->pT.assign(pT, pT + npT); e->phi.assign(phi, phi + nphi);
+  e->y.assign(y ? y : pT, y ? y + std::max(ny, 0) : pT);
+  e->eta.assign(eta ? eta : pT, eta ? eta + std::max(neta, 0) : pT);
+  e->eta_w.assign(eta_weight ? eta_weight : pT, eta_weight ? eta_weight + std::max(neta, 0) : pT);
+  e->have_grid = true;
+  e->tables_dirty = true;
+  return IS3D_OK;
+}
+
+extern "C" int is3d_set_gauss_laguerre(is3d_engine* e, int alpha, int points, const double* roots, const double* weights) {
+  if (!e) return IS3D_ERR_ARG;
+  if (alpha < 3 || points <= 0 || !roots || !weights) return e->fail(IS3D_ERR_ARG, "Gauss-Laguerre table needs alpha >= 3");
+  e->gla_alpha = alpha; e->gla_pts = points;
+  e->gla_r.assign(roots, roots + (size_t)alpha * points);
+  e->gla_w.assign(weights, weights + (size_t)alpha * points);
+  e->have_gla = true;
+  e->tables_dirty = true;
+  return IS3D_OK;
+}
+
+extern "C" int is3d_set_df_tables(is3d_engine* e, int nT, int nmuB, const double* T, const double* muB,
+                                  const double* tables, double T_avg) {
+  if (!e) return IS3D_ERR_ARG;
+  if (nT < 3 || nmuB < 1 || !T || !muB || !tables) return e->fail(IS3D_ERR_ARG, "bad df coefficient tables");
+  e->nT = nT; e->nmuB = nmuB;
+  e->Tarr.assign(T, T + nT); e->muBarr.assign(muB, muB + nmuB);
+  e->tab.assign(tables, tables + (size_t)10 * nmuB * nT);
+  e->T_avg = T_avg;
+  e->have_df = true;
+  e->tables_dirty = true;
+  return IS3D_OK;
+}
+
+// Build the derived tables (splines, Jonah) and upload everything read-only to HBM.
+static int finalize_tables(is3d_engine* e) {
+  if (!e->have_params) return e->fail(IS3D_ERR_STATE, "is3d_set_params not called");
+  if (!e->have_species) return e->fail(IS3D_ERR_STATE, "is3d_set_species not called");
+  if (!e->have_grid) return e->fail(IS3D_ERR_STATE, "is3d_set_momentum_grid not called");
+  if (!e->have_df) return e->fail(IS3D_ERR_STATE, "is3d_set_df_tables not called");
+  const int mode = e->p.df_mode;
+  if ((mode == PTM || mode == PTB) && !e->have_gla) return e->fail(IS3D_ERR_STATE, "is3d_set_gauss_laguerre not called");
+  if ((mode == PTB || mode == PTMA) && !e->have_pdg) return e->fail(IS3D_ERR_STATE, "is3d_set_pdg not called");
+  if (e->p.dimension == 3 && e->y.empty()) return e->fail(IS3D_ERR_ARG, "dimension = 3 needs a y table");
+  if (e->p.dimension == 2 && e->eta.empty()) return e->fail(IS3D_ERR_ARG, "dimension = 2 needs an eta table");
+  if (!e->tables_dirty) return IS3D_OK;
+  HIPCHK(e, hipSetDevice(e->device));
+  const int nT = e->nT, nmuB_used = e->p.include_baryon ? e->nmuB : 1;
+  // --- delta-f blob: T | muB | tab | 7 x (y, c) | jonah x, l2, l2c, z, zc
+  std::vector<double> blob;
+  auto put = [&](const double* v, size_t n) { size_t off = blob.size(); blob.insert(blob.end(), v, v + n); return off; };
+  const size_t oT = put(e->Tarr.data(), nT);
+  const size_t omu = put(e->muBarr.data(), e->nmuB);
+  const size_t otab = put(e->tab.data(), e->tab.size());
+  size_t osy[NSPL] = {0}, osc[NSPL] = {0};
+  const int spl_col[NSPL] = {0, 2, 3, 5, 7, 8, 9};   // c0 c2 c3 F betabulk betaV betapi
+  if (!e->p.include_baryon) {
+    for (int k = 0; k < NSPL; k++) {
+      const double* yv = e->tab.data() + (size_t)spl_col[k] * e->nmuB * nT;   // muB row 0
+      std::vector<double> c;
+      if (!cspline_coeffs(e->Tarr.data(), yv, nT, c)) return e->fail(IS3D_ERR_ARG, "gsl: x values must be strictly increasing (T table)");
+      osy[k] = put(yv, nT);
+      osc[k] = put(c.data(), nT);
+    }
+  }
+  size_t ojx = 0, ojl = 0, ojlc = 0, ojz = 0, ojzc = 0;
+  int nj = 0;
+  if (!e->p.include_baryon && mode == PTB) {
+    const double* r2 = e->gla_r.data() + 2 * e->gla_pts;
+    const double* w2 = e->gla_w.data() + 2 * e->gla_pts;
+    jonah_table(e->T_avg, (int)e->pdg_mass.size(), e->pdg_mass.data(), e->pdg_degen.data(), e->pdg_sign.data(), r2, w2,
+                e->gla_pts, e->jl2, e->jz, e->jx, e->bp_max);
+    if (!cspline_coeffs(e->jx.data(), e->jl2.data(), 301, e->jl2c) || !cspline_coeffs(e->jx.data(), e->jz.data(), 301, e->jzc))
+      return e->fail(IS3D_ERR_DF_RANGE, "gsl: x values must be strictly increasing (Jonah bulkPi/P table)");
+    nj = 301;
+    ojx = put(e->jx.data(), 301); ojl = put(e->jl2.data(), 301); ojlc = put(e->jl2c.data(), 301);
+    ojz = put(e->jz.data(), 301); ojzc = put(e->jzc.data(), 301);
+  }
+  dfree(e->d_tables);
+  e->d_tables = dalloc<double>(blob.size());
+  if (!e->d_tables) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(tables) failed");
+  HIPCHK(e, hipMemcpy(e->d_tables, blob.data(), blob.size() * sizeof(double), hipMemcpyHostToDevice));
+  DfTables& tb = e->dtb;
+  tb.df_mode = mode; tb.include_baryon = e->p.include_baryon;
+  tb.nT = nT; tb.nmuB = nmuB_used;
+  tb.T = e->d_tables + oT; tb.muB = e->d_tables + omu; tb.tab = e->d_tables + otab;
+  tb.T_min = e->Tarr[0]; tb.muB_min = e->muBarr[0];
+  tb.dT = std::fabs(e->Tarr[1] - e->Tarr[0]);
+  tb.dmuB = e->nmuB > 1 ? std::fabs(e->muBarr[1] - e->muBarr[0]) : 0.0;
+  for (int k = 0; k < NSPL; k++) { tb.sy[k] = e->d_tables + osy[k]; tb.sc[k] = e->d_tables + osc[k]; }
+  tb.nj = nj; tb.jx = e->d_tables + ojx; tb.jl2 = e->d_tables + ojl; tb.jl2c = e->d_tables + ojlc;
+  tb.jz = e->d_tables + ojz; tb.jzc = e->d_tables + ojzc;
+  tb.bulk_over_P_max = e->bp_max;
+  // tab is laid out [10][nmuB][nT]; with include_baryon = 0 only muB row 0 is used (nmuB_used = 1)
+  // but the stride must stay the file's nmuB
+  if (!e->p.include_baryon) tb.nmuB = 1;
+  // --- constants blob: sorted species, original degeneracy, grids, gla, pdg
+  const int np = (int)e->mass.size();
+  std::vector<double> cb;
+  auto cput = [&](const double* v, size_t n) { size_t off = cb.size(); cb.insert(cb.end(), v, v + n); return off; };
+  std::vector<double> sm(np), ss(np), sb(np), sd(np);
+  for (int i = 0; i < np; i++) { const int o = e->order[i]; sm[i] = e->mass[o]; ss[i] = e->sign[o]; sb[i] = e->baryon[o]; sd[i] = e->degen[o]; }
+  const size_t osm = cput(sm.data(), np), oss = cput(ss.data(), np), osb = cput(sb.data(), np), osd = cput(sd.data(), np);
+  const size_t odg = cput(e->degen.data(), np);
+  const size_t opt = cput(e->pT.data(), e->pT.size());
+  std::vector<double> cph(e->phi.size()), sph(e->phi.size());
+  for (size_t j = 0; j < e->phi.size(); j++) { cph[j] = std::cos(e->phi[j]); sph[j] = std::sin(e->phi[j]); }
+  const size_t oc = cput(cph.data(), cph.size()), os = cput(sph.data(), sph.size());
+  const size_t oy = cput(e->y.data(), e->y.size()), oe = cput(e->eta.data(), e->eta.size()), ow = cput(e->eta_w.data(), e->eta_w.size());
+  const size_t og = cput(e->gla_r.data(), e->gla_r.size());
+  cput(e->gla_w.data(), e->gla_w.size());
+  const size_t opd = cput(e->pdg_mass.data(), e->pdg_mass.size());
+  cput(e->pdg_sign.data(), e->pdg_sign.size());
+  cput(e->pdg_degen.data(), e->pdg_degen.size());
+  std::vector<double> sorig(np);
+  dfree(e->d_const);
+  const size_t nconst = cb.size() + np;   // ints appended as raw space
+  e->d_const = dalloc<double>(nconst);
+  if (!e->d_const) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(constants) failed");
+  HIPCHK(e, hipMemcpy(e->d_const, cb.data(), cb.size() * sizeof(double), hipMemcpyHostToDevice));
+  std::vector<int> so(np);
+  for (int i = 0; i < np; i++) so[i] = e->order[i];
+  e->d_sorig = (int*)(e->d_const + cb.size());
+  HIPCHK(e, hipMemcpy(e->d_sorig, so.data(), np * sizeof(int), hipMemcpyHostToDevice));
+  e->d_smass = e->d_const + osm; e->d_ssign = e->d_const + oss; e->d_sbaryon = e->d_const + osb; e->d_sdegen = e->d_const + osd;
+  e->d_degen_orig = e->d_const + odg; e->d_pT = e->d_const + opt; e->d_cphi = e->d_const + oc; e->d_sphi = e->d_const + os;
+  e->d_y = e->d_const + oy; e->d_eta = e->d_const + oe; e->d_etaw = e->d_const + ow;
+  e->d_gla = e->d_const + og; e->d_pdg = e->d_const + opd;
+  e->tables_dirty = false;
+  return IS3D_OK;
+}
+
+extern "C" int is3d_set_surface(is3d_engine* e, long n, const is3d_surface* s) {
+  if (!e || !s || n < 0) return e ? e->fail(IS3D_ERR_ARG, "bad surface") : IS3D_ERR_ARG;
+  HIPCHK(e, hipSetDevice(e->device));
+  const double* fields[NSURF] = {s->tau, s->x, s->y, s->eta, s->dat, s->dax, s->day, s->dan, s->ux, s->uy, s->un,
+                                 s->E, s->T, s->P, s->pixx, s->pixy, s->pixn, s->piyy, s->piyn, s->bulkPi,
+                                 s->muB, s->nB, s->Vx, s->Vy, s->Vn};
+  for (int f = 0; f < S_MUB; f++)
+    if (!fields[f] && n > 0) return e->fail(IS3D_ERR_ARG, "surface field missing");
+  if (!e->surf_owned || e->surf_cap < n) {
+    if (e->surf_owned) dfree(e->d_surf);
+    e->d_surf = dalloc<double>((size_t)NSURF * std::max(n, 1L));
+    if (!e->d_surf) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(surface) failed");
+    e->surf_owned = true;
+    e->surf_cap = n;
+  }
+  e->ncell = n;
+  if (n == 0) return IS3D_OK;
+  for (int f = 0; f < NSURF; f++) {
+    double* dst = e->d_surf + (size_t)f * n;
+    if (fields[f]) HIPCHK(e, hipMemcpy(dst, fields[f], n * sizeof(double), hipMemcpyHostToDevice));
+    else HIPCHK(e, hipMemset(dst, 0, n * sizeof(double)));
+  }
+  return IS3D_OK;
+}
+
+extern "C" int is3d_set_surface_device(is3d_engine* e, long n, const double* dev_fields) {
+  if (!e || n < 0 || (!dev_fields && n > 0)) return e ? e->fail(IS3D_ERR_ARG, "bad device surface") : IS3D_ERR_ARG;
+  if (e->surf_owned) dfree(e->d_surf);
+  e->surf_owned = false;
+  e->surf_cap = 0;
+  e->d_surf = const_cast<double*>(dev_fields);
+  e->ncell = n;
+  return IS3D_OK;
+}
+
+extern "C" long is3d_output_size(const is3d_engine* e) {
+  if (!e || !e->have_species || !e->have_grid || !e->have_params) return -1;
+  const long ny = (e->p.dimension == 3) ? (long)e->y.size() : 1;
+  return (long)e->mass.size() * (long)e->pT.size() * (long)e->phi.size() * ny;
+}
+
+template <class T>
+static bool ensure(T*& p, long& cap, long need) {
+  if (cap >= need && p) return true;
+  dfree(p);
+  p = dalloc<T>((size_t)std::max(need, 1L));
+  cap = p ? need : 0;
+  return p != nullptr;
+}
+
+static PrepConsts make_consts(const is3d_engine* e) {
+  PrepConsts k{};
+  k.df_mode = e->p.df_mode; k.dim = e->p.dimension; k.include_baryon = e->p.include_baryon;
+  k.include_bulk = e->p.include_bulk_deltaf; k.include_shear = e->p.include_shear_deltaf;
+  k.include_diff = e->p.include_baryondiff_deltaf;
+  k.deta_min = e->p.deta_min; k.mass_pion0 = e->p.mass_pion0;
+  k.gla_pts = e->gla_pts;
+  if (e->have_gla) {
+    k.gla_r1 = e->d_gla + 1 * e->gla_pts; k.gla_r2 = e->d_gla + 2 * e->gla_pts;
+    const double* w = e->d_gla + (size_t)e->gla_alpha * e->gla_pts;
+    k.gla_w1 = w + 1 * e->gla_pts; k.gla_w2 = w + 2 * e->gla_pts;
+  }
+  k.two_pi2_hbarC3 = 2.0 * std::pow(M_PI, 2) * std::pow(kHbarC, 3);
+  return k;
+}
+
+template <int MODE>
+static void launch_spectra(dim3 grid, size_t shmem, hipStream_t st, const SpecArgs& a) {
+  hipLaunchKernelGGL(k_spectra<MODE>, grid, dim3(kBlock), shmem, st, a);
+}
+
+extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
+  if (!e) return IS3D_ERR_ARG;
+  int rc = finalize_tables(e);
+  if (rc) return rc;
+  if (!dev_out) return e->fail(IS3D_ERR_ARG, "null output buffer");
+  HIPCHK(e, hipSetDevice(e->device));
+  hipStream_t st = (hipStream_t)stream;
+  const long n = e->ncell;
+  const int mode = e->p.df_mode, dim = e->p.dimension;
+  const long outsize = is3d_output_size(e);
+  const int np = (int)e->mass.size(), npT = (int)e->pT.size(), nphi = (int)e->phi.size();
+  const int ny_out = (dim == 3) ? (int)e->y.size() : 1;
+  const int nk = ny_out, nl = (dim == 3) ? 1 : (int)e->eta.size();
+  e->st = is3d_stats{};
+  e->st.cells = n;
+  HIPCHK(e, hipMemsetAsync(e->d_err, 0, sizeof(int), st));
+  HIPCHK(e, hipMemsetAsync(e->d_cnt, 0, 8 * sizeof(unsigned long long), st));
+  HIPCHK(e, hipEventRecord(e->ev[0], st));
+  if (n == 0) {
+    HIPCHK(e, hipMemsetAsync(dev_out, 0, outsize * sizeof(double), st));
+    HIPCHK(e, hipEventRecord(e->ev[1], st));
+    HIPCHK(e, hipEventRecord(e->ev[2], st));
+    HIPCHK(e, hipEventRecord(e->ev[3], st));
+    e->launched = true;
+    return IS3D_OK;
+  }
+  if (!ensure(e->d_rec, e->rec_cap, (long)NREC * n)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(records) failed");
+  if (!ensure(e->d_aux, e->aux_cap, 9L * n)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(aux) failed");
+  if (mode == PTMA && !ensure(e->d_sol, e->sol_cap, 6L * n)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(sol) failed");
+  PrepArgs pa{};
+  pa.k = make_consts(e); pa.tb = e->dtb; pa.surf = e->d_surf; pa.rec = e->d_rec; pa.aux = e->d_aux; pa.n = n;
+  pa.err = e->d_err; pa.cnt = e->d_cnt;
+  const dim3 g1((unsigned)((n + 255) / 256)), b1(256);
+  switch (mode) {
+    case GRAD: hipLaunchKernelGGL(k_prep<GRAD>, g1, b1, 0, st, pa); break;
+    case CE: hipLaunchKernelGGL(k_prep<CE>, g1, b1, 0, st, pa); break;
+    case PTM: hipLaunchKernelGGL(k_prep<PTM>, g1, b1, 0, st, pa); break;
+    case PTB: hipLaunchKernelGGL(k_prep<PTB>, g1, b1, 0, st, pa); break;
+    default: hipLaunchKernelGGL(k_prep<PTMA>, g1, b1, 0, st, pa); break;
+  }
+  HIPCHK(e, hipGetLastError());
+  if (mode == PTMA) {
+    AnisoArgs aa{};
+    aa.rec = e->d_rec; aa.ain = e->d_aux; aa.sol = e->d_sol; aa.n = n;
+    aa.chains = (e->p.famod_chains > 0) ? std::min<long>(e->p.famod_chains, n) : n;
+    const int nh = std::min(320, (int)e->pdg_mass.size());
+    aa.h = Hadrons{nh, e->d_pdg, e->d_pdg + e->pdg_mass.size(), e->d_pdg + 2 * e->pdg_mass.size()};
+    aa.fp2 = 4.0 * std::pow(M_PI, 2) * std::pow(kHbarC, 3);
+    aa.cnt = e->d_cnt;
+    hipLaunchKernelGGL(k_aniso, dim3((unsigned)aa.chains), dim3(64), 0, st, aa);
+    HIPCHK(e, hipGetLastError());
+    hipLaunchKernelGGL(k_famod_b, g1, b1, 0, st, pa, (const double*)e->d_sol);
+    HIPCHK(e, hipGetLastError());
+  }
+  if (mode == PTM) {
+    if (!ensure(e->d_renorm, e->renorm_cap, n * (long)np)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(renorm) failed");
+    RenormArgs ra{};
+    ra.k = pa.k; ra.rec = e->d_rec; ra.aux = e->d_aux; ra.renorm = e->d_renorm;
+    ra.mass = e->d_smass; ra.sign = e->d_ssign; ra.degen = e->d_sdegen; ra.baryon = e->d_sbaryon; ra.n = n; ra.npart = np;
+    const long tot = n * (long)np;
+    hipLaunchKernelGGL(k_renorm, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, ra);
+    HIPCHK(e, hipGetLastError());
+  }
+  HIPCHK(e, hipEventRecord(e->ev[1], st));
+  // --- main integral
+  const int njb = (nphi + kJmax - 1) / kJmax;
+  const long ntask = (long)np * nk * njb;
+  const long bx = (ntask + kBlock - 1) / kBlock;
+  const long wgs = bx * npT;
+  const long target = 8192;
+  const long max_split = (n + kTile - 1) / kTile;
+  long nsplit = std::max(1L, std::min(max_split, (target + wgs - 1) / wgs));
+  long cps = (n + nsplit - 1) / nsplit;
+  cps = ((cps + kTile - 1) / kTile) * kTile;
+  nsplit = (n + cps - 1) / cps;
+  if (!ensure(e->d_slab, e->slab_cap, nsplit * outsize)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(slabs) failed");
+  SpecArgs sa{};
+  sa.rec = e->d_rec; sa.n = n; sa.renorm = e->d_renorm; sa.slab = e->d_slab; sa.outsize = outsize;
+  sa.smass = e->d_smass; sa.ssign = e->d_ssign; sa.sbaryon = e->d_sbaryon; sa.sorig = e->d_sorig;
+  sa.pT = e->d_pT; sa.cphi = e->d_cphi; sa.sphi = e->d_sphi; sa.yv = e->d_y; sa.etav = e->d_eta; sa.etaw = e->d_etaw;
+  sa.npart = np; sa.npT = npT; sa.nphi = nphi; sa.ny_out = ny_out; sa.nk = nk; sa.nl = nl; sa.nq = nk * nl; sa.njb = njb;
+  sa.ntask = ntask; sa.cells_per_split = cps;
+  sa.regulate = e->p.regulate_deltaf; sa.outflow = e->p.outflow; sa.dim = dim;
+  const size_t shmem = sizeof(double) * ((size_t)kTile * NREC + (size_t)kTile * nphi * NPT + (size_t)kTile * sa.nq * NYT);
+  if (shmem > 160 * 1024) return e->fail(IS3D_ERR_ARG, "momentum grid too large for the LDS tile");
+  const dim3 grid((unsigned)bx, (unsigned)npT, (unsigned)nsplit);
+  switch (mode) {
+    case GRAD: launch_spectra<GRAD>(grid, shmem, st, sa); break;
+    case CE: launch_spectra<CE>(grid, shmem, st, sa); break;
+    case PTM: launch_spectra<PTM>(grid, shmem, st, sa); break;
+    case PTB: launch_spectra<PTB>(grid, shmem, st, sa); break;
+    default: launch_spectra<PTMA>(grid, shmem, st, sa); break;
+  }
+  HIPCHK(e, hipGetLastError());
+  HIPCHK(e, hipEventRecord(e->ev[2], st));
+  const double prefactor = std::pow(2.0 * M_PI * kHbarC, -3);
+  const long per_species = (long)npT * nphi * ny_out;
+  hipLaunchKernelGGL(k_reduce, dim3((unsigned)((outsize + 255) / 256)), dim3(256), 0, st, (const double*)e->d_slab, outsize,
+                     (int)nsplit, e->d_degen_orig, per_species, prefactor, dev_out);
+  HIPCHK(e, hipGetLastError());
+  HIPCHK(e, hipEventRecord(e->ev[3], st));
+  e->launched = true;
+  return IS3D_OK;
+}
+
+extern "C" int is3d_finish(is3d_engine* e) {
+  if (!e) return IS3D_ERR_ARG;
+  if (!e->launched) return e->fail(IS3D_ERR_STATE, "nothing launched");
+  HIPCHK(e, hipSetDevice(e->device));
+  HIPCHK(e, hipEventSynchronize(e->ev[3]));
+  e->launched = false;
+  int derr = 0;
+  unsigned long long cnt[8];
+  HIPCHK(e, hipMemcpy(&derr, e->d_err, sizeof(int), hipMemcpyDeviceToHost));
+  HIPCHK(e, hipMemcpy(cnt, e->d_cnt, sizeof(cnt), hipMemcpyDeviceToHost));
+  e->st.breakdown = (long)cnt[0]; e->st.pl_negative = (long)cnt[1]; e->st.recon_fail = (long)cnt[2]; e->st.iterations = (long)cnt[3];
+  float ms = 0.f;
+  if (hipEventElapsedTime(&ms, e->ev[0], e->ev[1]) == hipSuccess) e->st.ms_prepass = ms;
+  if (hipEventElapsedTime(&ms, e->ev[1], e->ev[2]) == hipSuccess) e->st.ms_spectra = ms;
+  if (hipEventElapsedTime(&ms, e->ev[0], e->ev[3]) == hipSuccess) e->st.ms_total = ms;
+  switch (derr) {
+    case DF_OK: return IS3D_OK;
+    case DF_SPLINE_RANGE: return e->fail(IS3D_ERR_DF_RANGE, "gsl: interp.c: interpolation error (df coefficient spline evaluated outside its table)");
+    case DF_TABLE_RANGE: return e->fail(IS3D_ERR_DF_RANGE, "Error: (T,muB) outside df coefficient table. Exiting...");
+    case DF_PTB_BARYON: return e->fail(IS3D_ERR_UNSUPPORTED, "Bilinear interpolation error: Jonah df doesn't work for nonzero muB. Exiting..");
+    default: return e->fail(IS3D_ERR_ARG, "Error: choose df_mode = (1,2,3,4,5)");
+  }
+}
+
+extern "C" int is3d_calculate_spectra(is3d_engine* e, double* dN_out) {
+  if (!e || !dN_out) return e ? e->fail(IS3D_ERR_ARG, "null output") : IS3D_ERR_ARG;
+  int rc = finalize_tables(e);
+  if (rc) return rc;
+  const long outsize = is3d_output_size(e);
+  if (!ensure(e->d_out, e->out_cap, outsize)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(output) failed");
+  rc = is3d_launch(e, e->d_out, nullptr);
+  if (rc) return rc;
+  rc = is3d_finish(e);
+  if (rc) return rc;
+  HIPCHK(e, hipMemcpy(dN_out, e->d_out, outsize * sizeof(double), hipMemcpyDeviceToHost));
+  return IS3D_OK;
+}
+
+extern "C" int is3d_get_stats(const is3d_engine* e, is3d_stats* out) {
+  if (!e || !out) return IS3D_ERR_ARG;
+  *out = e->st;
+  return IS3D_OK;
+}
+
+extern "C" int is3d_evaluate_df_coefficients(is3d_engine* e, double T, double muB, double E, double P, double bulkPi,
+                                             double* out15) {
+  if (!e || !out15) return IS3D_ERR_ARG;
+  int rc = finalize_tables(e);
+  if (rc) return rc;
+  HIPCHK(e, hipSetDevice(e->device));
+  double* d = dalloc<double>(16);
+  if (!d) return e->fail(IS3D_ERR_DEVICE, "hipMalloc failed");
+  hipLaunchKernelGGL(k_df_eval, dim3(1), dim3(1), 0, 0, e->dtb, T, muB, E, P, bulkPi, d, (int*)(d + 15));
+  hipError_t h = hipDeviceSynchronize();
+  int derr = 0;
+  if (h == hipSuccess) h = hipMemcpy(out15, d, 15 * sizeof(double), hipMemcpyDeviceToHost);
+  if (h == hipSuccess) h = hipMemcpy(&derr, d + 15, sizeof(int), hipMemcpyDeviceToHost);
+  dfree(d);
+  if (h != hipSuccess) return hip_fail(e, h, "df eval");
+  if (derr == DF_SPLINE_RANGE || derr == DF_TABLE_RANGE) return e->fail(IS3D_ERR_DF_RANGE, "df coefficient evaluated out of range");
+  if (derr) return e->fail(IS3D_ERR_ARG, "df coefficient error");
+  return IS3D_OK;
+}
+
+extern "C" int is3d_get_jonah_table(const is3d_engine* e, double* l2, double* z, double* bp, double* bpmax) {
+  if (!e || e->jx.size() != 301) return IS3D_ERR_STATE;
+  std::copy(e->jl2.begin(), e->jl2.end(), l2);
+  std::copy(e->jz.begin(), e->jz.end(), z);
+  std::copy(e->jx.begin(), e->jx.end(), bp);
+  *bpmax = e->bp_max;
+  return IS3D_OK;
+}
+
+extern "C" int is3d_surface_averages(long n, const is3d_surface* s, int include_baryon, double* out) {
+  if (!s || !out || n <= 0) return IS3D_ERR_ARG;
+  double T_avg = 0, E_avg = 0, P_avg = 0, muB_avg = 0, nB_avg = 0, vol = 0;
+  for (long i = 0; i < n; i++) {
+    const double tau = s->tau[i], tau2 = tau * tau, ux = s->ux[i], uy = s->uy[i], un = s->un[i];
+    const double ut = std::sqrt(1. + ux * ux + uy * uy + tau2 * un * un);
+    const double dat = s->dat[i], dax = s->dax[i], day = s->day[i], dan = s->dan[i];
+    const double uds = ut * dat + ux * dax + uy * day + un * dan;
+    const double ds_ds = dat * dat - dax * dax - day * day - dan * dan / tau2;
+    const double ds_max = std::fabs(uds) + std::sqrt(std::fabs(uds * uds - ds_ds));
+    const double muB = (include_baryon && s->muB) ? s->muB[i] : 0.0;
+    const double nB = (include_baryon && s->nB) ? s->nB[i] : 0.0;
+    vol += ds_max;
+    E_avg += (s->E[i] * ds_max); T_avg += (s->T[i] * ds_max); P_avg += (s->P[i] * ds_max);
+    muB_avg += (muB * ds_max); nB_avg += (nB * ds_max);
+  }
+  const double v[5] = {T_avg / vol, E_avg / vol, P_avg / vol, muB_avg / vol, nB_avg / vol};
+  for (int k = 0; k < 5; k++) {   // ofstream << setprecision(15) then fscanf %lf (readindata.cpp:364-366, :104-119)
+    char buf[64];
+    std::snprintf(buf, sizeof(buf), "%.15g", v[k]);
+    out[k] = std::strtod(buf, nullptr);
+  }
+  return IS3D_OK;
+}

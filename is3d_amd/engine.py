@@ -1,0 +1,188 @@
+"""Python host binding of the MI355X engine, shaped like the reference's plug-in
+surface for operation = 1:
+
+  EmissionFunctionArray(params, chosen species, pT/phi/y/eta tables, PDG, FO surface, Deltaf_Data)
+      -> calculate_spectra()  ->  dN/(pT dpT dphi dy)[species][pT][phi][y]
+
+(EmissionFunction.h:135-140, EmissionFunction.cpp:114-391, 981-1231).  Every call goes
+through libis3d_amd.so; there is no CPU fallback.
+"""
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from . import data as _data
+from . import hrg as _hrg
+
+_DEFAULTS = dict(operation=1, dimension=2, df_mode=1, include_baryon=0, include_bulk_deltaf=1,
+                 include_shear_deltaf=1, include_baryondiff_deltaf=0, regulate_deltaf=0, outflow=0,
+                 famod_chains=0, deta_min=1.e-5, mass_pion0=0.138)
+
+
+def _dp(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def _arr(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+class IS3DError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("is3d error %d: %s" % (code, msg))
+        self.code = code
+
+
+class Engine:
+    """One engine per GPU (device index in the current process's visible devices)."""
+
+    def __init__(self, device=0):
+        self.lib = _lib.load()
+        self._e = self.lib.is3d_create(int(device))
+        if not self._e:
+            raise IS3DError(_lib.IS3D_ERR_DEVICE, "is3d_create(%d) failed (no HIP device?)" % device)
+        self._keep = []
+
+    def close(self):
+        if getattr(self, "_e", None):
+            self.lib.is3d_destroy(self._e)
+            self._e = None
+
+    def __del__(self):
+        self.close()
+
+    def _chk(self, rc):
+        if rc != 0:
+            raise IS3DError(rc, self.lib.is3d_last_error(self._e).decode())
+        return rc
+
+    # --- setup, mirroring the reference services --------------------------------------
+    def set_params(self, **kw):
+        p = dict(_DEFAULTS)
+        p.update({k: v for k, v in kw.items() if k in _DEFAULTS})
+        self.params = p
+        self._chk(self.lib.is3d_set_params(self._e, C.byref(_lib.Params(**p))))
+
+    def set_species(self, mass, sign, degen, baryon):
+        a = [_arr(x) for x in (mass, sign, degen, baryon)]
+        self._chk(self.lib.is3d_set_species(self._e, len(a[0]), *[_dp(x) for x in a]))
+        self.npart = len(a[0])
+
+    def set_pdg(self, mass, sign, degen, baryon):
+        a = [_arr(x) for x in (mass, sign, degen, baryon)]
+        self._chk(self.lib.is3d_set_pdg(self._e, len(a[0]), *[_dp(x) for x in a]))
+
+    def set_momentum_grid(self, pT, phi, y, eta, eta_w):
+        a = [_arr(x) for x in (pT, phi, y, eta, eta_w)]
+        self._chk(self.lib.is3d_set_momentum_grid(self._e, len(a[0]), _dp(a[0]), len(a[1]), _dp(a[1]),
+                                                  len(a[2]), _dp(a[2]), len(a[3]), _dp(a[3]), _dp(a[4])))
+
+    def set_gauss_laguerre(self, roots, weights):
+        r, w = _arr(roots), _arr(weights)
+        self._chk(self.lib.is3d_set_gauss_laguerre(self._e, r.shape[0], r.shape[1], _dp(r), _dp(w)))
+
+    def set_df_tables(self, T, muB, tab, T_avg):
+        T, muB, tab = _arr(T), _arr(muB), _arr(tab)
+        self._chk(self.lib.is3d_set_df_tables(self._e, len(T), len(muB), _dp(T), _dp(muB), _dp(tab), float(T_avg)))
+
+    def set_surface(self, surf):
+        cols = [_arr(surf[k]) if surf.get(k) is not None else None for k in _lib.SURFACE_FIELDS]
+        n = len(cols[0])
+        self._keep = cols
+        s = _lib.Surface(*[(_dp(c) if c is not None else C.POINTER(C.c_double)()) for c in cols])
+        self._chk(self.lib.is3d_set_surface(self._e, n, C.byref(s)))
+        self.ncell = n
+
+    def set_surface_device(self, ptr, n):
+        self._chk(self.lib.is3d_set_surface_device(self._e, int(n), C.c_void_p(ptr)))
+        self.ncell = n
+
+    # --- compute -----------------------------------------------------------------------
+    def output_size(self):
+        return self.lib.is3d_output_size(self._e)
+
+    def calculate_spectra(self):
+        out = np.zeros(self.output_size(), dtype=np.float64)
+        self._chk(self.lib.is3d_calculate_spectra(self._e, _dp(out)))
+        return out
+
+    def launch(self, dev_out_ptr, stream_ptr=None):
+        self._chk(self.lib.is3d_launch(self._e, C.c_void_p(dev_out_ptr), C.c_void_p(stream_ptr or 0)))
+
+    def finish(self):
+        self._chk(self.lib.is3d_finish(self._e))
+
+    def stats(self):
+        s = _lib.Stats()
+        self._chk(self.lib.is3d_get_stats(self._e, C.byref(s)))
+        return {k: getattr(s, k) for k, _ in s._fields_}
+
+    def evaluate_df_coefficients(self, T, muB, E, P, bulkPi):
+        out = np.zeros(15)
+        self._chk(self.lib.is3d_evaluate_df_coefficients(self._e, T, muB, E, P, bulkPi, _dp(out)))
+        return out
+
+    def jonah_table(self):
+        l2, z, bp, mx = np.zeros(301), np.zeros(301), np.zeros(301), np.zeros(1)
+        self._chk(self.lib.is3d_get_jonah_table(self._e, _dp(l2), _dp(z), _dp(bp), _dp(mx)))
+        return l2, z, bp, mx[0]
+
+
+def surface_averages(surf, include_baryon=0):
+    """Plasma averages (T, E, P, muB, nB) after the reference's setprecision(15) file round trip."""
+    lib = _lib.load()
+    cols = [_arr(surf[k]) if surf.get(k) is not None else None for k in _lib.SURFACE_FIELDS]
+    s = _lib.Surface(*[(_dp(c) if c is not None else C.POINTER(C.c_double)()) for c in cols])
+    out = np.zeros(5)
+    rc = lib.is3d_surface_averages(len(cols[0]), C.byref(s), int(include_baryon), _dp(out))
+    if rc:
+        raise IS3DError(rc, "surface averages")
+    return out
+
+
+# ------------------------------------------------------------------------------------------
+# run specifications (inputs shared by the engine, the oracle and the bench)
+# ------------------------------------------------------------------------------------------
+def make_spec(hrg_eos=2, chosen="pikp", pT="pT24", phi="phi24", y="y21", eta="eta24", dimension=2, df_mode=1,
+              gla_points=32, **flags):
+    """Everything calculate_spectra needs except the surface: parameters, species, grids,
+    Gauss-Laguerre table, delta-f tables.  `chosen` is a key of PDG/chosen_particles_*.dat
+    ('pikp', 'smash', 'urqmd', 'box', 'default') or an explicit MCID list."""
+    parts = _hrg.pdg_particles(hrg_eos)
+    mcids = _hrg.chosen_mcids(chosen) if isinstance(chosen, str) else np.asarray(chosen, dtype=np.int64)
+    sp = _hrg.chosen_species(parts, mcids)
+    pTv, _ = _data.grid(pT)
+    phiv, _ = _data.grid(phi)
+    yv, _ = _data.grid(y)
+    etav, etaw = _data.grid(eta)
+    roots, weights = _data.gauss_laguerre(gla_points)
+    T, muB, tab = _data.df_tables(hrg_eos)
+    params = dict(_DEFAULTS)
+    params.update(dimension=dimension, df_mode=df_mode)
+    params.update({k: v for k, v in flags.items() if k in _DEFAULTS})
+    return dict(params=params, species=sp, pdg=parts, pT=pTv, phi=phiv, y=yv, eta=etav, eta_w=etaw,
+                gla=(roots, weights), df=(T, muB, tab), hrg_eos=hrg_eos)
+
+
+def build_engine(spec, surf, T_avg=None, device=0):
+    e = Engine(device)
+    p = spec["params"]
+    e.set_params(**p)
+    sp = spec["species"]
+    e.set_species(sp["mass"], sp["sign"], sp["degen"], sp["baryon"])
+    pdg = spec["pdg"]
+    e.set_pdg(pdg["mass"], pdg["sign"], pdg["gspin"], pdg["baryon"])
+    e.set_momentum_grid(spec["pT"], spec["phi"], spec["y"], spec["eta"], spec["eta_w"])
+    e.set_gauss_laguerre(*spec["gla"])
+    if T_avg is None:
+        T_avg = surface_averages(surf, p["include_baryon"])[0]
+    e.set_df_tables(*spec["df"], T_avg)
+    if surf is not None:
+        e.set_surface(surf)
+    return e
+
+
+def output_shape(spec):
+    ny = len(spec["y"]) if spec["params"]["dimension"] == 3 else 1
+    return (len(spec["species"]["mass"]), len(spec["pT"]), len(spec["phi"]), ny)

@@ -1,0 +1,161 @@
+// cf_emulator.cpp -- TEST INFRASTRUCTURE ONLY.
+//
+// Runs the engine's device math (is3d_amd/csrc/cf_math.h, aniso_math.h) serially on
+// the host, in the same order of operations per lane as k_spectra, so the
+// factorised integrand can be checked against the oracle in the CPU test tier.
+// It is never linked into the product and is not a fallback: the product path
+// (libis3d_amd.so) has no host implementation of the kernels.
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "../../is3d_amd/csrc/aniso_math.h"
+#include "../../is3d_amd/csrc/cf_math.h"
+#include "../../is3d_amd/csrc/spline_host.h"
+#include "../../oracle/is3d_oracle.h"
+
+using namespace is3d;
+
+extern "C" int emu_spectra(const orc_params* p, const orc_setup* su, const orc_surface* S, int chains, double* out,
+                           long* stats) {
+  const int mode = p->df_mode, dim = p->dimension;
+  const long n = S->n;
+  const int np = su->npart, npT = su->npT, nphi = su->nphi;
+  const int ny_out = (dim == 3) ? su->ny : 1, nk = ny_out, nl = (dim == 3) ? 1 : su->neta;
+  // --- tables (as finalize_tables)
+  DfTables tb{};
+  tb.df_mode = mode; tb.include_baryon = p->include_baryon;
+  tb.nT = su->nT; tb.nmuB = p->include_baryon ? su->nmuB : 1;
+  tb.T = su->Tarr; tb.muB = su->muBarr; tb.tab = su->dftab;
+  tb.T_min = su->Tarr[0]; tb.muB_min = su->muBarr[0];
+  tb.dT = fabs(su->Tarr[1] - su->Tarr[0]);
+  tb.dmuB = su->nmuB > 1 ? fabs(su->muBarr[1] - su->muBarr[0]) : 0.0;
+  std::vector<std::vector<double>> sy(NSPL), sc(NSPL);
+  const int col[NSPL] = {0, 2, 3, 5, 7, 8, 9};
+  if (!p->include_baryon) {
+    for (int k = 0; k < NSPL; k++) {
+      const double* yv = su->dftab + (size_t)col[k] * su->nmuB * su->nT;
+      sy[k].assign(yv, yv + su->nT);
+      cspline_coeffs(su->Tarr, yv, su->nT, sc[k]);
+      tb.sy[k] = sy[k].data(); tb.sc[k] = sc[k].data();
+    }
+  }
+  std::vector<double> jl2, jz, jx, jl2c, jzc;
+  double bpmax = -1.0;
+  if (!p->include_baryon && mode == PTB) {
+    jonah_table(su->T_avg, su->npdg, su->pdg_mass, su->pdg_degen, su->pdg_sign, su->gla_root + 2 * su->gla_points,
+                su->gla_weight + 2 * su->gla_points, su->gla_points, jl2, jz, jx, bpmax);
+    cspline_coeffs(jx.data(), jl2.data(), 301, jl2c);
+    cspline_coeffs(jx.data(), jz.data(), 301, jzc);
+    tb.nj = 301; tb.jx = jx.data(); tb.jl2 = jl2.data(); tb.jl2c = jl2c.data(); tb.jz = jz.data(); tb.jzc = jzc.data();
+  }
+  tb.bulk_over_P_max = bpmax;
+  PrepConsts k{};
+  k.df_mode = mode; k.dim = dim; k.include_baryon = p->include_baryon; k.include_bulk = p->include_bulk_deltaf;
+  k.include_shear = p->include_shear_deltaf; k.include_diff = p->include_baryondiff_deltaf;
+  k.deta_min = p->deta_min; k.mass_pion0 = p->mass_pion0; k.gla_pts = su->gla_points;
+  k.gla_r1 = su->gla_root + su->gla_points; k.gla_r2 = su->gla_root + 2 * su->gla_points;
+  k.gla_w1 = su->gla_weight + su->gla_points; k.gla_w2 = su->gla_weight + 2 * su->gla_points;
+  k.two_pi2_hbarC3 = 2.0 * pow(M_PI, 2) * pow(kHbarC, 3);
+  // --- prepass
+  std::vector<double> rec((size_t)n * NREC), aux((size_t)n * 9), sol((size_t)n * 6);
+  const double* fields[NSURF] = {S->tau, S->x, S->y, S->eta, S->dat, S->dax, S->day, S->dan, S->ux, S->uy, S->un,
+                                 S->E, S->T, S->P, S->pixx, S->pixy, S->pixn, S->piyy, S->piyn, S->bulkPi,
+                                 S->muB, S->nB, S->Vx, S->Vy, S->Vn};
+  long st_break = 0, st_pl = 0, st_fail = 0, st_it = 0;
+  for (long c = 0; c < n; c++) {
+    double s[NSURF];
+    for (int f = 0; f < NSURF; f++) s[f] = fields[f] ? fields[f][c] : 0.0;
+    double* R = &rec[(size_t)c * NREC];
+    int err = 0;
+    if (mode <= CE) err = prep_grad_ce(k, tb, s, R);
+    else if (mode <= PTB) {
+      int flags[2];
+      err = prep_feqmod(k, tb, s, R, &aux[(size_t)c * 9], flags);
+      if (!err) { st_break += (flags[0] && R[R_KIND] != 0.0); st_pl += flags[1]; }
+    } else prep_famod_a(k, s, R, &aux[(size_t)c * 9]);
+    if (err) return 100 + err;
+  }
+  if (mode == PTMA) {
+    const int nh = su->npdg < 320 ? su->npdg : 320;
+    Hadrons h{nh, su->pdg_mass, su->pdg_sign, su->pdg_degen};
+    const double fp2 = 4.0 * pow(M_PI, 2) * pow(kHbarC, 3);
+    auto id = [](double v) { return v; };
+    const long C = (chains > 0) ? (chains < n ? chains : n) : n;
+    for (long ch = 0; ch < C; ch++) {
+      double state[4] = {0, 0, 0, 0};
+      long cnt[3] = {0, 0, 0};
+      for (long c = ch; c < n; c += C) {
+        if (rec[(size_t)c * NREC + R_KIND] == 0.0) continue;
+        aniso_cell(&aux[(size_t)c * 9], h, 0, 1, id, fp2, state, &sol[(size_t)c * 6], cnt);
+      }
+      st_pl += cnt[0]; st_fail += cnt[1]; st_it += cnt[2];
+    }
+    for (long c = 0; c < n; c++) {
+      double* R = &rec[(size_t)c * NREC];
+      if (R[R_KIND] == 0.0) continue;
+      int broken = 0;
+      prep_famod_b(k, R, &aux[(size_t)c * 9], &sol[(size_t)c * 6], &broken);
+      st_break += broken;
+    }
+  }
+  // --- spectra (same per-lane order as k_spectra: cells ascending, then l, then phi)
+  const double prefactor = pow(2.0 * M_PI * kHbarC, -3);
+  std::vector<double> cph(nphi), sph(nphi);
+  for (int j = 0; j < nphi; j++) { cph[j] = cos(su->phi[j]); sph[j] = sin(su->phi[j]); }
+  const int nq = nk * nl;
+  std::vector<double> Yall((size_t)nq * NYT), PHall((size_t)nphi * NPT);
+  std::vector<double> acc((size_t)np * nk * nphi);
+  for (int i = 0; i < npT; i++) {
+    const double pT = su->pT[i];
+    std::fill(acc.begin(), acc.end(), 0.0);
+    for (long c = 0; c < n; c++) {
+      const double* R = &rec[(size_t)c * NREC];
+      const double kind = R[R_KIND];
+      if (kind == 0.0) continue;
+      for (int j = 0; j < nphi; j++) phiterms(mode, R, pT, cph[j], sph[j], &PHall[(size_t)j * NPT]);
+      for (int q = 0; q < nq; q++) {
+        const int kk = q / nl, l = q % nl;
+        const double y = (dim == 3) ? su->y[kk] : 0.0;
+        const double eta = (dim == 3) ? R[R_ETA] : su->eta[l];
+        const double w = (dim == 3) ? 1.0 : su->eta_w[l];
+        yterms(mode, R, y, eta, w, &Yall[(size_t)q * NYT]);
+      }
+      for (int s = 0; s < np; s++) {
+        const double mass = su->mass[s], m2 = mass * mass, sign = su->sign[s], baryon = su->baryon[s];
+        const double mT = sqrt(m2 + pT * pT);
+        double rn_abs = R[R_RENORM];
+        if (mode == PTM || mode == PTB) {
+          const double rn = (mode == PTM) ? ptm_renorm(k, &aux[(size_t)c * 9], mass, sign, su->degen[s], baryon) : R[R_RENORM];
+          if (!std::isfinite(rn)) continue;
+          rn_abs = fabs(rn);
+        }
+        for (int kk = 0; kk < nk; kk++) {
+          double* a = &acc[((size_t)s * nk + kk) * nphi];
+          for (int l = 0; l < nl; l++) {
+            const double* Y = &Yall[(size_t)(kk * nl + l) * NYT];
+            const bool sep = (mode <= CE) || kind == 1.0 || Y[Y_NARROW] != 0.0;
+            if (sep) {
+              SepLane L;
+              sep_setup(sep_flavor(mode), R, Y, mT, m2, pT, sign, baryon, L);
+              if (L.skip) continue;
+              for (int j = 0; j < nphi; j++)
+                a[j] += sep_point(sep_flavor(mode), R, L, &PHall[(size_t)j * NPT], p->regulate_deltaf, p->outflow);
+            } else {
+              ModLane M;
+              mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, M);
+              if (M.skip) continue;
+              for (int j = 0; j < nphi; j++) a[j] += mod_point(M, &PHall[(size_t)j * NPT], p->outflow);
+            }
+          }
+        }
+      }
+    }
+    for (int s = 0; s < np; s++)
+      for (int kk = 0; kk < nk; kk++)
+        for (int j = 0; j < nphi; j++)
+          out[(((size_t)s * npT + i) * nphi + j) * ny_out + kk] = prefactor * su->degen[s] * acc[((size_t)s * nk + kk) * nphi + j];
+  }
+  if (stats) { stats[0] = st_break; stats[1] = st_pl; stats[2] = st_fail; stats[3] = st_it; }
+  return 0;
+}

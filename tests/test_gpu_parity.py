@@ -1,0 +1,116 @@
+"""GPU tier: libis3d_amd.so on the MI355X against the oracle (same seeded inputs),
+all five delta-f modes, 2+1D and 3+1D, plus edge cases.  Bar: <= 1e-6 relative on
+dN/(pT dpT dphi dy) (north_star); we expect and assert far tighter where the math
+allows."""
+import numpy as np
+import pytest
+
+from helpers import parity
+from is3d_amd import IS3DError, build_engine, make_spec, surface_averages, synth
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-9   # measured ~1e-13 (CPU emulation of the same math); north_star bar is 1e-6
+
+
+def run_gpu(spec, surf, T_avg=None):
+    e = build_engine(spec, surf, T_avg=T_avg)
+    out = e.calculate_spectra()
+    st = e.stats()
+    e.close()
+    return out, st
+
+
+@pytest.mark.parametrize("dim", [2, 3])
+@pytest.mark.parametrize("mode", [1, 2, 3, 4, 5])
+def test_spectra_parity(dim, mode):
+    s = synth.as_read(synth.surface(200, seed=11, dimension=dim, full3d=(dim == 3)))
+    spec = make_spec(hrg_eos=2, chosen="pikp", df_mode=mode, dimension=dim, famod_chains=1)
+    ref, rst = O.spectra(spec, s, threads=1, return_stats=True)
+    got, st = run_gpu(spec, s)
+    rel, zr, zg = parity(got, ref)
+    assert rel < TOL, (rel, zr, zg)
+    assert zr == zg
+    assert st["breakdown"] == rst[0]
+    if mode == 5:
+        assert st["iterations"] == rst[3]
+
+
+def test_smash_3d_grad_subset():
+    # many species (mass-sorted lanes, several wavefronts per y) on the config-2 grid
+    s = synth.as_read(synth.surface(64, seed=2, dimension=3))
+    spec = make_spec(hrg_eos=2, chosen="smash", df_mode=1, dimension=3, pT="pT48", phi="phi32", y="y21")
+    ref = O.spectra(spec, s, threads=8)
+    got, _ = run_gpu(spec, s)
+    assert parity(got, ref)[0] < TOL
+
+
+@pytest.mark.parametrize("mode", [1, 2, 3])
+def test_baryon_on(mode):
+    s = synth.as_read(synth.surface(100, seed=5, dimension=3, baryon=True, full3d=True))
+    spec = make_spec(hrg_eos=2, chosen="pikp", df_mode=mode, dimension=3, include_baryon=1, include_baryondiff_deltaf=1)
+    ref = O.spectra(spec, s)
+    got, _ = run_gpu(spec, s)
+    assert parity(got, ref)[0] < TOL
+
+
+def test_outflow_regulate_flags():
+    s = synth.as_read(synth.surface(100, seed=9))
+    spec = make_spec(hrg_eos=2, chosen="pikp", df_mode=1, regulate_deltaf=1, outflow=1)
+    got, _ = run_gpu(spec, s)
+    assert parity(got, O.spectra(spec, s))[0] < TOL
+
+
+def test_ptma_independent_chains():
+    s = synth.as_read(synth.surface(150, seed=4))
+    spec = make_spec(hrg_eos=2, chosen="pikp", df_mode=5, famod_chains=0)
+    got, _ = run_gpu(spec, s)
+    ref = O.spectra(spec, s, threads=150)      # reference with one cell per OpenMP thread
+    assert parity(got, ref)[0] < TOL
+
+
+def test_empty_and_all_skipped_surfaces():
+    spec = make_spec(hrg_eos=2, chosen="pikp", df_mode=2)
+    s = synth.as_read(synth.surface(16, seed=1))
+    s["dat"] = -np.abs(s["dat"]) * 10          # u.dsigma <= 0 everywhere: every cell skipped
+    got, _ = run_gpu(spec, s, T_avg=0.15)
+    assert np.all(got == 0.0)
+    e = build_engine(spec, None, T_avg=0.15)
+    e.set_surface({k: np.zeros(0) for k in synth.FIELDS})
+    assert np.all(e.calculate_spectra() == 0.0)
+
+
+def test_temperature_out_of_table_is_an_error():
+    spec = make_spec(hrg_eos=2, chosen="pikp", df_mode=2)
+    s = synth.as_read(synth.surface(16, seed=1))
+    s["T"] = s["T"].copy(); s["T"][3] = 0.3
+    e = build_engine(spec, s, T_avg=0.15)
+    with pytest.raises(IS3DError, match="interpolation"):
+        e.calculate_spectra()
+
+
+def test_df_coefficients_on_device_match_oracle():
+    s = synth.as_read(synth.surface(200, seed=7))
+    for mode in (1, 2, 4):
+        spec = make_spec(hrg_eos=2, chosen="pikp", df_mode=mode)
+        T, E, P, muB, nB = surface_averages(s)
+        e = build_engine(spec, s)
+        for fac in (-0.3, -0.1, 0.05):
+            got = e.evaluate_df_coefficients(T, 0.0, E, P, fac * P)
+            rc, ref = O.df_coefficients(spec, T, 0.0, E, P, fac * P, T_avg=T)
+            assert rc == 0
+            np.testing.assert_allclose(got, ref, rtol=1e-14, atol=0)
+        e.close()
+
+
+def test_jonah_table_matches_oracle():
+    s = synth.as_read(synth.surface(200, seed=7))
+    spec = make_spec(hrg_eos=2, chosen="pikp", df_mode=4)
+    e = build_engine(spec, s)
+    e.calculate_spectra()
+    l2, z, bp, mx = e.jonah_table()
+    rc, l2r, zr, bpr, mxr = O.jonah_table(spec, surface_averages(s)[0])
+    np.testing.assert_allclose(l2, l2r, rtol=0, atol=0)
+    np.testing.assert_allclose(z, zr, rtol=1e-15)
+    np.testing.assert_allclose(bp, bpr, rtol=1e-13, atol=1e-15)
+    assert abs(mx - mxr) < 1e-14
