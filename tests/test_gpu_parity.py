@@ -10,7 +10,7 @@ from is3d_amd import IS3DError, build_engine, make_spec, surface_averages, synth
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
-TOL = 1e-9   # measured ~1e-13 (CPU emulation of the same math); north_star bar is 1e-6
+TOL = 1e-8   # measured 1e-13..2e-9 (cancellation in tiny high-pT entries); north_star bar is 1e-6
 
 
 def run_gpu(spec, surf, T_avg=None):
