@@ -7,7 +7,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libis3d_amd.so")
+LIB_PATH = os.environ.get("IS3D_LIB") or os.path.join(_HERE, "libis3d_amd.so")   # IS3D_LIB: A/B builds only
 
 SURFACE_FIELDS = ["tau", "x", "y", "eta", "dat", "dax", "day", "dan", "ux", "uy", "un", "E", "T", "P",
                   "pixx", "pixy", "pixn", "piyy", "piyn", "bulkPi", "muB", "nB", "Vx", "Vy", "Vn"]

@@ -36,6 +36,9 @@ namespace {
 constexpr int kBlock = 256;
 constexpr int kJmax = 32;     // phi accumulators per lane
 constexpr int kTile = 4;      // cells per LDS tile
+#ifndef IS3D_SPECTRA_WAVES
+#define IS3D_SPECTRA_WAVES 3      // waves per SIMD the spectra kernel is register-allocated for
+#endif
 
 struct DevTables {            // device copy of the delta-f tables (pointers into one blob)
   DfTables tb;
@@ -180,24 +183,25 @@ struct SpecArgs {
   int regulate, outflow, dim;
 };
 
-template <int MODE, bool FAST>
-__device__ __forceinline__ void sep_phi_loop(const SpecArgs& A, const double* R, const SepLane& L, const double* PHc,
-                                             int j0, int nj, double* acc) {
+// flag bits of the spectra kernel instantiation
+constexpr int F_REG = 1, F_OUT = 2, F_DIFF = 4;
+
+template <int MODE, int FLAGS, bool FAST>
+__device__ __forceinline__ void sep_phi_loop(const double* R, const SepLane& L, const double* PHc, int j0, double* acc) {
   constexpr int FL = (MODE == GRAD) ? SEP_GRAD : (MODE == CE || MODE == PTM) ? SEP_CE : (MODE == PTB) ? SEP_PTB : SEP_FEQ;
-  SepLane Lf = L;
-  Lf.fast = FAST ? 1 : 0;
 #pragma unroll
-  for (int jj = 0; jj < kJmax; jj++) {
-    if (jj < nj) acc[jj] += sep_point(FL, R, Lf, PHc + (j0 + jj) * NPT, A.regulate, A.outflow);
-  }
+  for (int jj = 0; jj < kJmax; jj++)   // phi rows are padded to a multiple of kJmax: no per-point guard
+    acc[jj] += sep_point_t<FL, (FLAGS & F_REG) != 0, (FLAGS & F_OUT) != 0, (FLAGS & F_DIFF) != 0, FAST>(
+        R, L, PHc + (j0 + jj) * NPT);
 }
 
-template <int MODE>
-__global__ __launch_bounds__(kBlock) void k_spectra(SpecArgs A) {
+template <int MODE, int FLAGS>
+__global__ __launch_bounds__(kBlock, IS3D_SPECTRA_WAVES) void k_spectra(SpecArgs A) {
   extern __shared__ double smem[];
   double* s_rec = smem;                                   // [kTile][NREC]
   double* s_phi = s_rec + kTile * NREC;                   // [kTile][nphi][NPT]
-  double* s_y = s_phi + (long)kTile * A.nphi * NPT;       // [kTile][nq][NYT]
+  const int nphp = A.njb * kJmax;                         // phi rows padded to kJmax multiples
+  double* s_y = s_phi + (long)kTile * nphp * NPT;         // [kTile][nq][NYT]
 
   const int tid = threadIdx.x;
   const int ipt = blockIdx.y;
@@ -230,10 +234,16 @@ __global__ __launch_bounds__(kBlock) void k_spectra(SpecArgs A) {
       s_rec[t * NREC + f] = (t < nt) ? A.rec[(long)f * A.n + cb + t] : 0.0;
     }
     __syncthreads();
-    for (int idx = tid; idx < nt * A.nphi; idx += kBlock) {
-      const int t = idx / A.nphi, j = idx % A.nphi;
+    for (int idx = tid; idx < nt * nphp; idx += kBlock) {
+      const int t = idx / nphp, j = idx % nphp;
       const double* R = s_rec + t * NREC;
-      if (R[R_KIND] != 0.0) phiterms(MODE, R, pT, A.cphi[j], A.sphi[j], s_phi + ((long)t * A.nphi + j) * NPT);
+      double* PH = s_phi + ((long)t * nphp + j) * NPT;
+      if (j >= A.nphi) {
+#pragma unroll
+        for (int f = 0; f < NPT; f++) PH[f] = 0.0;         // padding: finite, never written out
+      } else if (R[R_KIND] != 0.0) {
+        phiterms(MODE, R, pT, A.cphi[j], A.sphi[j], PH);
+      }
     }
     for (int idx = tid; idx < nt * A.nq; idx += kBlock) {
       const int t = idx / A.nq, q = idx % A.nq;
@@ -258,7 +268,7 @@ __global__ __launch_bounds__(kBlock) void k_spectra(SpecArgs A) {
           if (!isfinite(rn)) continue;    // species skipped (MomentumSpectra.cpp:828-832)
           rn_abs = fabs(rn);
         }
-        const double* PHc = s_phi + (long)t * A.nphi * NPT;
+        const double* PHc = s_phi + (long)t * nphp * NPT;
         for (int l = 0; l < A.nl; l++) {
           const int q = k * A.nl + l;
           const double* Y = s_y + ((long)t * A.nq + q) * NYT;
@@ -267,16 +277,14 @@ __global__ __launch_bounds__(kBlock) void k_spectra(SpecArgs A) {
             SepLane L;
             sep_setup(sep_flavor(MODE), R, Y, mT, m2, pT, sign, baryon, L);
             if (L.skip) continue;
-            if (L.fast) sep_phi_loop<MODE, true>(A, R, L, PHc, j0, nj, acc);
-            else sep_phi_loop<MODE, false>(A, R, L, PHc, j0, nj, acc);
+            if (L.fast) sep_phi_loop<MODE, FLAGS, true>(R, L, PHc, j0, acc);
+            else sep_phi_loop<MODE, FLAGS, false>(R, L, PHc, j0, acc);
           } else if (MODE >= PTM) {
             ModLane M;
             mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, M);
             if (M.skip) continue;
 #pragma unroll
-            for (int jj = 0; jj < kJmax; jj++) {
-              if (jj < nj) acc[jj] += mod_point(M, PHc + (j0 + jj) * NPT, A.outflow);
-            }
+            for (int jj = 0; jj < kJmax; jj++) acc[jj] += mod_point_t<(FLAGS & F_OUT) != 0>(M, PHc + (j0 + jj) * NPT);
           }
         }
       }
@@ -644,8 +652,17 @@ static PrepConsts make_consts(const is3d_engine* e) {
 }
 
 template <int MODE>
-static void launch_spectra(dim3 grid, size_t shmem, hipStream_t st, const SpecArgs& a) {
-  hipLaunchKernelGGL(k_spectra<MODE>, grid, dim3(kBlock), shmem, st, a);
+static void launch_spectra(dim3 grid, size_t shmem, hipStream_t st, const SpecArgs& a, int flags) {
+  switch (flags) {
+    case 0: hipLaunchKernelGGL((k_spectra<MODE, 0>), grid, dim3(kBlock), shmem, st, a); break;
+    case 1: hipLaunchKernelGGL((k_spectra<MODE, 1>), grid, dim3(kBlock), shmem, st, a); break;
+    case 2: hipLaunchKernelGGL((k_spectra<MODE, 2>), grid, dim3(kBlock), shmem, st, a); break;
+    case 3: hipLaunchKernelGGL((k_spectra<MODE, 3>), grid, dim3(kBlock), shmem, st, a); break;
+    case 4: hipLaunchKernelGGL((k_spectra<MODE, 4>), grid, dim3(kBlock), shmem, st, a); break;
+    case 5: hipLaunchKernelGGL((k_spectra<MODE, 5>), grid, dim3(kBlock), shmem, st, a); break;
+    case 6: hipLaunchKernelGGL((k_spectra<MODE, 6>), grid, dim3(kBlock), shmem, st, a); break;
+    default: hipLaunchKernelGGL((k_spectra<MODE, 7>), grid, dim3(kBlock), shmem, st, a); break;
+  }
 }
 
 extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
@@ -731,15 +748,17 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   sa.npart = np; sa.npT = npT; sa.nphi = nphi; sa.ny_out = ny_out; sa.nk = nk; sa.nl = nl; sa.nq = nk * nl; sa.njb = njb;
   sa.ntask = ntask; sa.cells_per_split = cps;
   sa.regulate = e->p.regulate_deltaf; sa.outflow = e->p.outflow; sa.dim = dim;
-  const size_t shmem = sizeof(double) * ((size_t)kTile * NREC + (size_t)kTile * nphi * NPT + (size_t)kTile * sa.nq * NYT);
+  const size_t shmem = sizeof(double) * ((size_t)kTile * NREC + (size_t)kTile * njb * kJmax * NPT + (size_t)kTile * sa.nq * NYT);
   if (shmem > 160 * 1024) return e->fail(IS3D_ERR_ARG, "momentum grid too large for the LDS tile");
   const dim3 grid((unsigned)bx, (unsigned)npT, (unsigned)nsplit);
+  const int diff = (e->p.include_baryon && e->p.include_baryondiff_deltaf && mode <= PTM) ? F_DIFF : 0;
+  const int kflags = (e->p.regulate_deltaf ? F_REG : 0) | (e->p.outflow ? F_OUT : 0) | diff;
   switch (mode) {
-    case GRAD: launch_spectra<GRAD>(grid, shmem, st, sa); break;
-    case CE: launch_spectra<CE>(grid, shmem, st, sa); break;
-    case PTM: launch_spectra<PTM>(grid, shmem, st, sa); break;
-    case PTB: launch_spectra<PTB>(grid, shmem, st, sa); break;
-    default: launch_spectra<PTMA>(grid, shmem, st, sa); break;
+    case GRAD: launch_spectra<GRAD>(grid, shmem, st, sa, kflags); break;
+    case CE: launch_spectra<CE>(grid, shmem, st, sa, kflags); break;
+    case PTM: launch_spectra<PTM>(grid, shmem, st, sa, kflags); break;
+    case PTB: launch_spectra<PTB>(grid, shmem, st, sa, kflags); break;
+    default: launch_spectra<PTMA>(grid, shmem, st, sa, kflags); break;
   }
   HIPCHK(e, hipGetLastError());
   HIPCHK(e, hipEventRecord(e->ev[2], st));
