@@ -1,0 +1,79 @@
+// is3d_driver.h -- drop-in C++ facade of iS3D2's particlization plug-in surface for
+// operation = 1, running the MI355X engine (libis3d_amd.so) underneath.
+//
+//   class IS3D                (iS3D.h:25-104)   read_fo_surf_from_memory + run_particlization
+//   class EmissionFunctionArray (EmissionFunction.h:135-140) ctor + calculate_spectra
+//
+// Same inputs (iS3D_parameters.dat, input/surface.dat, PDG/, deltaf_coefficients/, tables/
+// relative to a working directory) and the same outputs (results/continuous/*.dat).
+// Differences from the reference: errors are returned / thrown instead of exit(); only
+// operation = 1 is on this path; cells may be sharded over several GPUs in one process.
+#pragma once
+#include <string>
+#include <vector>
+
+#include "host_io.h"
+
+namespace is3d {
+namespace host {
+
+struct RunOptions {
+  int device = 0;          // first HIP device
+  int num_devices = 1;     // cells sharded over devices [device, device + num_devices)
+  bool write_files = true;
+  bool quiet = false;
+};
+
+// EmissionFunctionArray(paraRdr, chosen, pT, phi, y, eta, particles, Nparticles, surface, FO_length, df tables)
+class EmissionFunctionArray {
+ public:
+  EmissionFunctionArray(const ParameterReader& params, const Table& chosen, const Table& pT, const Table& phi,
+                        const Table& y, const Table& eta, const std::vector<Particle>& particles, const Surface& surf,
+                        const DfTablesData& df, const Averages& plasma, const std::vector<double>& gla_roots,
+                        const std::vector<double>& gla_weights, int gla_alpha, int gla_points);
+  // computes dN/(pT dpT dphi dy) [species][pT][phi][y]; throws std::runtime_error on failure
+  void calculate_spectra(const RunOptions& opt);
+  void write_files(const std::string& dir) const;
+  const std::vector<double>& spectra() const { return dN_; }
+  const std::vector<long>& mcid() const { return mcid_; }
+  double seconds() const { return seconds_; }
+
+ private:
+  const ParameterReader& p_;
+  const Table &pT_, &phi_, &y_, &eta_;
+  const Surface& surf_;
+  const DfTablesData& df_;
+  Averages plasma_;
+  const std::vector<double>&gr_, &gw_;
+  int galpha_, gpts_;
+  int dimension_ = 2;
+  std::vector<double> mass_, sign_, degen_, baryon_;
+  std::vector<double> pdg_mass_, pdg_sign_, pdg_degen_, pdg_baryon_;
+  std::vector<long> mcid_;
+  std::vector<double> dN_;
+  double seconds_ = 0.0;
+};
+
+class IS3D {
+ public:
+  explicit IS3D(std::string workdir = ".") : dir_(std::move(workdir)) {}
+  // iS3D.cpp:33-78 (units: reader-converted, GeV / fm)
+  void read_fo_surf_from_memory(std::vector<double> tau, std::vector<double> x, std::vector<double> y,
+                                std::vector<double> eta, std::vector<double> dsigma_tau, std::vector<double> dsigma_x,
+                                std::vector<double> dsigma_y, std::vector<double> dsigma_eta, std::vector<double> E,
+                                std::vector<double> T, std::vector<double> P, std::vector<double> ux,
+                                std::vector<double> uy, std::vector<double> un, std::vector<double> pixx,
+                                std::vector<double> pixy, std::vector<double> pixn, std::vector<double> piyy,
+                                std::vector<double> piyn, std::vector<double> pinn, std::vector<double> Pi);
+  // iS3D.cpp:81-282 restricted to operation = 1; throws std::runtime_error
+  void run_particlization(int fo_from_file, const RunOptions& opt = RunOptions());
+  const std::vector<double>& spectra() const { return dN_; }
+
+ private:
+  std::string dir_;
+  Surface mem_;
+  std::vector<double> dN_;
+};
+
+}  // namespace host
+}  // namespace is3d

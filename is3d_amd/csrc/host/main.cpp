@@ -1,0 +1,23 @@
+// iS3D_amd -- drop-in replacement of the reference executable (src/cpp/Main.cpp) for
+// operation = 1: run in a directory laid out like the reference's (iS3D_parameters.dat,
+// input/surface.dat, PDG/, deltaf_coefficients/, tables/, results/continuous/).
+// Environment: IS3D_DEVICE (first GPU, default 0), IS3D_NUM_GPUS (cells sharded, default 1).
+#include <cstdio>
+#include <cstdlib>
+#include <exception>
+
+#include "is3d_driver.h"
+
+int main(int argc, char** argv) {
+  is3d::host::RunOptions opt;
+  if (const char* d = std::getenv("IS3D_DEVICE")) opt.device = std::atoi(d);
+  if (const char* n = std::getenv("IS3D_NUM_GPUS")) opt.num_devices = std::atoi(n);
+  try {
+    is3d::host::IS3D particlization(argc > 1 ? argv[1] : ".");
+    particlization.run_particlization(1, opt);
+  } catch (const std::exception& e) {
+    std::fprintf(stderr, "iS3D_amd: %s\n", e.what());
+    return 1;
+  }
+  return 0;
+}

@@ -89,3 +89,40 @@ def write_mode1(path, surf, include_baryon=False):
     with open(path, "w") as f:
         for row in a:
             f.write(" ".join("%.17g" % v for v in row) + "\n")
+
+
+def write_music(path, surf, include_baryon=False):
+    """MUSIC (public) surface format (readindata.cpp:383-390, mode 6): dsigma_mu/tau, u^tau, tau u^eta,
+    E, T, muB [fm^-n], muS, muC, (E+P)/T, pi^{mu nu} with tau factors, Pi, [nB, V^mu]."""
+    n = len(surf["tau"])
+    tau = surf["tau"]
+    ut = np.sqrt(1.0 + surf["ux"] ** 2 + surf["uy"] ** 2 + tau * tau * surf["un"] ** 2)
+    cols = [tau, surf["x"], surf["y"], surf["eta"],
+            surf["dat"] / tau, surf["dax"] / tau, surf["day"] / tau, surf["dan"] / tau,
+            ut, surf["ux"], surf["uy"], tau * surf["un"],
+            surf["E"] / HBARC, surf["T"] / HBARC, surf["muB"] / HBARC, np.zeros(n), np.zeros(n),
+            (surf["E"] + surf["P"]) / surf["T"],
+            np.zeros(n), np.zeros(n), np.zeros(n), np.zeros(n),
+            surf["pixx"] / HBARC, surf["pixy"] / HBARC, tau * surf["pixn"] / HBARC,
+            surf["piyy"] / HBARC, tau * surf["piyn"] / HBARC, np.zeros(n), surf["bulkPi"] / HBARC]
+    if include_baryon:
+        cols += [surf["nB"], np.zeros(n), surf["Vx"], surf["Vy"], tau * surf["Vn"]]
+    a = np.stack(cols, axis=1)
+    with open(path, "w") as f:
+        for row in a:
+            f.write(" ".join("%.17g" % v for v in row) + "\n")
+
+
+def write_hic(path, surf):
+    """HIC-EventGen surface format (readindata.cpp:570-731, mode 7), GeV units, v = u/u^tau."""
+    n = len(surf["tau"])
+    tau = surf["tau"]
+    ut = np.sqrt(1.0 + surf["ux"] ** 2 + surf["uy"] ** 2)
+    z = np.zeros(n)
+    cols = [tau, surf["x"], surf["y"], z, surf["dat"] / tau, surf["dax"] / tau, surf["day"] / tau, z,
+            surf["ux"] / ut, surf["uy"] / ut, z, z, z, z, z, surf["pixx"], surf["pixy"], z, surf["piyy"], z, z,
+            surf["bulkPi"], surf["T"], surf["E"], surf["P"], surf["muB"]]
+    a = np.stack(cols, axis=1)
+    with open(path, "w") as f:
+        for row in a:
+            f.write(" ".join("%.17g" % v for v in row) + "\n")

@@ -1,0 +1,53 @@
+"""N > 1 decomposition on CPU: world_size-2 gloo processes shard the cells, integrate their
+shard (oracle as the per-rank worker; on the GPU the engine does this) and all-reduce the
+spectra -- the result equals the single-process integral over the whole surface."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    from is3d_amd import dist as D, make_spec, synth
+    from oracle import oracle as O
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    s = synth.as_read(synth.surface(101, seed=5))
+    lo, hi = D.shard_range(101, rank, world)
+    shard = {k: v[lo:hi] for k, v in s.items()}
+    avg = D.global_averages(D.average_sums(shard), D.torch_all_reduce(dist))
+    spec = make_spec(hrg_eos=2, chosen="pikp", df_mode=4)        # PTB: needs the global T_avg
+    part = torch.from_numpy(O.spectra(spec, shard, T_avg=avg[0]))
+    dist.all_reduce(part)
+    if rank == 0:
+        q.put((avg, part.numpy()))
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_shard_and_allreduce():
+    import torch.multiprocessing as mp
+    from is3d_amd import make_spec, synth
+    from oracle import oracle as O
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + os.getpid() % 1000
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    avg, got = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    s = synth.as_read(synth.surface(101, seed=5))
+    full_avg = O.averages(s)
+    assert abs(avg[0] - full_avg[0]) <= 1e-14 * full_avg[0]
+    spec = make_spec(hrg_eos=2, chosen="pikp", df_mode=4)
+    ref = O.spectra(spec, s, T_avg=full_avg[0])
+    np.testing.assert_allclose(got, ref, rtol=1e-11)

@@ -1,0 +1,104 @@
+"""C++ host layer (libis3d_host.so): reference file formats on both sides of the hot path.
+
+CPU tier: readers pinned bit-for-bit against the reference's own readindata.cpp /
+ParameterReader.cpp (oracle/_ref harness, where built); GPU tier: the whole drop-in
+workflow (run directory in, results/continuous/*.dat out) against the oracle."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from helpers import parity
+from is3d_amd import host, make_spec, rundir, synth
+from oracle import oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HARNESS = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+REF = "/root/reference"
+need_ref = pytest.mark.skipif(not (os.path.exists(HARNESS) and os.path.isdir(REF)), reason="oracle/_ref absent")
+
+
+def harness(args, cwd):
+    out = subprocess.run([HARNESS] + args, cwd=cwd, capture_output=True, text=True, check=True).stdout
+    return out.split("@@BEGIN\n", 1)[1] if "@@BEGIN\n" in out else out
+
+
+@need_ref
+@pytest.mark.parametrize("fmt,dim,baryon", [(1, 2, 0), (1, 3, 1), (6, 3, 0), (6, 3, 1), (7, 2, 0)])
+def test_surface_readers_match_reference(tmp_path, fmt, dim, baryon):
+    s = synth.surface(200, seed=21, dimension=dim, baryon=bool(baryon), full3d=(dim == 3 and fmt != 7))
+    d = rundir.write_run_dir(str(tmp_path), s, dict(dimension=dim, df_mode=1, include_baryon=baryon,
+                                                    include_bulk_deltaf=1, include_shear_deltaf=1,
+                                                    include_baryondiff_deltaf=baryon), surface_format=fmt)
+    out = harness(["surface"], d).strip().split("\n")
+    n = int(out[0])
+    ref = np.array([[float(v) for v in ln.split()] for ln in out[1:1 + n]])
+    ref_avg = np.array([float(v) for v in out[1 + n].split()])
+    fields, avg = host.read_surface(d, fmt, dim, baryon)
+    for k, name in enumerate(synth.FIELDS):
+        if not baryon and name in ("nB", "Vx", "Vy", "Vn") or (fmt == 1 and not baryon and name == "muB"):
+            continue
+        np.testing.assert_array_equal(fields[k], ref[:, k], err_msg=name)
+    np.testing.assert_array_equal(avg, ref_avg)
+
+
+@need_ref
+@pytest.mark.parametrize("hrg_eos", [1, 2, 3])
+def test_pdg_reader_matches_reference_on_reference_files(tmp_path, hrg_eos):
+    os.symlink(os.path.join(REF, "PDG"), tmp_path / "PDG")
+    (tmp_path / "iS3D_parameters.dat").write_text("hrg_eos = %d\n" % hrg_eos)
+    out = harness(["pdg"], str(tmp_path)).split("\n")
+    n = int(out[0])
+    ref = np.array([[float(v) for v in ln.split()] for ln in out[1:1 + n]])
+    mine = host.read_pdg(str(tmp_path), hrg_eos)
+    assert len(mine["mcid"]) == n
+    for k, name in enumerate(["mcid", "mass", "gspin", "baryon", "sign"]):
+        np.testing.assert_array_equal(mine[name], ref[:, k], err_msg=name)
+
+
+@need_ref
+def test_parameter_reader_matches_reference():
+    path = os.path.join(REF, "iS3D_parameters.dat")
+    keys = ["operation", "mode", "hrg_eos", "dimension", "df_mode", "include_baryon", "deta_min", "mass_pion0",
+            "threads_per_block", "min_num_hadrons", "y_cut", "pT_bins", "lightest_particle"]
+    out = harness(["params", path] + keys, ROOT).split()
+    for k, v in zip(keys, out):
+        assert host.param(path, k) == float(v), k
+
+
+def test_table_reader_drops_unterminated_last_line(tmp_path):
+    # Arsenal.cpp readBlockData: rows are '\n'-terminated lines
+    (tmp_path / "iS3D_parameters.dat").write_text("a = 1\nb=2 # c\n  C  =  3.5e-2\n")
+    assert host.param(str(tmp_path / "iS3D_parameters.dat"), "c") == 0.035
+    assert host.param(str(tmp_path / "iS3D_parameters.dat"), "B") == 2.0
+
+
+def _spec_for(params, hrg, chosen, pT, phi):
+    return make_spec(hrg_eos=hrg, chosen=chosen, pT=pT, phi=phi, **params)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fmt,dim,mode", [(1, 2, 1), (1, 3, 2), (6, 3, 2), (7, 2, 3), (1, 2, 4)])
+def test_dropin_workflow_matches_oracle(tmp_path, fmt, dim, mode):
+    s = synth.surface(150, seed=31, dimension=dim, full3d=(dim == 3 and fmt != 7))
+    params = dict(dimension=dim, df_mode=mode, include_baryon=0, include_bulk_deltaf=1, include_shear_deltaf=1,
+                  include_baryondiff_deltaf=0, regulate_deltaf=0, outflow=0, deta_min=1e-5, mass_pion0=0.138)
+    d = rundir.write_run_dir(str(tmp_path), s, params, hrg_eos=2, chosen="pikp", surface_format=fmt)
+    spec = _spec_for(params, 2, "pikp", "pT24", "phi24")
+    fields, avg = host.read_surface(d, fmt, dim, 0)
+    surf = {k: fields[i] for i, k in enumerate(synth.FIELDS)}
+    ref = O.spectra(spec, surf, T_avg=avg[0])
+    got = host.run_particlization(d, len(ref))
+    assert parity(got, ref)[0] < 1e-8
+    # the five reference output files per species, reference layout
+    npT, nphi, ny = 24, 24, (21 if dim == 3 else 1)
+    for mc in spec["species"]["mcid"]:
+        lines = open(os.path.join(d, "results/continuous/dN_pTdpTdphidy_%d.dat" % mc)).read().split("\n")
+        assert lines[0] == "y\tphip\tpT\tdN_pTdpTdphidy"
+        assert len([ln for ln in lines[1:] if ln]) == npT * nphi * ny
+        for name in ("vn", "dN_2pipTdpTdy", "dN_dphidy", "dN_dy"):
+            assert os.path.exists(os.path.join(d, "results/continuous/%s_%d.dat" % (name, mc)))
+    vals = np.array([float(ln.split("\t")[3]) for ln in lines[1:] if ln])
+    last = ref.reshape(3, npT, nphi, ny)[2]          # file order: y, phi, pT
+    np.testing.assert_allclose(vals, np.transpose(last, (2, 1, 0)).ravel(), rtol=5e-9)
