@@ -54,17 +54,6 @@ def make_surface(cfg, rank, world, dim, baryon):
     return synth.as_read(synth.surface(cfg["cells"], seed=7 + rank, dimension=dim, baryon=baryon, full3d=(dim == 3)))
 
 
-def local_average_sums(s, include_baryon):
-    tau = s["tau"]; tau2 = tau * tau
-    ut = np.sqrt(1. + s["ux"] ** 2 + s["uy"] ** 2 + tau2 * s["un"] ** 2)
-    uds = ut * s["dat"] + s["ux"] * s["dax"] + s["uy"] * s["day"] + s["un"] * s["dan"]
-    ds_ds = s["dat"] ** 2 - s["dax"] ** 2 - s["day"] ** 2 - s["dan"] ** 2 / tau2
-    w = np.abs(uds) + np.sqrt(np.abs(uds * uds - ds_ds))
-    muB = s["muB"] if include_baryon else np.zeros_like(w)
-    nB = s["nB"] if include_baryon else np.zeros_like(w)
-    return np.array([w.sum(), (s["T"] * w).sum(), (s["E"] * w).sum(), (s["P"] * w).sum(), (muB * w).sum(), (nB * w).sum()])
-
-
 def cpu_baseline(spec, surf, units_per_cell, target_s=15.0):
     """Oracle ('port' of the reference loop) on the host cores, on a cell prefix of the same workload."""
     from oracle import oracle as O
@@ -122,12 +111,9 @@ def main():
                      dimension=cfg["dim"], df_mode=mode, **flags)
     surf = make_surface(cfg, rank, world, cfg["dim"], bool(flags.get("include_baryon", 0)))
     n_local = len(surf["tau"])
-    sums = torch.tensor(local_average_sums(surf, flags.get("include_baryon", 0)), dtype=torch.float64)
-    if world > 1:
-        sums = sums.to(dev)
-        dist.all_reduce(sums)
-        sums = sums.cpu()
-    T_avg = float("%.15g" % (sums[1].item() / sums[0].item()))
+    from is3d_amd import dist as D
+    reduce = D.torch_all_reduce(dist, dev) if world > 1 else (lambda a: a)
+    T_avg = D.global_averages(D.average_sums(surf, flags.get("include_baryon", 0)), reduce)[0]
 
     eng = build_engine(spec, surf, T_avg=T_avg, device=local_rank)
     outsize = eng.output_size()

@@ -32,6 +32,51 @@
 
 namespace is3d {
 
+// exp(x) for |x| <= 690 (the fast-path domain: no overflow, no subnormal result).
+// Cody-Waite reduction x = k ln2 + r, |r| <= ln2/2, degree-13 Taylor polynomial (truncation
+// < 5e-18 relative), 2^k by ldexp; max error measured ~1 ulp against glibc (test_kernel_math_cpu).
+// On the device each coefficient passes through an empty asm that pins it to an SGPR pair at
+// the point of use: otherwise the compiler hoists all of them out of the cell loop into VGPRs
+// and spills them to scratch (one serialized reload per coefficient per lane setup).
+IS3D_HD double kconst(double v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  asm volatile("" : "+s"(v));
+#endif
+  return v;
+}
+
+struct ExpCoef { double l2e, ln2hi, ln2lo, c[11]; };   // c: 1/13! ... 1/3!
+
+IS3D_HD ExpCoef exp_coef() {
+  ExpCoef e;
+  e.l2e = kconst(1.4426950408889634);
+  e.ln2hi = kconst(6.93147180369123816490e-01);    // low 32 bits zero
+  e.ln2lo = kconst(1.90821492927058770002e-10);
+  const double f[11] = {1.0 / 6227020800.0, 1.0 / 479001600.0, 1.0 / 39916800.0, 1.0 / 3628800.0, 1.0 / 362880.0,
+                        1.0 / 40320.0, 1.0 / 5040.0, 1.0 / 720.0, 1.0 / 120.0, 1.0 / 24.0, 1.0 / 6.0};
+  for (int i = 0; i < 11; i++) e.c[i] = kconst(f[i]);
+  return e;
+}
+
+IS3D_HD double exp_poly(const ExpCoef& E, double x) {
+  const double k = rint(x * E.l2e);
+  double r = fma(-k, E.ln2hi, x);
+  r = fma(-k, E.ln2lo, r);
+  double p = E.c[0];
+  for (int i = 1; i < 11; i++) p = fma(p, r, E.c[i]);
+  p = fma(p, r, 0.5);
+  p = fma(p, r, 1.0);
+  p = fma(p, r, 1.0);
+  return ldexp(p, (int)k);
+}
+
+IS3D_HD double exp_dom690(double x) { return exp_poly(exp_coef(), x); }
+
+// exp(x) for any x: clamped into [-746, 710] so that k fits an int; ldexp saturates to +inf
+// above 709.78 (the reference's exp overflow, after which 1/(inf + sign) = 0) and rounds to
+// subnormal / zero below -708.4
+IS3D_HD double exp_clamped(const ExpCoef& E, double x) { return exp_poly(E, fmin(fmax(x, -746.0), 710.0)); }
+
 // 16-byte pair for ds_read_b128 of the phi-term rows (96-byte, 16-byte aligned)
 #if defined(__HIP_DEVICE_COMPILE__)
 typedef double dbl2 __attribute__((ext_vector_type(2)));
@@ -44,7 +89,8 @@ enum DfMode : int { GRAD = 1, CE = 2, PTM = 3, PTB = 4, PTMA = 5 };
 static constexpr double kHbarC = 0.197327053;            // iS3D.h:14
 
 // ---------------------------------------------------------------------------
-// Per-cell record (output of the prepass, input of the spectra kernel), SoA.
+// Per-cell record (output of the prepass, input of the spectra kernel), stored as an array of
+// records rec[cell][NREC] so a tile of consecutive cells is one contiguous block.
 // ---------------------------------------------------------------------------
 enum Rec : int {
   R_KIND = 0,   // 0 skip (u.dsigma<=0), 1 separable (Grad/CE or breakdown), 2 modified
@@ -58,12 +104,12 @@ enum Rec : int {
   R_SHEAR, R_BULK0, R_BULK1, R_BULK2, R_DIFF0, R_DIFF1, R_DLAM, R_DZ,
   R_ETASCALE, R_DET, R_NARROW, R_RENORM, R_ZB, R_VB,
   R_UCX, R_UCY, R_UCZ, R_USX, R_USY, R_USZ, R_VCX, R_VCY, R_VCZ, R_VSX, R_VSY, R_VSZ,
+  R_PAD,        // NREC even: a record is a whole number of 16-byte pairs
   NREC
 };
 
-// y-term (per cell, q) and phi-term (per cell, j) layouts
+// y-term layout (per cell, q); phi-terms are dbl2 pairs, see phiterms
 enum YT : int { Y_A = 0, Y_D, Y_Q1, Y_CH, Y_SH, Y_W, Y_WT, Y_MUX, Y_MUY, Y_MUZ, Y_MD, Y_NARROW, NYT };
-enum PT : int { P_B = 0, P_PTB, P_PTDP, P_PT, P_PN, P_Q3, P_WP, P_Z, P_VX, P_VY, P_VZ, P_PAD, NPT };
 
 // surface field order (include/is3d_amd.h, is3d_surface)
 enum Surf : int {
@@ -585,25 +631,27 @@ IS3D_HD void yterms(int mode, const double* R, double y, double eta, double w, d
   }
 }
 
-// phi-terms for (cell R, pT, phi)
-IS3D_HD void phiterms(int mode, const double* R, double pT, double c, double s, double* PH) {
-  const double B = c * R[R_UX] + s * R[R_UY];
-  PH[P_PTB] = pT * B;
-  PH[P_Z] = PH[P_PTB] / R[R_T];
-  PH[P_B] = exp(PH[P_Z]);             // b' = exp(+pT B/T): feq = b' / (a + sign b')
-  PH[P_PTDP] = pT * (c * R[R_DAX] + s * R[R_DAY]);
-  PH[P_PT] = pT * (-2.0 * (R[R_PITX] * c + R[R_PITY] * s));
-  PH[P_PN] = pT * (2.0 * (R[R_TPIXN] * c + R[R_TPIYN] * s));
-  PH[P_Q3] = R[R_SHEAR] * (pT * pT * (R[R_PIXX] * c * c + R[R_PIYY] * s * s + 2.0 * R[R_PIXY] * c * s));
-  PH[P_WP] = pT * (R[R_VX] * c + R[R_VY] * s);
-  if (mode >= PTM) {
-    PH[P_VX] = pT * (c * R[R_VCX] + s * R[R_VSX]);
-    PH[P_VY] = pT * (c * R[R_VCY] + s * R[R_VSY]);
-    PH[P_VZ] = pT * (c * R[R_VCZ] + s * R[R_VSZ]);
+// phi-terms.  Everything the integrand needs per (cell, phi) except two numbers is linear in
+// (pc, ps) = (pT cos phi, pT sin phi): u.p, p.dsigma, pi^{t i} p_i, pi^{n i} p_i, V.p and the
+// modified momentum A^{-1} p all are.  Those linear pieces are folded into per-lane
+// coefficients at sep_setup / mod_setup time, so a point reads only
+//   cs = {pc, ps}        per phi          (shared by every cell of the workgroup)
+//   bp = {b', Phi}       per (cell, phi)  b' = exp(+pT B/T) with B = u^x cos + u^y sin,
+//                                         Phi = the part of delta-f quadratic in (pc, ps)
+// Grad: Phi = shear p_i pi^{ij} p_j + bulk2 (pT B)^2 + c4 (pT B)(V.p)   (E^2 and E (V.p) cross terms)
+// CE / PTM / PTB (separable): Phi = shear p_i pi^{ij} p_j
+IS3D_HD dbl2 phiterms(int mode, const double* R, double pT, double c, double s) {
+  const double PTB = pT * (c * R[R_UX] + s * R[R_UY]);
+  const double Q3 = R[R_SHEAR] * (pT * pT * (R[R_PIXX] * c * c + R[R_PIYY] * s * s + 2.0 * R[R_PIXY] * c * s));
+  dbl2 o;
+  o.x = exp(PTB / R[R_T]);
+  if (mode == GRAD) {
+    const double WP = pT * (R[R_VX] * c + R[R_VY] * s);
+    o.y = Q3 + PTB * (R[R_BULK2] * PTB + R[R_DIFF1] * WP);
   } else {
-    PH[P_VX] = PH[P_VY] = PH[P_VZ] = 0.0;
+    o.y = Q3;
   }
-  PH[P_PAD] = 0.0;
+  return o;
 }
 
 // exp(x) overflows above this; 1/(inf + sign) == 0 exactly as in the reference
@@ -613,39 +661,75 @@ static constexpr double kFastMax = 690.0;
 // ---------------------------------------------------------------------------
 // Lane state for one (cell, species, pT, q) and the per-phi integrand.
 // ---------------------------------------------------------------------------
+// A lin3 is c0 + cc pc + cs ps.
 struct SepLane {
-  double EA, x, a, mTD, w, q1, mch, msh, mW, c0, b1b, d0b;   // see sep_setup
-  double sign, m2, baryon;
+  double a, ssc, sign;         // a = exp(mT A/T - chem - S), ssc = sign e^-S:  b' / (a + ssc b') = e^S feq
+  double D0, Dc, Ds;           // e^-S p.dsigma (x w_eta)
+  double S0, Sc, Ss;           // Grad: S (with Phi); CE/PTB: numerator N of the 1/E part (with Phi)
+  double E0, Ec, Es;           // CE/PTB: E = u.p
+  double L0, Lc, Ls;           // CE/PTB: part of delta-f linear in E
+  double c0;                   // PTB: constant added outside (1 - sign feq)
+  double x, Zc, Zs;            // slow path: feq = 1/(exp(x - Zc pc - Zs ps) + sign)
   int skip, fast;
 };
 
 // Per-(cell, q, species) setup for the separable integrand.  Returns skip=1 when every
 // phi point underflows (exp argument > 709.78 for all phi: contributes exactly 0).
+// The delta-f polynomials (MomentumSpectra.cpp:304-361 Grad, :565-600 CE, :920-923 PTB) are
+// expanded in (pc, ps); see phiterms for the quadratic remainder Phi.
 IS3D_HD void sep_setup(int flavor, const double* R, const double* Y, double mT, double m2, double pT, double sign,
                        double baryon, SepLane& L) {
-  const double T = R[R_T];
-  L.sign = sign; L.m2 = m2; L.baryon = baryon;
-  L.EA = mT * Y[Y_A];
-  L.x = L.EA * R[R_INVT] - baryon * R[R_CHEM];
+  L.sign = sign;
+  const double EA = mT * Y[Y_A];
+  L.x = EA * R[R_INVT] - baryon * R[R_CHEM];
   const double zb = pT * R[R_ZB];                 // >= max_j |pT B_j / T|
   L.skip = (L.x - zb > kExpMax) ? 1 : 0;
-  // fast: a = e^x and b' = e^z both <= e^690, so a + sign b' and (a + sign b') E stay finite
-  L.fast = (fabs(L.x) <= kFastMax && zb <= kFastMax) ? 1 : 0;
-  L.a = L.fast ? exp(L.x) : 0.0;
-  L.mTD = mT * Y[Y_D];
-  L.w = Y[Y_WT];
+  // fast: a = e^(x-S) and b' = e^z both <= e^690, so a + ssc b' and (a + ssc b') E stay finite.
+  // S = 0 unless x > 600; then S = rint(x) - 600 (an integer, so x - S is exact) keeps the lanes
+  // near the exp-overflow edge on the factorised path instead of the per-point exp path
+  const double S = (L.x > 600.0) ? rint(L.x) - 600.0 : 0.0;
+  L.fast = (L.x >= -kFastMax && zb <= kFastMax && S <= kFastMax) ? 1 : 0;
+  L.a = L.fast ? exp_dom690(L.x - S) : 0.0;
+  const double esc = (L.fast && S > 0.0) ? exp_dom690(-S) : 1.0;
+  L.ssc = sign * esc;
+  L.Zc = R[R_UX] * R[R_INVT]; L.Zs = R[R_UY] * R[R_INVT];
+  const double w = Y[Y_WT];
+  L.D0 = esc * (mT * Y[Y_D]); L.Dc = esc * (w * R[R_DAX]); L.Ds = esc * (w * R[R_DAY]);
   const double shear = R[R_SHEAR];
-  L.q1 = shear * mT * mT * Y[Y_Q1];
-  L.mch = shear * mT * Y[Y_CH];
-  L.msh = shear * mT * Y[Y_SH];
-  L.mW = mT * Y[Y_W];
+  const double q1 = shear * mT * mT * Y[Y_Q1];
+  const double mch = shear * mT * Y[Y_CH], msh = shear * mT * Y[Y_SH];
+  const double mW = mT * Y[Y_W];
+  const double ux = R[R_UX], uy = R[R_UY], Vx = R[R_VX], Vy = R[R_VY];
+  // shear p.pi.p = q1 + Phi + (pc, ps) . (-2 mch pi^{t i} + 2 msh tau pi^{n i})
+  const double Pc = 2.0 * (msh * R[R_TPIXN] - mch * R[R_PITX]);
+  const double Ps = 2.0 * (msh * R[R_TPIYN] - mch * R[R_PITY]);
+  L.E0 = EA; L.Ec = -ux; L.Es = -uy;
+  L.L0 = L.Lc = L.Ls = 0.0; L.c0 = 0.0;
   if (flavor == SEP_GRAD) {
-    L.c0 = R[R_BULK0] * m2; L.b1b = R[R_BULK1] * baryon; L.d0b = R[R_DIFF0] * baryon;
-    L.q1 += L.c0;
+    // S = (bulk2 E + b1b) E + c0 + p.pi.p + (c4 E + c3 b)(W - V.p),  E = EA - PTB, PTB = ux pc + uy ps
+    const double bulk2 = R[R_BULK2], diff1 = R[R_DIFF1];
+    const double b1b = R[R_BULK1] * baryon, d0b = R[R_DIFF0] * baryon;
+    const double kB = -(2.0 * bulk2 * EA + b1b + diff1 * mW);     // coefficient of PTB
+    const double kW = -(diff1 * EA + d0b);                          // coefficient of V.p
+    L.S0 = (bulk2 * EA + b1b) * EA + R[R_BULK0] * m2 + q1 + (diff1 * EA + d0b) * mW;
+    L.Sc = Pc + kB * ux + kW * Vx;
+    L.Ss = Ps + kB * uy + kW * Vy;
   } else if (flavor == SEP_CE) {
-    L.c0 = 0.0; L.b1b = R[R_BULK1] * baryon; L.d0b = R[R_DIFF1] * baryon;
+    // S = N / E + L:  N = p.pi.p - bulk2 m^2 - d b (W - V.p),  L = (bulk0 + bulk2) E + b1b + diff0 (W - V.p)
+    const double bsum = R[R_BULK0] + R[R_BULK2];
+    const double b1b = R[R_BULK1] * baryon, d0b = R[R_DIFF1] * baryon, diff0 = R[R_DIFF0];
+    L.S0 = q1 - R[R_BULK2] * m2 - d0b * mW;
+    L.Sc = Pc + d0b * Vx; L.Ss = Ps + d0b * Vy;
+    L.L0 = bsum * EA + b1b + diff0 * mW;
+    L.Lc = -bsum * ux - diff0 * Vx; L.Ls = -bsum * uy - diff0 * Vy;
+  } else if (flavor == SEP_PTB) {
+    // delta-f = (1 - sign feq)(N / E + L) + c0:  N = p.pi.p - dlam m^2 / T,  L = dlam E / T
+    const double dl = R[R_DLAM] * R[R_INVT];
+    L.S0 = q1 - dl * m2; L.Sc = Pc; L.Ss = Ps;
+    L.L0 = dl * EA; L.Lc = -dl * ux; L.Ls = -dl * uy;
+    L.c0 = R[R_DZ] - 3.0 * R[R_DLAM];
   } else {
-    L.c0 = R[R_DZ] - 3.0 * R[R_DLAM]; L.b1b = 0.0; L.d0b = 0.0;
+    L.S0 = L.Sc = L.Ss = 0.0;
   }
 }
 
@@ -674,69 +758,61 @@ IS3D_HD double fast_rcp(double d) {
 #endif
 }
 
+IS3D_HD double lin(double c0, double cc, double cs, dbl2 p) { return fma(cc, p.x, fma(cs, p.y, c0)); }
+
 // One separable integrand point; returns w * p.dsigma * f (0 when outflow-cut).
-// FL: separable flavour; REG: regulate_deltaf; OUT: outflow; DIFF: baryon diffusion terms
-// (V^mu = 0 otherwise, so they vanish identically); FAST: exp factorised (see sep_setup).
-template <int FL, bool REG, bool OUT, bool DIFF, bool FAST>
-IS3D_HD double sep_point_t(const double* R, const SepLane& L, const double* PH) {
-  const dbl2 v0 = ((const dbl2*)PH)[0], v1 = ((const dbl2*)PH)[1], v2 = ((const dbl2*)PH)[2];
-  const double phB = v0.x, phPTB = v0.y, phPTDP = v1.x, phPT = v1.y, phPN = v2.x, phQ3 = v2.y;
-  const double pds = L.mTD + L.w * phPTDP;
-  const double E = L.EA - phPTB;
+// FL: separable flavour; REG: regulate_deltaf; OUT: outflow; FAST: exp factorised (see sep_setup).
+template <int FL, bool REG, bool OUT, bool FAST>
+IS3D_HD double sep_point_t(const SepLane& L, dbl2 cs, dbl2 bp) {
+  const double pds = lin(L.D0, L.Dc, L.Ds, cs);
   // feq = 1/(exp(u.p/T - chem) + sign) = b'/(a + sign b'); CE/PTB also need 1/E: one reciprocal
   double feq, iE = 0.0;
+  const bool needE = (FL == SEP_CE || FL == SEP_PTB);
+  const double E = needE ? lin(L.E0, L.Ec, L.Es, cs) : 0.0;
+  // FAST: feq holds e^S feq = b'/(a + ssc b'); the e^-S sits in pds, and 1 - sign feq = 1 - ssc (e^S feq)
   if (FAST) {
-    const double den = fma(L.sign, phB, L.a);
-    if (FL == SEP_CE || FL == SEP_PTB) {
+    const double den = fma(L.ssc, bp.x, L.a);
+    if (needE) {
       const double r = rcp1(den * E);
-      feq = phB * (E * r);
+      feq = bp.x * (E * r);
       iE = den * r;
     } else {
-      feq = phB * rcp1(den);
+      feq = bp.x * rcp1(den);
     }
   } else {
-    feq = 1.0 / (exp(L.x - PH[P_Z]) + L.sign);
-    if (FL == SEP_CE || FL == SEP_PTB) iE = 1.0 / E;
+    feq = 1.0 / (exp(L.x - lin(0.0, L.Zc, L.Zs, cs)) + L.sign);
+    if (needE) iE = 1.0 / E;
   }
-  double f;
-  if (FL == SEP_FEQ) {
-    f = feq;
+  double g = feq * pds;
+  if (OUT) g = (pds <= 0.0) ? 0.0 : g;
+  if (FL == SEP_FEQ) return g;
+  const double fbar = fma(FAST ? -L.ssc : -L.sign, feq, 1.0);
+  double S = fma(L.Sc, cs.x, fma(L.Ss, cs.y, L.S0 + bp.y));
+  if (needE) S = fma(S, iE, lin(L.L0, L.Lc, L.Ls, cs));
+  double t;
+  if (REG) {
+    double dfv = fbar * S;
+    if (FL == SEP_PTB) dfv += L.c0;
+    t = 1.0 + fmax(-1.0, fmin(dfv, 1.0));
   } else {
-    const double fbar = fma(-L.sign, feq, 1.0);
-    const double ppp = fma(L.mch, phPT, fma(L.msh, phPN, L.q1 + phQ3));   // shear * pi.pp (+ c0 for Grad)
-    double dfv;
-    if (FL == SEP_GRAD) {
-      double S = fma(fma(R[R_BULK2], E, L.b1b), E, ppp);
-      if (DIFF) S = fma(fma(R[R_DIFF1], E, L.d0b), L.mW - PH[P_WP], S);
-      dfv = fbar * S;
-    } else if (FL == SEP_CE) {
-      double S = ppp * iE + R[R_BULK0] * E + L.b1b + R[R_BULK2] * (E - L.m2 * iE);
-      if (DIFF) S = fma(R[R_DIFF0] - L.d0b * iE, L.mW - PH[P_WP], S);
-      dfv = fbar * S;
-    } else {   // PTB linearised (:920-923)
-      dfv = fbar * (ppp * iE + R[R_DLAM] * (E - L.m2 * iE) * R[R_INVT]) + L.c0;
-    }
-    if (REG) dfv = fmax(-1.0, fmin(dfv, 1.0));
-    f = fma(feq, dfv, feq);
+    t = fma(fbar, S, (FL == SEP_PTB) ? 1.0 + L.c0 : 1.0);
   }
-  const double r = pds * f;
-  if (OUT) return (pds <= 0.0) ? 0.0 : r;
-  return r;
+  return g * t;
 }
 
-IS3D_HD double sep_point(int flavor, const double* R, const SepLane& L, const double* PH, int regulate, int outflow) {
+IS3D_HD double sep_point(int flavor, const SepLane& L, dbl2 cs, dbl2 bp, int regulate, int outflow) {
 #define IS3D_SEP_CASE(FLV)                                                                               \
   if (flavor == FLV) {                                                                                   \
     if (L.fast) {                                                                                        \
-      if (regulate) return outflow ? sep_point_t<FLV, true, true, true, true>(R, L, PH)                   \
-                                   : sep_point_t<FLV, true, false, true, true>(R, L, PH);                 \
-      return outflow ? sep_point_t<FLV, false, true, true, true>(R, L, PH)                                \
-                     : sep_point_t<FLV, false, false, true, true>(R, L, PH);                              \
+      if (regulate) return outflow ? sep_point_t<FLV, true, true, true>(L, cs, bp)                       \
+                                   : sep_point_t<FLV, true, false, true>(L, cs, bp);                     \
+      return outflow ? sep_point_t<FLV, false, true, true>(L, cs, bp)                                    \
+                     : sep_point_t<FLV, false, false, true>(L, cs, bp);                                  \
     }                                                                                                    \
-    if (regulate) return outflow ? sep_point_t<FLV, true, true, true, false>(R, L, PH)                    \
-                                 : sep_point_t<FLV, true, false, true, false>(R, L, PH);                  \
-    return outflow ? sep_point_t<FLV, false, true, true, false>(R, L, PH)                                 \
-                   : sep_point_t<FLV, false, false, true, false>(R, L, PH);                               \
+    if (regulate) return outflow ? sep_point_t<FLV, true, true, false>(L, cs, bp)                        \
+                                 : sep_point_t<FLV, true, false, false>(L, cs, bp);                      \
+    return outflow ? sep_point_t<FLV, false, true, false>(L, cs, bp)                                     \
+                   : sep_point_t<FLV, false, false, false>(L, cs, bp);                                   \
   }
   IS3D_SEP_CASE(SEP_GRAD)
   IS3D_SEP_CASE(SEP_CE)
@@ -746,16 +822,23 @@ IS3D_HD double sep_point(int flavor, const double* R, const SepLane& L, const do
   return 0.0;
 }
 
+// Modified (PTM/PTB/PTMA) lane: p_mod = mT (ch Uc + sh Us) + (pc Vc + ps Vs)  (MomentumSpectra.cpp:932-982
+// without the iterative refinement, which only changes rounding: A is linear)
 struct ModLane {
-  double mUx, mUy, mUz, mTD, w, m2, invTm, chemm, rn, sign;
+  double mUx, mUy, mUz, D0, Dc, Ds, Vcx, Vsx, Vcy, Vsy, Vcz, Vsz, m2, invTm, chemm, rn, sign;
+  ExpCoef ec;    // pinned once per lane setup, reused by every phi point
   int skip;
 };
 
 IS3D_HD void mod_setup(const double* R, const double* Y, double mT, double m2, double pT, double sign, double baryon,
                        double renorm_abs, ModLane& L) {
   L.mUx = mT * Y[Y_MUX]; L.mUy = mT * Y[Y_MUY]; L.mUz = mT * Y[Y_MUZ];
-  L.mTD = mT * Y[Y_MD]; L.w = Y[Y_WT]; L.m2 = m2; L.sign = sign;
+  const double w = Y[Y_WT];
+  L.D0 = mT * Y[Y_MD]; L.Dc = w * R[R_DAX]; L.Ds = w * R[R_DAY];
+  L.Vcx = R[R_VCX]; L.Vsx = R[R_VSX]; L.Vcy = R[R_VCY]; L.Vsy = R[R_VSY]; L.Vcz = R[R_VCZ]; L.Vsz = R[R_VSZ];
+  L.m2 = m2; L.sign = sign;
   L.invTm = R[R_INVTM]; L.chemm = baryon * R[R_CHEMM]; L.rn = renorm_abs;
+  L.ec = exp_coef();
   // E_mod >= | |mT U| - pT |V|max |; if even that overflows exp, every phi point is exactly 0
   const double mu = sqrt(L.mUx * L.mUx + L.mUy * L.mUy + L.mUz * L.mUz);
   const double lo = mu - pT * R[R_VB];
@@ -763,17 +846,19 @@ IS3D_HD void mod_setup(const double* R, const double* Y, double mT, double m2, d
   L.skip = (emin * L.invTm - L.chemm > kExpMax + 1.0) ? 1 : 0;
 }
 
-IS3D_HD double mod_point(const ModLane& L, const double* PH, int outflow) {
-  const dbl2 v4 = ((const dbl2*)PH)[4];
-  const double qx = L.mUx + v4.x, qy = L.mUy + v4.y, qz = L.mUz + PH[P_VZ];
-  const double Emod = sqrt(L.m2 + qx * qx + qy * qy + qz * qz);
-  const double f = L.rn * fast_rcp(exp(Emod * L.invTm - L.chemm) + L.sign);
-  const double pds = L.mTD + L.w * PH[P_PTDP];
+template <bool OUT>
+IS3D_HD double mod_point_t(const ModLane& L, dbl2 cs) {
+  const double qx = lin(L.mUx, L.Vcx, L.Vsx, cs), qy = lin(L.mUy, L.Vcy, L.Vsy, cs), qz = lin(L.mUz, L.Vcz, L.Vsz, cs);
+  const double Emod = sqrt(fma(qx, qx, fma(qy, qy, fma(qz, qz, L.m2))));
+  const double f = L.rn * fast_rcp(exp_clamped(L.ec, Emod * L.invTm - L.chemm) + L.sign);
+  const double pds = lin(L.D0, L.Dc, L.Ds, cs);
   const double r = pds * f;
-  return (outflow && pds <= 0.0) ? 0.0 : r;
+  return (OUT && pds <= 0.0) ? 0.0 : r;
 }
 
-template <bool OUT>
-IS3D_HD double mod_point_t(const ModLane& L, const double* PH) { return mod_point(L, PH, OUT ? 1 : 0); }
+IS3D_HD double mod_point(const ModLane& L, dbl2 cs, int outflow) {
+  return outflow ? mod_point_t<true>(L, cs) : mod_point_t<false>(L, cs);
+}
 
 }  // namespace is3d
+

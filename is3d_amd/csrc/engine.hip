@@ -35,9 +35,17 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kJmax = 32;     // phi accumulators per lane
-constexpr int kTile = 4;      // cells per LDS tile
-#ifndef IS3D_SPECTRA_WAVES
-#define IS3D_SPECTRA_WAVES 3      // waves per SIMD the spectra kernel is register-allocated for
+#ifndef IS3D_KTILE
+#define IS3D_KTILE 8
+#endif
+constexpr int kTile = IS3D_KTILE;   // cells per LDS tile
+// waves per SIMD the spectra kernel is register-allocated for (measured on MI355X, config2):
+// the separable modes run best at 3 (168 VGPRs), the modified-momentum modes at 2 (no spills)
+#ifndef IS3D_SPECTRA_WAVES_SEP
+#define IS3D_SPECTRA_WAVES_SEP 3
+#endif
+#ifndef IS3D_SPECTRA_WAVES_MOD
+#define IS3D_SPECTRA_WAVES_MOD 2
 #endif
 
 struct DevTables {            // device copy of the delta-f tables (pointers into one blob)
@@ -51,7 +59,7 @@ struct PrepArgs {
   PrepConsts k;
   DfTables tb;
   const double* surf;   // [NSURF][n]
-  double* rec;          // [NREC][n]
+  double* rec;          // [n][NREC]
   double* aux;          // PTM/PTB: [9][n]; PTMA: [9][n] Newton inputs
   long n;
   int* err;
@@ -86,8 +94,9 @@ __global__ __launch_bounds__(256) void k_prep(PrepArgs A) {
     for (int f = 0; f < 9; f++) A.aux[(long)f * A.n + c] = ain[f];
   }
   if (err) { atomicMax(A.err, err); R[R_KIND] = 0.0; }
+  R[R_PAD] = 0.0;
 #pragma unroll
-  for (int f = 0; f < NREC; f++) A.rec[(long)f * A.n + c] = R[f];
+  for (int f = 0; f < NREC; f++) A.rec[c * NREC + f] = R[f];
 }
 
 struct WaveSum {
@@ -99,7 +108,7 @@ struct WaveSum {
 };
 
 struct AnisoArgs {
-  const double* rec; const double* ain; double* sol;   // sol [6][n]
+  const double* rec; const double* ain; double* sol;   // rec [n][NREC], sol [6][n]
   long n, chains;
   Hadrons h;
   double fp2;
@@ -113,7 +122,7 @@ __global__ __launch_bounds__(64) void k_aniso(AnisoArgs A) {
   double state[4] = {0.0, 0.0, 0.0, 0.0};
   long cnt[3] = {0, 0, 0};
   for (long c = chain; c < A.n; c += A.chains) {
-    if (A.rec[(long)R_KIND * A.n + c] == 0.0) continue;
+    if (A.rec[c * NREC + R_KIND] == 0.0) continue;
     double ain[4];
 #pragma unroll
     for (int f = 0; f < 4; f++) ain[f] = A.ain[(long)f * A.n + c];
@@ -134,10 +143,10 @@ __global__ __launch_bounds__(64) void k_aniso(AnisoArgs A) {
 __global__ __launch_bounds__(256) void k_famod_b(PrepArgs A, const double* sol) {
   const long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= A.n) return;
-  if (A.rec[(long)R_KIND * A.n + c] == 0.0) return;
+  if (A.rec[c * NREC + R_KIND] == 0.0) return;
   double R[NREC], ain[9], so[6];
 #pragma unroll
-  for (int f = 0; f < NREC; f++) R[f] = A.rec[(long)f * A.n + c];
+  for (int f = 0; f < NREC; f++) R[f] = A.rec[c * NREC + f];
 #pragma unroll
   for (int f = 0; f < 9; f++) ain[f] = A.aux[(long)f * A.n + c];
 #pragma unroll
@@ -146,7 +155,7 @@ __global__ __launch_bounds__(256) void k_famod_b(PrepArgs A, const double* sol) 
   prep_famod_b(A.k, R, ain, so, &broken);
   if (broken) atomicAdd(&A.cnt[0], 1ull);
 #pragma unroll
-  for (int f = 0; f < NREC; f++) A.rec[(long)f * A.n + c] = R[f];
+  for (int f = 0; f < NREC; f++) A.rec[c * NREC + f] = R[f];
 }
 
 struct RenormArgs {
@@ -161,7 +170,7 @@ __global__ __launch_bounds__(256) void k_renorm(RenormArgs A) {
   if (idx >= A.n * A.npart) return;
   const long c = idx / A.npart;
   const int s = (int)(idx % A.npart);
-  if (A.rec[(long)R_KIND * A.n + c] == 0.0) { A.renorm[idx] = 0.0; return; }
+  if (A.rec[c * NREC + R_KIND] == 0.0) { A.renorm[idx] = 0.0; return; }
   double aux[9];
 #pragma unroll
   for (int f = 0; f < 9; f++) aux[f] = A.aux[(long)f * A.n + c];
@@ -184,24 +193,75 @@ struct SpecArgs {
 };
 
 // flag bits of the spectra kernel instantiation
-constexpr int F_REG = 1, F_OUT = 2, F_DIFF = 4;
+constexpr int F_REG = 1, F_OUT = 2;
 
+// 32 phi points of one lane; the next point's two LDS pairs are loaded before the current
+// point is evaluated so the LDS latency overlaps the FP64 chain
 template <int MODE, int FLAGS, bool FAST>
-__device__ __forceinline__ void sep_phi_loop(const double* R, const SepLane& L, const double* PHc, int j0, double* acc) {
+__device__ __forceinline__ void sep_phi_loop(const SepLane& L, const dbl2* CS, const dbl2* BP, double* acc) {
   constexpr int FL = (MODE == GRAD) ? SEP_GRAD : (MODE == CE || MODE == PTM) ? SEP_CE : (MODE == PTB) ? SEP_PTB : SEP_FEQ;
+  dbl2 c = CS[0], b = BP[0];
 #pragma unroll
-  for (int jj = 0; jj < kJmax; jj++)   // phi rows are padded to a multiple of kJmax: no per-point guard
-    acc[jj] += sep_point_t<FL, (FLAGS & F_REG) != 0, (FLAGS & F_OUT) != 0, (FLAGS & F_DIFF) != 0, FAST>(
-        R, L, PHc + (j0 + jj) * NPT);
+  for (int jj = 0; jj < kJmax; jj++) {   // phi rows are padded to a multiple of kJmax: no per-point guard
+    dbl2 cn = c, bn = b;
+    if (jj + 1 < kJmax) { cn = CS[jj + 1]; bn = BP[jj + 1]; }
+    acc[jj] += sep_point_t<FL, (FLAGS & F_REG) != 0, (FLAGS & F_OUT) != 0, FAST>(L, c, b);
+    c = cn; b = bn;
+  }
 }
 
+template <int FLAGS>
+__device__ __forceinline__ void mod_phi_loop(const ModLane& M, const dbl2* CS, double* acc) {
+  dbl2 c = CS[0];
+#pragma unroll
+  for (int jj = 0; jj < kJmax; jj++) {
+    dbl2 cn = c;
+    if (jj + 1 < kJmax) cn = CS[jj + 1];
+    acc[jj] += mod_point_t<(FLAGS & F_OUT) != 0>(M, c);
+    c = cn;
+  }
+}
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations (lgkmcnt) but
+// not for its outstanding global loads -- a __syncthreads() (or a workgroup release fence) would
+// also wait for vmcnt(0) and drain the next tile's record copy.  The empty asm statements with a
+// memory clobber keep the compiler from moving LDS accesses across the barrier.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// dbl2 pairs of one record tile (kTile consecutive records of NREC doubles)
+constexpr int kTilePairs = kTile * NREC / 2;
+
+// Async copy of the record tile starting at cell cb into LDS (global_load_lds_dwordx4: no VGPR
+// staging; the LDS destination of a wave-instruction is base + 16 * lane, so the tile lands
+// in the same linear order as the records in HBM).  Completion is tracked by vmcnt.
+__device__ __forceinline__ void fetch_tile(const double* rec, long cb, long c_end, double* dst) {
+  const int tid = threadIdx.x;
+  const long lim = (min(c_end, cb + kTile) - cb) * (NREC / 2);
+  for (int base = 0; base < kTilePairs; base += kBlock) {
+    const int e = base + tid;
+    const int wave0 = base + (tid & ~63);
+    if (e < lim)
+      __builtin_amdgcn_global_load_lds((const void*)(rec + (cb * (NREC / 2) + e) * 2),
+                                       (__attribute__((address_space(3))) void*)(dst + 2 * wave0), 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ void wait_fetch() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
 template <int MODE, int FLAGS>
-__global__ __launch_bounds__(kBlock, IS3D_SPECTRA_WAVES) void k_spectra(SpecArgs A) {
+__global__ __launch_bounds__(kBlock, MODE >= PTM ? IS3D_SPECTRA_WAVES_MOD : IS3D_SPECTRA_WAVES_SEP) void k_spectra(SpecArgs A) {
   extern __shared__ double smem[];
-  double* s_rec = smem;                                   // [kTile][NREC]
-  double* s_phi = s_rec + kTile * NREC;                   // [kTile][nphi][NPT]
   const int nphp = A.njb * kJmax;                         // phi rows padded to kJmax multiples
-  double* s_y = s_phi + (long)kTile * nphp * NPT;         // [kTile][nq][NYT]
+  double* s_recb = smem;                                  // [2][kTile][NREC] double-buffered
+  dbl2* s_trig = (dbl2*)(s_recb + 2 * kTile * NREC);      // [nphp]        {cos, sin}
+  dbl2* s_cs = s_trig + nphp;                             // [nphp]        {pT cos, pT sin}
+  dbl2* s_bp = s_cs + nphp;                               // [kTile][nphp] {b', Phi}
+  double* s_grid = (double*)(s_bp + kTile * nphp);        // y[nk] | eta[nl] | eta_w[nl]
+  double* s_y = s_grid + A.nk + 2 * A.nl;                 // [kTile][nq][NYT]
 
   const int tid = threadIdx.x;
   const int ipt = blockIdx.y;
@@ -220,6 +280,22 @@ __global__ __launch_bounds__(kBlock, IS3D_SPECTRA_WAVES) void k_spectra(SpecArgs
   const double mass = A.smass[s], m2 = mass * mass, sign = A.ssign[s], baryon = A.sbaryon[s];
   const double mT = sqrt(m2 + pT * pT);
 
+  // per-workgroup constants into LDS: inside the cell loop the only global loads are the
+  // record prefetch (and PTM's renormalisation factor)
+  for (int j = tid; j < nphp; j += kBlock) {
+    const bool in = j < A.nphi;
+    const double c = in ? A.cphi[j] : 0.0, sn = in ? A.sphi[j] : 0.0;
+    dbl2 v; v.x = c; v.y = sn;
+    s_trig[j] = v;
+    v.x = pT * c; v.y = pT * sn;
+    s_cs[j] = v;
+  }
+  for (int i = tid; i < A.nk; i += kBlock) s_grid[i] = (A.dim == 3) ? A.yv[i] : 0.0;
+  for (int i = tid; i < A.nl; i += kBlock) {
+    s_grid[A.nk + i] = (A.dim == 3) ? 0.0 : A.etav[i];
+    s_grid[A.nk + A.nl + i] = (A.dim == 3) ? 1.0 : A.etaw[i];
+  }
+
   double acc[kJmax];
 #pragma unroll
   for (int jj = 0; jj < kJmax; jj++) acc[jj] = 0.0;
@@ -227,36 +303,37 @@ __global__ __launch_bounds__(kBlock, IS3D_SPECTRA_WAVES) void k_spectra(SpecArgs
   const long c_begin = (long)blockIdx.z * A.cells_per_split;
   const long c_end = min(A.n, c_begin + A.cells_per_split);
 
-  for (long cb = c_begin; cb < c_end; cb += kTile) {
+  // record tiles: tile i lives in buffer i & 1; tile i + 1 is copied in while tile i is integrated
+  if (c_begin < c_end) fetch_tile(A.rec, c_begin, c_end, s_recb);
+  int buf = 0;
+  for (long cb = c_begin; cb < c_end; cb += kTile, buf ^= 1) {
     const int nt = (int)min((long)kTile, c_end - cb);
-    for (int idx = tid; idx < kTile * NREC; idx += kBlock) {
-      const int f = idx / kTile, t = idx % kTile;
-      s_rec[t * NREC + f] = (t < nt) ? A.rec[(long)f * A.n + cb + t] : 0.0;
-    }
-    __syncthreads();
+    double* s_rec = s_recb + buf * (kTile * NREC);
+    wait_fetch();
+    lds_barrier();     // tile cb visible to all waves; everyone is done with the previous tile
+    if (cb + kTile < c_end) fetch_tile(A.rec, cb + kTile, c_end, s_recb + (buf ^ 1) * (kTile * NREC));
     for (int idx = tid; idx < nt * nphp; idx += kBlock) {
       const int t = idx / nphp, j = idx % nphp;
       const double* R = s_rec + t * NREC;
-      double* PH = s_phi + ((long)t * nphp + j) * NPT;
-      if (j >= A.nphi) {
-#pragma unroll
-        for (int f = 0; f < NPT; f++) PH[f] = 0.0;         // padding: finite, never written out
-      } else if (R[R_KIND] != 0.0) {
-        phiterms(MODE, R, pT, A.cphi[j], A.sphi[j], PH);
+      dbl2 v; v.x = 0.0; v.y = 0.0;                        // padding: finite, never written out
+      if (j < A.nphi && R[R_KIND] != 0.0) {
+        const dbl2 tr = s_trig[j];
+        v = phiterms(MODE, R, pT, tr.x, tr.y);
       }
+      s_bp[t * nphp + j] = v;
     }
     for (int idx = tid; idx < nt * A.nq; idx += kBlock) {
       const int t = idx / A.nq, q = idx % A.nq;
       const double* R = s_rec + t * NREC;
       if (R[R_KIND] != 0.0) {
         const int kk = q / A.nl, l = q % A.nl;
-        const double y = (A.dim == 3) ? A.yv[kk] : 0.0;
-        const double eta = (A.dim == 3) ? R[R_ETA] : A.etav[l];
-        const double w = (A.dim == 3) ? 1.0 : A.etaw[l];
+        const double y = s_grid[kk];
+        const double eta = (A.dim == 3) ? R[R_ETA] : s_grid[A.nk + l];
+        const double w = s_grid[A.nk + A.nl + l];
         yterms(MODE, R, y, eta, w, s_y + ((long)t * A.nq + q) * NYT);
       }
     }
-    __syncthreads();
+    lds_barrier();
     if (active) {
       for (int t = 0; t < nt; t++) {
         const double* R = s_rec + t * NREC;
@@ -268,7 +345,7 @@ __global__ __launch_bounds__(kBlock, IS3D_SPECTRA_WAVES) void k_spectra(SpecArgs
           if (!isfinite(rn)) continue;    // species skipped (MomentumSpectra.cpp:828-832)
           rn_abs = fabs(rn);
         }
-        const double* PHc = s_phi + (long)t * nphp * NPT;
+        const dbl2* BP = s_bp + t * nphp + j0;
         for (int l = 0; l < A.nl; l++) {
           const int q = k * A.nl + l;
           const double* Y = s_y + ((long)t * A.nq + q) * NYT;
@@ -277,19 +354,17 @@ __global__ __launch_bounds__(kBlock, IS3D_SPECTRA_WAVES) void k_spectra(SpecArgs
             SepLane L;
             sep_setup(sep_flavor(MODE), R, Y, mT, m2, pT, sign, baryon, L);
             if (L.skip) continue;
-            if (L.fast) sep_phi_loop<MODE, FLAGS, true>(R, L, PHc, j0, acc);
-            else sep_phi_loop<MODE, FLAGS, false>(R, L, PHc, j0, acc);
+            if (L.fast) sep_phi_loop<MODE, FLAGS, true>(L, s_cs + j0, BP, acc);
+            else sep_phi_loop<MODE, FLAGS, false>(L, s_cs + j0, BP, acc);
           } else if (MODE >= PTM) {
             ModLane M;
             mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, M);
             if (M.skip) continue;
-#pragma unroll
-            for (int jj = 0; jj < kJmax; jj++) acc[jj] += mod_point_t<(FLAGS & F_OUT) != 0>(M, PHc + (j0 + jj) * NPT);
+            mod_phi_loop<FLAGS>(M, s_cs + j0, acc);
           }
         }
       }
     }
-    __syncthreads();
   }
   if (active) {
     double* out = A.slab + (long)blockIdx.z * A.outsize;
@@ -657,11 +732,7 @@ static void launch_spectra(dim3 grid, size_t shmem, hipStream_t st, const SpecAr
     case 0: hipLaunchKernelGGL((k_spectra<MODE, 0>), grid, dim3(kBlock), shmem, st, a); break;
     case 1: hipLaunchKernelGGL((k_spectra<MODE, 1>), grid, dim3(kBlock), shmem, st, a); break;
     case 2: hipLaunchKernelGGL((k_spectra<MODE, 2>), grid, dim3(kBlock), shmem, st, a); break;
-    case 3: hipLaunchKernelGGL((k_spectra<MODE, 3>), grid, dim3(kBlock), shmem, st, a); break;
-    case 4: hipLaunchKernelGGL((k_spectra<MODE, 4>), grid, dim3(kBlock), shmem, st, a); break;
-    case 5: hipLaunchKernelGGL((k_spectra<MODE, 5>), grid, dim3(kBlock), shmem, st, a); break;
-    case 6: hipLaunchKernelGGL((k_spectra<MODE, 6>), grid, dim3(kBlock), shmem, st, a); break;
-    default: hipLaunchKernelGGL((k_spectra<MODE, 7>), grid, dim3(kBlock), shmem, st, a); break;
+    default: hipLaunchKernelGGL((k_spectra<MODE, 3>), grid, dim3(kBlock), shmem, st, a); break;
   }
 }
 
@@ -748,11 +819,11 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   sa.npart = np; sa.npT = npT; sa.nphi = nphi; sa.ny_out = ny_out; sa.nk = nk; sa.nl = nl; sa.nq = nk * nl; sa.njb = njb;
   sa.ntask = ntask; sa.cells_per_split = cps;
   sa.regulate = e->p.regulate_deltaf; sa.outflow = e->p.outflow; sa.dim = dim;
-  const size_t shmem = sizeof(double) * ((size_t)kTile * NREC + (size_t)kTile * njb * kJmax * NPT + (size_t)kTile * sa.nq * NYT);
+  const size_t shmem = sizeof(double) * (2 * (size_t)kTile * NREC + 2 * (size_t)(kTile + 2) * njb * kJmax + (size_t)(nk + 2 * nl) +
+                                         (size_t)kTile * sa.nq * NYT);
   if (shmem > 160 * 1024) return e->fail(IS3D_ERR_ARG, "momentum grid too large for the LDS tile");
   const dim3 grid((unsigned)bx, (unsigned)npT, (unsigned)nsplit);
-  const int diff = (e->p.include_baryon && e->p.include_baryondiff_deltaf && mode <= PTM) ? F_DIFF : 0;
-  const int kflags = (e->p.regulate_deltaf ? F_REG : 0) | (e->p.outflow ? F_OUT : 0) | diff;
+  const int kflags = (e->p.regulate_deltaf ? F_REG : 0) | (e->p.outflow ? F_OUT : 0);
   switch (mode) {
     case GRAD: launch_spectra<GRAD>(grid, shmem, st, sa, kflags); break;
     case CE: launch_spectra<CE>(grid, shmem, st, sa, kflags); break;

@@ -104,7 +104,8 @@ extern "C" int emu_spectra(const orc_params* p, const orc_setup* su, const orc_s
   std::vector<double> cph(nphi), sph(nphi);
   for (int j = 0; j < nphi; j++) { cph[j] = cos(su->phi[j]); sph[j] = sin(su->phi[j]); }
   const int nq = nk * nl;
-  std::vector<double> Yall((size_t)nq * NYT), PHall((size_t)nphi * NPT);
+  std::vector<double> Yall((size_t)nq * NYT);
+  std::vector<dbl2> CS(nphi), BP(nphi);
   std::vector<double> acc((size_t)np * nk * nphi);
   for (int i = 0; i < npT; i++) {
     const double pT = su->pT[i];
@@ -113,7 +114,10 @@ extern "C" int emu_spectra(const orc_params* p, const orc_setup* su, const orc_s
       const double* R = &rec[(size_t)c * NREC];
       const double kind = R[R_KIND];
       if (kind == 0.0) continue;
-      for (int j = 0; j < nphi; j++) phiterms(mode, R, pT, cph[j], sph[j], &PHall[(size_t)j * NPT]);
+      for (int j = 0; j < nphi; j++) {
+        CS[j].x = pT * cph[j]; CS[j].y = pT * sph[j];
+        BP[j] = phiterms(mode, R, pT, cph[j], sph[j]);
+      }
       for (int q = 0; q < nq; q++) {
         const int kk = q / nl, l = q % nl;
         const double y = (dim == 3) ? su->y[kk] : 0.0;
@@ -140,12 +144,12 @@ extern "C" int emu_spectra(const orc_params* p, const orc_setup* su, const orc_s
               sep_setup(sep_flavor(mode), R, Y, mT, m2, pT, sign, baryon, L);
               if (L.skip) continue;
               for (int j = 0; j < nphi; j++)
-                a[j] += sep_point(sep_flavor(mode), R, L, &PHall[(size_t)j * NPT], p->regulate_deltaf, p->outflow);
+                a[j] += sep_point(sep_flavor(mode), L, CS[j], BP[j], p->regulate_deltaf, p->outflow);
             } else {
               ModLane M;
               mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, M);
               if (M.skip) continue;
-              for (int j = 0; j < nphi; j++) a[j] += mod_point(M, &PHall[(size_t)j * NPT], p->outflow);
+              for (int j = 0; j < nphi; j++) a[j] += mod_point(M, CS[j], p->outflow);
             }
           }
         }
@@ -158,4 +162,10 @@ extern "C" int emu_spectra(const orc_params* p, const orc_setup* su, const orc_s
   }
   if (stats) { stats[0] = st_break; stats[1] = st_pl; stats[2] = st_fail; stats[3] = st_it; }
   return 0;
+}
+
+// the device exp used by the spectra kernel (exp_dom690 / exp_clamped), evaluated on the host
+extern "C" void emu_exp(const double* x, long n, double* out) {
+  const ExpCoef E = exp_coef();
+  for (long i = 0; i < n; i++) out[i] = exp_clamped(E, x[i]);
 }

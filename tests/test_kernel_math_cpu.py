@@ -48,3 +48,22 @@ def test_ptma_chains_match_reference_thread_count():
         got, st2 = emu_spectra(spec, s, chains=C)
         assert parity(got, ref)[0] < 1e-9
         assert st[3] == st2[3]        # identical Newton iteration counts
+
+
+def test_kernel_exp_accuracy():
+    """exp_dom690/exp_clamped (cf_math.h) against libm exp: <= 2 ulp over the fast-path domain,
+    saturation to +inf past the overflow point, exact zero far below underflow."""
+    import ctypes as C
+    from helpers import emulator
+    lib = emulator()
+    rng = np.random.default_rng(3)
+    x = np.concatenate([rng.uniform(-690, 690, 200000), rng.uniform(-2, 2, 100000),
+                        np.array([0.0, 1e-300, -1e-300, 690.0, -690.0, 709.78, 709.79, 800.0, -746.0, -1e6, 1e6])])
+    out = np.empty_like(x)
+    lib.emu_exp(x.ctypes.data_as(C.POINTER(C.c_double)), C.c_long(len(x)), out.ctypes.data_as(C.POINTER(C.c_double)))
+    ref = np.exp(x)
+    fin = np.isfinite(ref) & (np.abs(x) <= 700)
+    ulp = np.abs(out[fin] - ref[fin]) / np.spacing(ref[fin])
+    assert ulp.max() <= 2.0, ulp.max()
+    assert np.isinf(out[x >= 709.79]).all()
+    assert (out[x <= -746.0] == 0.0).all()

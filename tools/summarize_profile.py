@@ -1,0 +1,76 @@
+#!/usr/bin/env python3
+"""Fold a tools/profile_round.sh output directory into committed summaries under profiles/.
+
+  profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (verbatim)
+  profiles/<tag>_pmc.json           per-kernel averages of the PMC passes
+  profiles/pmc_traffic.json         HBM bytes per k_spectra launch, keyed "<config>_mode<m>",
+                                    read by bench.py for roofline.traffic
+
+HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (KiB -> B): on gfx950 FETCH_SIZE counts
+half the bytes of wide coalesced reads (MI355X_MICROARCH.md, HBM section); WRITE_SIZE is exact
+for 16-B-per-lane stores, which is what k_spectra's slab stores are.
+usage: summarize_profile.py <prof_dir> <tag> <config> <df_mode>
+"""
+import csv
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def short(name):
+    for k in ("k_spectra", "k_reduce", "k_prep", "k_aniso", "k_famod_b", "k_renorm", "k_df_eval"):
+        if k in name:
+            return name[name.index(k):].split("(")[0]
+    return name.split("(")[0][:60]
+
+
+def counters(path):
+    acc = defaultdict(lambda: defaultdict(list))
+    dur = defaultdict(list)
+    seen = set()
+    for r in csv.DictReader(open(path)):
+        k = short(r["Kernel_Name"])
+        acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        if r["Dispatch_Id"] not in seen:
+            seen.add(r["Dispatch_Id"])
+            dur[k].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    return acc, dur
+
+
+def main():
+    d, tag, config, mode = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4])
+    prof = os.path.join(ROOT, "profiles")
+    os.makedirs(prof, exist_ok=True)
+    shutil.copy(os.path.join(d, "trace", "run_kernel_stats.csv"), os.path.join(prof, "%s_kernel_stats.csv" % tag))
+    out = {}
+    for sub in ("pmcA", "pmcB", "pmcC"):
+        p = os.path.join(d, sub, "run_counter_collection.csv")
+        if not os.path.exists(p):
+            continue
+        acc, dur = counters(p)
+        for k, cs in acc.items():
+            e = out.setdefault(k, {})
+            for c, v in cs.items():
+                e[c] = sum(v) / len(v)
+            e.setdefault("launches", len(dur[k]))
+            e.setdefault("avg_ns_pmc_pass", sum(dur[k]) / len(dur[k]))
+    for k, e in out.items():
+        if "FETCH_SIZE" in e and "WRITE_SIZE" in e:
+            e["hbm_bytes_per_launch"] = (2.0 * e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024.0
+    json.dump(out, open(os.path.join(prof, "%s_pmc.json" % tag), "w"), indent=1, sort_keys=True)
+    spec = [k for k in out if k.startswith("k_spectra")]
+    if spec and "hbm_bytes_per_launch" in out[spec[0]]:
+        tp = os.path.join(prof, "pmc_traffic.json")
+        t = json.load(open(tp)) if os.path.exists(tp) else {}
+        t["%s_mode%d" % (config, mode)] = out[spec[0]]["hbm_bytes_per_launch"]
+        json.dump(t, open(tp, "w"), indent=1, sort_keys=True)
+    for k, e in sorted(out.items()):
+        print(k, {c: round(v, 3) for c, v in e.items()})
+
+
+if __name__ == "__main__":
+    main()
