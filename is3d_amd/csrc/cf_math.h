@@ -104,9 +104,9 @@ enum Rec : int {
   R_SHEAR, R_BULK0, R_BULK1, R_BULK2, R_DIFF0, R_DIFF1, R_DLAM, R_DZ,
   R_ETASCALE, R_DET, R_NARROW, R_RENORM, R_ZB, R_VB,
   R_UCX, R_UCY, R_UCZ, R_USX, R_USY, R_USZ, R_VCX, R_VCY, R_VCZ, R_VSX, R_VSY, R_VSZ,
-  R_PAD,        // NREC even: a record is a whole number of 16-byte pairs
   NREC
 };
+static_assert(NREC % 2 == 0, "records are moved as 16-byte pairs: keep NREC even");
 
 // y-term layout (per cell, q); phi-terms are dbl2 pairs, see phiterms
 enum YT : int { Y_A = 0, Y_D, Y_Q1, Y_CH, Y_SH, Y_W, Y_WT, Y_MUX, Y_MUY, Y_MUZ, Y_MD, Y_NARROW, NYT };

@@ -94,7 +94,6 @@ __global__ __launch_bounds__(256) void k_prep(PrepArgs A) {
     for (int f = 0; f < 9; f++) A.aux[(long)f * A.n + c] = ain[f];
   }
   if (err) { atomicMax(A.err, err); R[R_KIND] = 0.0; }
-  R[R_PAD] = 0.0;
 #pragma unroll
   for (int f = 0; f < NREC; f++) A.rec[c * NREC + f] = R[f];
 }

@@ -114,3 +114,46 @@ def test_jonah_table_matches_oracle():
     np.testing.assert_allclose(z, zr, rtol=1e-15)
     np.testing.assert_allclose(bp, bpr, rtol=1e-13, atol=1e-15)
     assert abs(mx - mxr) < 1e-14
+
+
+def _config2(mode=1, n=100000):
+    s = synth.as_read(synth.surface(n, seed=7, dimension=3, full3d=True))
+    spec = make_spec(hrg_eos=2, chosen="smash", df_mode=mode, dimension=3, pT="pT48", phi="phi32", y="y21")
+    return spec, s
+
+
+def _rel(a, b):
+    m = np.abs(b) > 1e-290
+    return float((np.abs(a[m] - b[m]) / np.abs(b[m])).max())
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_full_size_properties(mode):
+    """BASELINE config 2 at full size (10^5 cells x 444 species x 48 x 32 x 21), where the oracle
+    would take hours: the spectrum is a sum over cells, so it must be additive over a cell split
+    and invariant under a cell permutation (to summation-order rounding), and p.dsigma enters
+    linearly, so doubling dsigma_mu must double every (normal-range) entry bit for bit."""
+    spec, s = _config2(mode)
+    e = build_engine(spec, s)
+    full = e.calculate_spectra()
+    n = len(s["tau"])
+    h = n // 2 + 12345
+    e.set_surface({k: np.ascontiguousarray(v[:h]) for k, v in s.items()})
+    a = e.calculate_spectra()
+    e.set_surface({k: np.ascontiguousarray(v[h:]) for k, v in s.items()})
+    b = e.calculate_spectra()
+    perm = np.random.default_rng(1).permutation(n)
+    e.set_surface({k: np.ascontiguousarray(v[perm]) for k, v in s.items()})
+    p = e.calculate_spectra()
+    s2 = dict(s)
+    for k in ("dat", "dax", "day", "dan"):
+        s2[k] = 2.0 * s[k]
+    e.set_surface(s2)
+    d = e.calculate_spectra()
+    e.close()
+    assert np.isfinite(full).all() and (full != 0).sum() > 0.5 * full.size
+    assert _rel(a + b, full) < 1e-11
+    assert _rel(p, full) < 1e-11
+    m = np.abs(full) > 1e-290          # below that, subnormal products round on an absolute grid
+    assert np.array_equal(d[m], 2.0 * full[m])
+    assert np.abs(d[~m] - 2.0 * full[~m]).max(initial=0.0) <= 1e-300
