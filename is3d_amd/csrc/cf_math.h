@@ -104,12 +104,18 @@ enum Rec : int {
   R_SHEAR, R_BULK0, R_BULK1, R_BULK2, R_DIFF0, R_DIFF1, R_DLAM, R_DZ,
   R_ETASCALE, R_DET, R_NARROW, R_RENORM, R_ZB, R_VB,
   R_UCX, R_UCY, R_UCZ, R_USX, R_USY, R_USZ, R_VCX, R_VCY, R_VCZ, R_VSX, R_VSY, R_VSZ,
+  // species-independent pieces of the separable lane coefficients (sep_cell_consts)
+  R_S0M2, R_SCB, R_SSB, R_L0B, R_LC, R_LS,
   NREC
 };
 static_assert(NREC % 2 == 0, "records are moved as 16-byte pairs: keep NREC even");
 
 // y-term layout (per cell, q); phi-terms are dbl2 pairs, see phiterms
-enum YT : int { Y_A = 0, Y_D, Y_Q1, Y_CH, Y_SH, Y_W, Y_WT, Y_MUX, Y_MUY, Y_MUZ, Y_MD, Y_NARROW, NYT };
+// Y_AT = A/T, Y_A = A (u.p = mT A - pT B), Y_D (p.dsigma = mT D + ...), Y_WDX/Y_WDY = w_eta dsigma_{x,y};
+// Y_S2, Y_S1, Y_SC1, Y_SS1, Y_L1: the (cell, y) factors of the separable lane coefficients
+// (sep_setup); Y_MUX..Y_MD, Y_NARROW: modified-momentum path.  Padded to 16 doubles.
+enum YT : int { Y_AT = 0, Y_A, Y_D, Y_WDX, Y_WDY, Y_S2, Y_S1, Y_SC1, Y_SS1, Y_L1,
+                Y_MUX, Y_MUY, Y_MUZ, Y_MD, Y_NARROW, Y_PAD, NYT };
 
 // surface field order (include/is3d_amd.h, is3d_surface)
 enum Surf : int {
@@ -606,18 +612,66 @@ enum SepFlavor : int { SEP_GRAD = 0, SEP_CE = 1, SEP_PTB = 2, SEP_FEQ = 3 };
 IS3D_HD int sep_flavor(int mode) { return mode == GRAD ? SEP_GRAD : (mode == CE || mode == PTM) ? SEP_CE : mode == PTB ? SEP_PTB : SEP_FEQ; }
 IS3D_HD int quirk_pds(int mode) { return (mode == PTM || mode == PTB) ? 1 : 0; }
 
-// y-terms for (cell R, rapidity y, space-time rapidity eta, weight w)
+// Species- and y-independent pieces of the separable lane coefficients, per cell (record
+// fields R_S0M2 .. R_LS; see yterms / sep_setup for the factorisation).
+IS3D_HD void sep_cell_consts(int mode, double* R) {
+  const int fl = sep_flavor(mode);
+  double s0m2 = 0.0, scb = 0.0, ssb = 0.0, l0b = 0.0, lc = 0.0, ls = 0.0;
+  if (fl == SEP_GRAD) {
+    s0m2 = R[R_BULK0];
+    scb = -(R[R_BULK1] * R[R_UX] + R[R_DIFF0] * R[R_VX]);
+    ssb = -(R[R_BULK1] * R[R_UY] + R[R_DIFF0] * R[R_VY]);
+  } else if (fl == SEP_CE) {
+    const double bsum = R[R_BULK0] + R[R_BULK2];
+    s0m2 = -R[R_BULK2];
+    scb = R[R_DIFF1] * R[R_VX]; ssb = R[R_DIFF1] * R[R_VY];
+    l0b = R[R_BULK1];
+    lc = -bsum * R[R_UX] - R[R_DIFF0] * R[R_VX];
+    ls = -bsum * R[R_UY] - R[R_DIFF0] * R[R_VY];
+  } else if (fl == SEP_PTB) {
+    const double dl = R[R_DLAM] * R[R_INVT];
+    s0m2 = -dl; lc = -dl * R[R_UX]; ls = -dl * R[R_UY];
+  }
+  R[R_S0M2] = s0m2; R[R_SCB] = scb; R[R_SSB] = ssb; R[R_L0B] = l0b; R[R_LC] = lc; R[R_LS] = ls;
+}
+
+// y-terms for (cell R, rapidity y, space-time rapidity eta, weight w).  With
+// ch = cosh(y - eta), sh = sinh(y - eta), p^tau = mT ch, tau p^eta = mT sh:
+//   A = ch u^tau - sh tau u^eta,  D = w (ch dsigma_tau + sh dsigma_eta/tau)   (:304-330)
+//   Q1 = pi^tt ch^2 + tau^2 pi^ee sh^2 - 2 tau pi^te ch sh,  W = V^t ch - tau V^e sh
+// and the separable delta-f coefficients factor as  S0 = mT^2 S2 + mT b S1 + m^2 R_S0M2,
+// Sc = mT SC1 + b R_SCB,  Ss = mT SS1 + b R_SSB,  L0 = mT L1 + b R_L0B  (see sep_setup).
 IS3D_HD void yterms(int mode, const double* R, double y, double eta, double w, double* Y) {
   const int quirk = quirk_pds(mode);
   // separable part: p^tau = mT cosh(y-eta) (Grad/CE: sqrt(1+sinh^2), :307-308)
   const double sh = sinh(y - eta);
   const double ch = (mode <= CE) ? sqrt(1.0 + sh * sh) : cosh(y - eta);
-  Y[Y_A] = ch * R[R_UT] - sh * R[R_TAUUN];
+  const double A = ch * R[R_UT] - sh * R[R_TAUUN];
+  Y[Y_A] = A;
+  Y[Y_AT] = A * R[R_INVT];
   Y[Y_D] = quirk ? (w * ch * R[R_DAT] + sh * R[R_DANT]) : w * (ch * R[R_DAT] + sh * R[R_DANT]);
-  Y[Y_Q1] = R[R_PITT] * ch * ch + R[R_T2PINN] * sh * sh - 2.0 * R[R_TPITN] * ch * sh;
-  Y[Y_CH] = ch; Y[Y_SH] = sh;
-  Y[Y_W] = R[R_VT] * ch - R[R_TVN] * sh;
-  Y[Y_WT] = w;
+  Y[Y_WDX] = w * R[R_DAX]; Y[Y_WDY] = w * R[R_DAY];
+  const double shear = R[R_SHEAR];
+  const double Q1 = R[R_PITT] * ch * ch + R[R_T2PINN] * sh * sh - 2.0 * R[R_TPITN] * ch * sh;
+  const double W = R[R_VT] * ch - R[R_TVN] * sh;
+  // shear p.pi.p linear part: (pc, ps) . 2 shear mT (sh tau pi^{n i} - ch pi^{t i})
+  const double Pc = 2.0 * shear * (sh * R[R_TPIXN] - ch * R[R_PITX]);
+  const double Ps = 2.0 * shear * (sh * R[R_TPIYN] - ch * R[R_PITY]);
+  const int fl = sep_flavor(mode);
+  double S2 = shear * Q1, S1 = 0.0, SC1 = Pc, SS1 = Ps, L1 = 0.0;
+  if (fl == SEP_GRAD) {
+    const double bulk2 = R[R_BULK2], diff1 = R[R_DIFF1];
+    S2 = (bulk2 * A + diff1 * W) * A + shear * Q1;
+    S1 = R[R_BULK1] * A + R[R_DIFF0] * W;
+    SC1 = Pc - (2.0 * bulk2 * A + diff1 * W) * R[R_UX] - diff1 * A * R[R_VX];
+    SS1 = Ps - (2.0 * bulk2 * A + diff1 * W) * R[R_UY] - diff1 * A * R[R_VY];
+  } else if (fl == SEP_CE) {
+    S1 = -R[R_DIFF1] * W;
+    L1 = (R[R_BULK0] + R[R_BULK2]) * A + R[R_DIFF0] * W;
+  } else if (fl == SEP_PTB) {
+    L1 = R[R_DLAM] * R[R_INVT] * A;
+  }
+  Y[Y_S2] = S2; Y[Y_S1] = S1; Y[Y_SC1] = SC1; Y[Y_SS1] = SS1; Y[Y_L1] = L1;
   if (mode >= PTM) {
     const double es = R[R_ETASCALE];
     const double shm = sinh(y - es * eta), chm = cosh(y - es * eta);
@@ -629,6 +683,7 @@ IS3D_HD void yterms(int mode, const double* R, double y, double eta, double w, d
   } else {
     Y[Y_MUX] = Y[Y_MUY] = Y[Y_MUZ] = Y[Y_MD] = Y[Y_NARROW] = 0.0;
   }
+  Y[Y_PAD] = 0.0;
 }
 
 // phi-terms.  Everything the integrand needs per (cell, phi) except two numbers is linear in
@@ -636,7 +691,8 @@ IS3D_HD void yterms(int mode, const double* R, double y, double eta, double w, d
 // modified momentum A^{-1} p all are.  Those linear pieces are folded into per-lane
 // coefficients at sep_setup / mod_setup time, so a point reads only
 //   cs = {pc, ps}        per phi          (shared by every cell of the workgroup)
-//   bp = {b', Phi}       per (cell, phi)  b' = exp(+pT B/T) with B = u^x cos + u^y sin,
+//   bp = {b', Phi}       per (cell, phi)  b' = exp(pT B/T - zb) with B = u^x cos + u^y sin and
+//                                         zb = pT |u_perp|/T its bound over phi (so b' <= 1),
 //                                         Phi = the part of delta-f quadratic in (pc, ps)
 // Grad: Phi = shear p_i pi^{ij} p_j + bulk2 (pT B)^2 + c4 (pT B)(V.p)   (E^2 and E (V.p) cross terms)
 // CE / PTM / PTB (separable): Phi = shear p_i pi^{ij} p_j
@@ -644,7 +700,7 @@ IS3D_HD dbl2 phiterms(int mode, const double* R, double pT, double c, double s) 
   const double PTB = pT * (c * R[R_UX] + s * R[R_UY]);
   const double Q3 = R[R_SHEAR] * (pT * pT * (R[R_PIXX] * c * c + R[R_PIYY] * s * s + 2.0 * R[R_PIXY] * c * s));
   dbl2 o;
-  o.x = exp(PTB / R[R_T]);
+  o.x = exp(PTB / R[R_T] - pT * R[R_ZB]);      // b' e^-zb <= 1, zb = pT |u_perp| / T >= pT B / T
   if (mode == GRAD) {
     const double WP = pT * (R[R_VX] * c + R[R_VY] * s);
     o.y = Q3 + PTB * (R[R_BULK2] * PTB + R[R_DIFF1] * WP);
@@ -663,7 +719,7 @@ static constexpr double kFastMax = 690.0;
 // ---------------------------------------------------------------------------
 // A lin3 is c0 + cc pc + cs ps.
 struct SepLane {
-  double a, ssc, sign;         // a = exp(mT A/T - chem - S), ssc = sign e^-S:  b' / (a + ssc b') = e^S feq
+  double a, ssc, sign;         // a = exp(mT A/T - chem - zb - S), ssc = sign e^-S:  b' / (a + ssc b') = e^S feq
   double D0, Dc, Ds;           // e^-S p.dsigma (x w_eta)
   double S0, Sc, Ss;           // Grad: S (with Phi); CE/PTB: numerator N of the 1/E part (with Phi)
   double E0, Ec, Es;           // CE/PTB: E = u.p
@@ -676,61 +732,36 @@ struct SepLane {
 // Per-(cell, q, species) setup for the separable integrand.  Returns skip=1 when every
 // phi point underflows (exp argument > 709.78 for all phi: contributes exactly 0).
 // The delta-f polynomials (MomentumSpectra.cpp:304-361 Grad, :565-600 CE, :920-923 PTB) are
-// expanded in (pc, ps); see phiterms for the quadratic remainder Phi.
-IS3D_HD void sep_setup(int flavor, const double* R, const double* Y, double mT, double m2, double pT, double sign,
-                       double baryon, SepLane& L) {
+// expanded in (pc, ps); their coefficients factor into (cell, y) terms (yterms), per-cell
+// terms (sep_cell_consts) and the lane's mT, m^2, baryon number b:
+//   Grad  S  = S0 + Phi + Sc pc + Ss ps               delta-f = (1 - sign feq) S
+//   CE    S  = (S0 + Phi + Sc pc + Ss ps) / E + L0 + Lc pc + Ls ps,   E = mT A - ux pc - uy ps
+//   PTB   as CE, delta-f = (1 - sign feq) S + dz - 3 dlambda
+// mT2 = mT * mT and mTb = mT * b are per-lane constants hoisted by the caller.
+IS3D_HD void sep_setup(int flavor, const double* R, const double* Y, double mT, double mT2, double m2, double mTb,
+                       double pT, double sign, double baryon, SepLane& L) {
   L.sign = sign;
-  const double EA = mT * Y[Y_A];
-  L.x = EA * R[R_INVT] - baryon * R[R_CHEM];
+  L.x = fma(mT, Y[Y_AT], -baryon * R[R_CHEM]);
   const double zb = pT * R[R_ZB];                 // >= max_j |pT B_j / T|
   L.skip = (L.x - zb > kExpMax) ? 1 : 0;
-  // fast: a = e^(x-S) and b' = e^z both <= e^690, so a + ssc b' and (a + ssc b') E stay finite.
-  // S = 0 unless x > 600; then S = rint(x) - 600 (an integer, so x - S is exact) keeps the lanes
-  // near the exp-overflow edge on the factorised path instead of the per-point exp path
-  const double S = (L.x > 600.0) ? rint(L.x) - 600.0 : 0.0;
-  L.fast = (L.x >= -kFastMax && zb <= kFastMax && S <= kFastMax) ? 1 : 0;
-  L.a = L.fast ? exp_dom690(L.x - S) : 0.0;
+  // b' carries e^-zb, so a = e^(x - zb - S).  u.p > 0 makes x - zb >= -chem, so without the shift
+  // S the lane's a spans [e^-chem, e^710]; S = rint(x - zb) - 300 (an integer: the subtraction is
+  // exact) for x - zb > 300 keeps every denominator a + ssc b' in ~[1e-2, e^300], so the
+  // product of two of them (paired reciprocals) stays finite and normal
+  const double xs = L.x - zb;
+  const double S = (xs > 300.0) ? rint(xs) - 300.0 : 0.0;
+  L.fast = (xs >= -300.0 && S <= kFastMax) ? 1 : 0;
+  L.a = L.fast ? exp_dom690(xs - S) : 0.0;
   const double esc = (L.fast && S > 0.0) ? exp_dom690(-S) : 1.0;
   L.ssc = sign * esc;
-  L.Zc = R[R_UX] * R[R_INVT]; L.Zs = R[R_UY] * R[R_INVT];
-  const double w = Y[Y_WT];
-  L.D0 = esc * (mT * Y[Y_D]); L.Dc = esc * (w * R[R_DAX]); L.Ds = esc * (w * R[R_DAY]);
-  const double shear = R[R_SHEAR];
-  const double q1 = shear * mT * mT * Y[Y_Q1];
-  const double mch = shear * mT * Y[Y_CH], msh = shear * mT * Y[Y_SH];
-  const double mW = mT * Y[Y_W];
-  const double ux = R[R_UX], uy = R[R_UY], Vx = R[R_VX], Vy = R[R_VY];
-  // shear p.pi.p = q1 + Phi + (pc, ps) . (-2 mch pi^{t i} + 2 msh tau pi^{n i})
-  const double Pc = 2.0 * (msh * R[R_TPIXN] - mch * R[R_PITX]);
-  const double Ps = 2.0 * (msh * R[R_TPIYN] - mch * R[R_PITY]);
-  L.E0 = EA; L.Ec = -ux; L.Es = -uy;
-  L.L0 = L.Lc = L.Ls = 0.0; L.c0 = 0.0;
-  if (flavor == SEP_GRAD) {
-    // S = (bulk2 E + b1b) E + c0 + p.pi.p + (c4 E + c3 b)(W - V.p),  E = EA - PTB, PTB = ux pc + uy ps
-    const double bulk2 = R[R_BULK2], diff1 = R[R_DIFF1];
-    const double b1b = R[R_BULK1] * baryon, d0b = R[R_DIFF0] * baryon;
-    const double kB = -(2.0 * bulk2 * EA + b1b + diff1 * mW);     // coefficient of PTB
-    const double kW = -(diff1 * EA + d0b);                          // coefficient of V.p
-    L.S0 = (bulk2 * EA + b1b) * EA + R[R_BULK0] * m2 + q1 + (diff1 * EA + d0b) * mW;
-    L.Sc = Pc + kB * ux + kW * Vx;
-    L.Ss = Ps + kB * uy + kW * Vy;
-  } else if (flavor == SEP_CE) {
-    // S = N / E + L:  N = p.pi.p - bulk2 m^2 - d b (W - V.p),  L = (bulk0 + bulk2) E + b1b + diff0 (W - V.p)
-    const double bsum = R[R_BULK0] + R[R_BULK2];
-    const double b1b = R[R_BULK1] * baryon, d0b = R[R_DIFF1] * baryon, diff0 = R[R_DIFF0];
-    L.S0 = q1 - R[R_BULK2] * m2 - d0b * mW;
-    L.Sc = Pc + d0b * Vx; L.Ss = Ps + d0b * Vy;
-    L.L0 = bsum * EA + b1b + diff0 * mW;
-    L.Lc = -bsum * ux - diff0 * Vx; L.Ls = -bsum * uy - diff0 * Vy;
-  } else if (flavor == SEP_PTB) {
-    // delta-f = (1 - sign feq)(N / E + L) + c0:  N = p.pi.p - dlam m^2 / T,  L = dlam E / T
-    const double dl = R[R_DLAM] * R[R_INVT];
-    L.S0 = q1 - dl * m2; L.Sc = Pc; L.Ss = Ps;
-    L.L0 = dl * EA; L.Lc = -dl * ux; L.Ls = -dl * uy;
-    L.c0 = R[R_DZ] - 3.0 * R[R_DLAM];
-  } else {
-    L.S0 = L.Sc = L.Ss = 0.0;
-  }
+  if (!L.fast) { L.Zc = R[R_UX] * R[R_INVT]; L.Zs = R[R_UY] * R[R_INVT]; } else { L.Zc = L.Zs = 0.0; }
+  L.D0 = esc * (mT * Y[Y_D]); L.Dc = esc * Y[Y_WDX]; L.Ds = esc * Y[Y_WDY];
+  L.S0 = fma(mT2, Y[Y_S2], fma(mTb, Y[Y_S1], m2 * R[R_S0M2]));
+  L.Sc = fma(mT, Y[Y_SC1], baryon * R[R_SCB]);
+  L.Ss = fma(mT, Y[Y_SS1], baryon * R[R_SSB]);
+  L.E0 = mT * Y[Y_A]; L.Ec = -R[R_UX]; L.Es = -R[R_UY];
+  L.L0 = fma(mT, Y[Y_L1], baryon * R[R_L0B]); L.Lc = R[R_LC]; L.Ls = R[R_LS];
+  L.c0 = (flavor == SEP_PTB) ? R[R_DZ] - 3.0 * R[R_DLAM] : 0.0;
 }
 
 // 1/d for finite normal d: v_rcp_f64 (measured max rel. error 4.5e-8 on gfx950) + one
@@ -760,6 +791,28 @@ IS3D_HD double fast_rcp(double d) {
 
 IS3D_HD double lin(double c0, double cc, double cs, dbl2 p) { return fma(cc, p.x, fma(cs, p.y, c0)); }
 
+// Everything after f_eq for one separable point: returns w * p.dsigma * f_eq (1 + delta-f)
+// (0 when outflow-cut).  feq is e^S f_eq on the fast path (the e^-S sits in pds).
+template <int FL, bool REG, bool OUT, bool FAST>
+IS3D_HD double sep_tail(const SepLane& L, dbl2 cs, dbl2 bp, double pds, double feq, double iE) {
+  const bool needE = (FL == SEP_CE || FL == SEP_PTB);
+  double g = feq * pds;
+  if (OUT) g = (pds <= 0.0) ? 0.0 : g;
+  if (FL == SEP_FEQ) return g;
+  const double fbar = fma(FAST ? -L.ssc : -L.sign, feq, 1.0);
+  double S = fma(L.Sc, cs.x, fma(L.Ss, cs.y, L.S0 + bp.y));
+  if (needE) S = fma(S, iE, lin(L.L0, L.Lc, L.Ls, cs));
+  double t;
+  if (REG) {
+    double dfv = fbar * S;
+    if (FL == SEP_PTB) dfv += L.c0;
+    t = 1.0 + fmax(-1.0, fmin(dfv, 1.0));
+  } else {
+    t = fma(fbar, S, (FL == SEP_PTB) ? 1.0 + L.c0 : 1.0);
+  }
+  return g * t;
+}
+
 // One separable integrand point; returns w * p.dsigma * f (0 when outflow-cut).
 // FL: separable flavour; REG: regulate_deltaf; OUT: outflow; FAST: exp factorised (see sep_setup).
 template <int FL, bool REG, bool OUT, bool FAST>
@@ -783,21 +836,50 @@ IS3D_HD double sep_point_t(const SepLane& L, dbl2 cs, dbl2 bp) {
     feq = 1.0 / (exp(L.x - lin(0.0, L.Zc, L.Zs, cs)) + L.sign);
     if (needE) iE = 1.0 / E;
   }
-  double g = feq * pds;
-  if (OUT) g = (pds <= 0.0) ? 0.0 : g;
-  if (FL == SEP_FEQ) return g;
-  const double fbar = fma(FAST ? -L.ssc : -L.sign, feq, 1.0);
-  double S = fma(L.Sc, cs.x, fma(L.Ss, cs.y, L.S0 + bp.y));
-  if (needE) S = fma(S, iE, lin(L.L0, L.Lc, L.Ls, cs));
-  double t;
-  if (REG) {
-    double dfv = fbar * S;
-    if (FL == SEP_PTB) dfv += L.c0;
-    t = 1.0 + fmax(-1.0, fmin(dfv, 1.0));
+  return sep_tail<FL, REG, OUT, FAST>(L, cs, bp, pds, feq, iE);
+}
+
+// Two fast-path points of one lane with one reciprocal: 1/q0 = q1/(q0 q1), 1/q1 = q0/(q0 q1),
+// q = a + ssc b' (times E for CE/PTB).  sep_setup bounds every q to ~[1e-3, e^310], so
+// q0 q1 is finite and normal.
+template <int FL, bool REG, bool OUT>
+IS3D_HD void sep_pair_t(const SepLane& L, dbl2 c0, dbl2 b0, dbl2 c1, dbl2 b1, double& v0, double& v1) {
+  const bool needE = (FL == SEP_CE || FL == SEP_PTB);
+  const double pds0 = lin(L.D0, L.Dc, L.Ds, c0), pds1 = lin(L.D0, L.Dc, L.Ds, c1);
+  const double den0 = fma(L.ssc, b0.x, L.a), den1 = fma(L.ssc, b1.x, L.a);
+  const double E0 = needE ? lin(L.E0, L.Ec, L.Es, c0) : 1.0, E1 = needE ? lin(L.E0, L.Ec, L.Es, c1) : 1.0;
+  const double q0 = needE ? den0 * E0 : den0, q1 = needE ? den1 * E1 : den1;
+  const double r = rcp1(q0 * q1);
+  const double r0 = r * q1, r1 = r * q0;
+  double feq0, feq1, iE0 = 0.0, iE1 = 0.0;
+  if (needE) {
+    feq0 = b0.x * (E0 * r0); iE0 = den0 * r0;
+    feq1 = b1.x * (E1 * r1); iE1 = den1 * r1;
   } else {
-    t = fma(fbar, S, (FL == SEP_PTB) ? 1.0 + L.c0 : 1.0);
+    feq0 = b0.x * r0; feq1 = b1.x * r1;
   }
-  return g * t;
+  v0 = sep_tail<FL, REG, OUT, true>(L, c0, b0, pds0, feq0, iE0);
+  v1 = sep_tail<FL, REG, OUT, true>(L, c1, b1, pds1, feq1, iE1);
+}
+
+IS3D_HD void sep_pair(int flavor, const SepLane& L, dbl2 c0, dbl2 b0, dbl2 c1, dbl2 b1, int regulate, int outflow,
+                      double& v0, double& v1) {
+#define IS3D_PAIR_CASE(FLV)                                                                       \
+  if (flavor == FLV) {                                                                            \
+    if (regulate) {                                                                               \
+      if (outflow) sep_pair_t<FLV, true, true>(L, c0, b0, c1, b1, v0, v1);                        \
+      else sep_pair_t<FLV, true, false>(L, c0, b0, c1, b1, v0, v1);                               \
+    } else {                                                                                      \
+      if (outflow) sep_pair_t<FLV, false, true>(L, c0, b0, c1, b1, v0, v1);                       \
+      else sep_pair_t<FLV, false, false>(L, c0, b0, c1, b1, v0, v1);                              \
+    }                                                                                             \
+    return;                                                                                       \
+  }
+  IS3D_PAIR_CASE(SEP_GRAD)
+  IS3D_PAIR_CASE(SEP_CE)
+  IS3D_PAIR_CASE(SEP_PTB)
+  IS3D_PAIR_CASE(SEP_FEQ)
+#undef IS3D_PAIR_CASE
 }
 
 IS3D_HD double sep_point(int flavor, const SepLane& L, dbl2 cs, dbl2 bp, int regulate, int outflow) {
@@ -833,8 +915,7 @@ struct ModLane {
 IS3D_HD void mod_setup(const double* R, const double* Y, double mT, double m2, double pT, double sign, double baryon,
                        double renorm_abs, ModLane& L) {
   L.mUx = mT * Y[Y_MUX]; L.mUy = mT * Y[Y_MUY]; L.mUz = mT * Y[Y_MUZ];
-  const double w = Y[Y_WT];
-  L.D0 = mT * Y[Y_MD]; L.Dc = w * R[R_DAX]; L.Ds = w * R[R_DAY];
+  L.D0 = mT * Y[Y_MD]; L.Dc = Y[Y_WDX]; L.Ds = Y[Y_WDY];
   L.Vcx = R[R_VCX]; L.Vsx = R[R_VSX]; L.Vcy = R[R_VCY]; L.Vsy = R[R_VSY]; L.Vcz = R[R_VCZ]; L.Vsz = R[R_VSZ];
   L.m2 = m2; L.sign = sign;
   L.invTm = R[R_INVTM]; L.chemm = baryon * R[R_CHEMM]; L.rn = renorm_abs;

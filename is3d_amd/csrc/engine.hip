@@ -94,6 +94,7 @@ __global__ __launch_bounds__(256) void k_prep(PrepArgs A) {
     for (int f = 0; f < 9; f++) A.aux[(long)f * A.n + c] = ain[f];
   }
   if (err) { atomicMax(A.err, err); R[R_KIND] = 0.0; }
+  if (R[R_KIND] != 0.0) sep_cell_consts(MODE, R);
 #pragma unroll
   for (int f = 0; f < NREC; f++) A.rec[c * NREC + f] = R[f];
 }
@@ -188,23 +189,43 @@ struct SpecArgs {
   int npart, npT, nphi, ny_out, nk, nl, nq, njb;
   long ntask;
   long cells_per_split;
+  int nbx, nsplit;            // lane groups per pT, cell splits (1-D grid of nbx * npT * nsplit)
+  long sstride;               // doubles per slab: npT * nbx * kJmax * kBlock
   int regulate, outflow, dim;
 };
 
 // flag bits of the spectra kernel instantiation
 constexpr int F_REG = 1, F_OUT = 2;
 
-// 32 phi points of one lane; the next point's two LDS pairs are loaded before the current
-// point is evaluated so the LDS latency overlaps the FP64 chain
+#ifndef IS3D_PAIR_RCP
+#define IS3D_PAIR_RCP 1       // fast path: two phi points per reciprocal (sep_pair_t)
+#endif
+
+// 32 phi points of one lane; the next points' LDS pairs are loaded before the current ones are
+// evaluated so the LDS latency overlaps the FP64 chain
 template <int MODE, int FLAGS, bool FAST>
 __device__ __forceinline__ void sep_phi_loop(const SepLane& L, const dbl2* CS, const dbl2* BP, double* acc) {
   constexpr int FL = (MODE == GRAD) ? SEP_GRAD : (MODE == CE || MODE == PTM) ? SEP_CE : (MODE == PTB) ? SEP_PTB : SEP_FEQ;
+  constexpr bool REG = (FLAGS & F_REG) != 0, OUT = (FLAGS & F_OUT) != 0;
+  if (FAST && IS3D_PAIR_RCP) {
+    dbl2 c0 = CS[0], b0 = BP[0], c1 = CS[1], b1 = BP[1];
+#pragma unroll
+    for (int jj = 0; jj < kJmax; jj += 2) {   // phi rows are padded to a multiple of kJmax
+      dbl2 n0 = c0, m0 = b0, n1 = c1, m1 = b1;
+      if (jj + 2 < kJmax) { n0 = CS[jj + 2]; m0 = BP[jj + 2]; n1 = CS[jj + 3]; m1 = BP[jj + 3]; }
+      double v0, v1;
+      sep_pair_t<FL, REG, OUT>(L, c0, b0, c1, b1, v0, v1);
+      acc[jj] += v0; acc[jj + 1] += v1;
+      c0 = n0; b0 = m0; c1 = n1; b1 = m1;
+    }
+    return;
+  }
   dbl2 c = CS[0], b = BP[0];
 #pragma unroll
-  for (int jj = 0; jj < kJmax; jj++) {   // phi rows are padded to a multiple of kJmax: no per-point guard
+  for (int jj = 0; jj < kJmax; jj++) {
     dbl2 cn = c, bn = b;
     if (jj + 1 < kJmax) { cn = CS[jj + 1]; bn = BP[jj + 1]; }
-    acc[jj] += sep_point_t<FL, (FLAGS & F_REG) != 0, (FLAGS & F_OUT) != 0, FAST>(L, c, b);
+    acc[jj] += sep_point_t<FL, REG, OUT, FAST>(L, c, b);
     c = cn; b = bn;
   }
 }
@@ -263,9 +284,17 @@ __global__ __launch_bounds__(kBlock, MODE >= PTM ? IS3D_SPECTRA_WAVES_MOD : IS3D
   double* s_y = s_grid + A.nk + 2 * A.nl;                 // [kTile][nq][NYT]
 
   const int tid = threadIdx.x;
-  const int ipt = blockIdx.y;
+  // XCD-aware block order (cdna_hip_programming.md T1): blocks that share an XCD (same
+  // blockIdx % 8) take one contiguous range of logical ids, and logical ids run split-major, so
+  // each XCD's L2 sees only its own cell splits (sized to fit) instead of every split
+  const long nwg = (long)A.nbx * A.npT * A.nsplit;
+  const long bid = blockIdx.x, q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
+  const long lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int lane_group = (int)(lid % A.nbx);
+  const int ipt = (int)((lid / A.nbx) % A.npT);
+  const int split = (int)(lid / ((long)A.nbx * A.npT));
   const double pT = A.pT[ipt];
-  const long task = (long)blockIdx.x * kBlock + tid;
+  const long task = (long)lane_group * kBlock + tid;
   const bool active = task < A.ntask;
   int s = 0, k = 0, jb = 0;
   if (active) {
@@ -275,9 +304,8 @@ __global__ __launch_bounds__(kBlock, MODE >= PTM ? IS3D_SPECTRA_WAVES_MOD : IS3D
     jb = (int)(r / A.nk);
   }
   const int j0 = jb * kJmax;
-  const int nj = min(kJmax, A.nphi - j0);
   const double mass = A.smass[s], m2 = mass * mass, sign = A.ssign[s], baryon = A.sbaryon[s];
-  const double mT = sqrt(m2 + pT * pT);
+  const double mT = sqrt(m2 + pT * pT), mT2 = mT * mT, mTb = mT * baryon;
 
   // per-workgroup constants into LDS: inside the cell loop the only global loads are the
   // record prefetch (and PTM's renormalisation factor)
@@ -299,7 +327,7 @@ __global__ __launch_bounds__(kBlock, MODE >= PTM ? IS3D_SPECTRA_WAVES_MOD : IS3D
 #pragma unroll
   for (int jj = 0; jj < kJmax; jj++) acc[jj] = 0.0;
 
-  const long c_begin = (long)blockIdx.z * A.cells_per_split;
+  const long c_begin = (long)split * A.cells_per_split;
   const long c_end = min(A.n, c_begin + A.cells_per_split);
 
   // record tiles: tile i lives in buffer i & 1; tile i + 1 is copied in while tile i is integrated
@@ -351,7 +379,7 @@ __global__ __launch_bounds__(kBlock, MODE >= PTM ? IS3D_SPECTRA_WAVES_MOD : IS3D
           const bool sep = (MODE <= CE) || kind == 1.0 || Y[Y_NARROW] != 0.0;
           if (sep) {
             SepLane L;
-            sep_setup(sep_flavor(MODE), R, Y, mT, m2, pT, sign, baryon, L);
+            sep_setup(sep_flavor(MODE), R, Y, mT, mT2, m2, mTb, pT, sign, baryon, L);
             if (L.skip) continue;
             if (L.fast) sep_phi_loop<MODE, FLAGS, true>(L, s_cs + j0, BP, acc);
             else sep_phi_loop<MODE, FLAGS, false>(L, s_cs + j0, BP, acc);
@@ -366,22 +394,40 @@ __global__ __launch_bounds__(kBlock, MODE >= PTM ? IS3D_SPECTRA_WAVES_MOD : IS3D
     }
   }
   if (active) {
-    double* out = A.slab + (long)blockIdx.z * A.outsize;
-    const long base = ((long)A.sorig[s] * A.npT + ipt) * A.nphi;
-#pragma unroll
-    for (int jj = 0; jj < kJmax; jj++) {
-      if (jj < nj) out[(base + j0 + jj) * A.ny_out + k] = acc[jj];
-    }
   }
+  // partial sums, slab layout [split][pT][lane group][phi slot][lane]: every store of the wave is
+  // one contiguous 512-byte row; non-temporal so the stream does not evict the cell records the
+  // XCD's other workgroups are still reading from L2.  k_reduce scatters into the reference layout.
+  double* out = A.slab + (long)split * A.sstride + ((long)ipt * A.nbx + lane_group) * (kJmax * kBlock) + tid;
+#pragma unroll
+  for (int jj = 0; jj < kJmax; jj++) __builtin_nontemporal_store(acc[jj], out + jj * kBlock);
 }
 
-__global__ __launch_bounds__(256) void k_reduce(const double* slab, long outsize, int nsplit, const double* degen_orig,
-                                                long per_species, double prefactor, double* out) {
-  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= outsize) return;
+struct ReduceArgs {
+  const double* slab; long sstride; int nsplit;
+  int nbx, npart, npT, nphi, nk, ny_out; long ntask;
+  const int* sorig; const double* degen_orig; double prefactor;
+  double* out;
+};
+
+// dN[s][pT][phi][y] = (2 pi hbarc)^-3 g_s * sum over cell splits, in fixed split order
+__global__ __launch_bounds__(256) void k_reduce(ReduceArgs A) {
+  const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= A.sstride) return;
+  const int lane = (int)(e % kBlock);
+  const int jj = (int)((e / kBlock) % kJmax);
+  const long rest = e / ((long)kBlock * kJmax);
+  const int lane_group = (int)(rest % A.nbx), ipt = (int)(rest / A.nbx);
+  const long task = (long)lane_group * kBlock + lane;
+  if (task >= A.ntask) return;
+  const int s = (int)(task % A.npart);
+  const long r = task / A.npart;
+  const int k = (int)(r % A.nk), j = (int)(r / A.nk) * kJmax + jj;
+  if (j >= A.nphi) return;
   double acc = 0.0;
-  for (int z = 0; z < nsplit; z++) acc += slab[(long)z * outsize + idx];
-  out[idx] = prefactor * degen_orig[idx / per_species] * acc;
+  for (int z = 0; z < A.nsplit; z++) acc += A.slab[(long)z * A.sstride + e];
+  const int so = A.sorig[s];
+  A.out[(((long)so * A.npT + ipt) * A.nphi + j) * A.ny_out + k] = A.prefactor * A.degen_orig[so] * acc;
 }
 
 __global__ void k_df_eval(DfTables tb, double T, double muB, double E, double P, double bulkPi, double* out, int* err) {
@@ -804,24 +850,31 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   const long ntask = (long)np * nk * njb;
   const long bx = (ntask + kBlock - 1) / kBlock;
   const long wgs = bx * npT;
-  const long target = 8192;
+  // cell splits: enough workgroups to fill the chip (>= 8k), and each split's records small enough
+  // (~2 MB) to stay in one XCD's 4 MB L2 while that XCD's workgroups stream them; a multiple of 8
+  // so every XCD owns whole splits; at most 64 slabs
   const long max_split = (n + kTile - 1) / kTile;
-  long nsplit = std::max(1L, std::min(max_split, (target + wgs - 1) / wgs));
+  const long by_fill = (8192 + wgs - 1) / wgs;
+  const long by_l2 = ((long)NREC * 8 * n + (2L << 20) - 1) / (2L << 20);
+  long nsplit = std::max(by_fill, std::min(by_l2, 64L));
+  if (nsplit >= 8) nsplit = (nsplit + 7) / 8 * 8;
+  nsplit = std::max(1L, std::min(nsplit, max_split));
   long cps = (n + nsplit - 1) / nsplit;
   cps = ((cps + kTile - 1) / kTile) * kTile;
   nsplit = (n + cps - 1) / cps;
-  if (!ensure(e->d_slab, e->slab_cap, nsplit * outsize)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(slabs) failed");
+  const long sstride = (long)npT * bx * kJmax * kBlock;
+  if (!ensure(e->d_slab, e->slab_cap, nsplit * sstride)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(slabs) failed");
   SpecArgs sa{};
   sa.rec = e->d_rec; sa.n = n; sa.renorm = e->d_renorm; sa.slab = e->d_slab; sa.outsize = outsize;
   sa.smass = e->d_smass; sa.ssign = e->d_ssign; sa.sbaryon = e->d_sbaryon; sa.sorig = e->d_sorig;
   sa.pT = e->d_pT; sa.cphi = e->d_cphi; sa.sphi = e->d_sphi; sa.yv = e->d_y; sa.etav = e->d_eta; sa.etaw = e->d_etaw;
   sa.npart = np; sa.npT = npT; sa.nphi = nphi; sa.ny_out = ny_out; sa.nk = nk; sa.nl = nl; sa.nq = nk * nl; sa.njb = njb;
-  sa.ntask = ntask; sa.cells_per_split = cps;
+  sa.ntask = ntask; sa.cells_per_split = cps; sa.nbx = (int)bx; sa.nsplit = (int)nsplit; sa.sstride = sstride;
   sa.regulate = e->p.regulate_deltaf; sa.outflow = e->p.outflow; sa.dim = dim;
   const size_t shmem = sizeof(double) * (2 * (size_t)kTile * NREC + 2 * (size_t)(kTile + 2) * njb * kJmax + (size_t)(nk + 2 * nl) +
                                          (size_t)kTile * sa.nq * NYT);
   if (shmem > 160 * 1024) return e->fail(IS3D_ERR_ARG, "momentum grid too large for the LDS tile");
-  const dim3 grid((unsigned)bx, (unsigned)npT, (unsigned)nsplit);
+  const dim3 grid((unsigned)(bx * npT * nsplit));
   const int kflags = (e->p.regulate_deltaf ? F_REG : 0) | (e->p.outflow ? F_OUT : 0);
   switch (mode) {
     case GRAD: launch_spectra<GRAD>(grid, shmem, st, sa, kflags); break;
@@ -832,10 +885,12 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   }
   HIPCHK(e, hipGetLastError());
   HIPCHK(e, hipEventRecord(e->ev[2], st));
-  const double prefactor = std::pow(2.0 * M_PI * kHbarC, -3);
-  const long per_species = (long)npT * nphi * ny_out;
-  hipLaunchKernelGGL(k_reduce, dim3((unsigned)((outsize + 255) / 256)), dim3(256), 0, st, (const double*)e->d_slab, outsize,
-                     (int)nsplit, e->d_degen_orig, per_species, prefactor, dev_out);
+  ReduceArgs ra{};
+  ra.slab = e->d_slab; ra.sstride = sstride; ra.nsplit = (int)nsplit;
+  ra.nbx = (int)bx; ra.npart = np; ra.npT = npT; ra.nphi = nphi; ra.nk = nk; ra.ny_out = ny_out; ra.ntask = ntask;
+  ra.sorig = e->d_sorig; ra.degen_orig = e->d_degen_orig; ra.prefactor = std::pow(2.0 * M_PI * kHbarC, -3);
+  ra.out = dev_out;
+  hipLaunchKernelGGL(k_reduce, dim3((unsigned)((sstride + 255) / 256)), dim3(256), 0, st, ra);
   HIPCHK(e, hipGetLastError());
   HIPCHK(e, hipEventRecord(e->ev[3], st));
   e->launched = true;

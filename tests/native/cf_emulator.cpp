@@ -75,6 +75,7 @@ extern "C" int emu_spectra(const orc_params* p, const orc_setup* su, const orc_s
       if (!err) { st_break += (flags[0] && R[R_KIND] != 0.0); st_pl += flags[1]; }
     } else prep_famod_a(k, s, R, &aux[(size_t)c * 9]);
     if (err) return 100 + err;
+    if (R[R_KIND] != 0.0) sep_cell_consts(mode, R);
   }
   if (mode == PTMA) {
     const int nh = su->npdg < 320 ? su->npdg : 320;
@@ -141,9 +142,19 @@ extern "C" int emu_spectra(const orc_params* p, const orc_setup* su, const orc_s
             const bool sep = (mode <= CE) || kind == 1.0 || Y[Y_NARROW] != 0.0;
             if (sep) {
               SepLane L;
-              sep_setup(sep_flavor(mode), R, Y, mT, m2, pT, sign, baryon, L);
+              sep_setup(sep_flavor(mode), R, Y, mT, mT * mT, m2, mT * baryon, pT, sign, baryon, L);
               if (L.skip) continue;
-              for (int j = 0; j < nphi; j++)
+              // same arithmetic as k_spectra: fast lanes evaluate phi points in pairs sharing one
+              // reciprocal (an odd tail point alone)
+              int j = 0;
+              if (L.fast) {
+                for (; j + 1 < nphi; j += 2) {
+                  double v0, v1;
+                  sep_pair(sep_flavor(mode), L, CS[j], BP[j], CS[j + 1], BP[j + 1], p->regulate_deltaf, p->outflow, v0, v1);
+                  a[j] += v0; a[j + 1] += v1;
+                }
+              }
+              for (; j < nphi; j++)
                 a[j] += sep_point(sep_flavor(mode), L, CS[j], BP[j], p->regulate_deltaf, p->outflow);
             } else {
               ModLane M;

@@ -131,7 +131,7 @@ def _rel(a, b):
 def test_full_size_properties(mode):
     """BASELINE config 2 at full size (10^5 cells x 444 species x 48 x 32 x 21), where the oracle
     would take hours: the spectrum is a sum over cells, so it must be additive over a cell split
-    and invariant under a cell permutation (to summation-order rounding), and p.dsigma enters
+    and invariant under a cell permutation (to summation-order rounding, TOL), and p.dsigma enters
     linearly, so doubling dsigma_mu must double every (normal-range) entry bit for bit."""
     spec, s = _config2(mode)
     e = build_engine(spec, s)
@@ -152,8 +152,10 @@ def test_full_size_properties(mode):
     d = e.calculate_spectra()
     e.close()
     assert np.isfinite(full).all() and (full != 0).sum() > 0.5 * full.size
-    assert _rel(a + b, full) < 1e-11
-    assert _rel(p, full) < 1e-11
+    # summation order changes: entries that are sums of mixed-sign contributions (delta-f < -1 at
+    # high pT) lose relative precision to cancellation (measured 4e-10), so the parity tolerance
+    assert _rel(a + b, full) < TOL
+    assert _rel(p, full) < TOL
     m = np.abs(full) > 1e-290          # below that, subnormal products round on an absolute grid
     assert np.array_equal(d[m], 2.0 * full[m])
     assert np.abs(d[~m] - 2.0 * full[~m]).max(initial=0.0) <= 1e-300
