@@ -775,20 +775,6 @@ IS3D_HD double rcp1(double d) {
 #endif
 }
 
-// 1/d to ~1 ulp (two Newton steps); d = +inf (exp overflow: the reference's 1/(inf + sign)) -> 0.
-IS3D_HD double fast_rcp(double d) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  double r = __builtin_amdgcn_rcp(d);
-  double e = fma(-d, r, 1.0);
-  r = fma(r, e, r);
-  e = fma(-d, r, 1.0);
-  r = fma(r, e, r);
-  return (d < 1.79769313486231570e308) ? r : 0.0;
-#else
-  return 1.0 / d;
-#endif
-}
-
 IS3D_HD double lin(double c0, double cc, double cs, dbl2 p) { return fma(cc, p.x, fma(cs, p.y, c0)); }
 
 // Everything after f_eq for one separable point: returns w * p.dsigma * f_eq (1 + delta-f)
@@ -904,10 +890,26 @@ IS3D_HD double sep_point(int flavor, const SepLane& L, dbl2 cs, dbl2 bp, int reg
   return 0.0;
 }
 
+// sqrt(v) for normal v > 0: v_rsq_f64 (5e-8) + one Newton-Goldschmidt step (~4e-15 relative);
+// IEEE sqrt on the host
+IS3D_HD double sqrt_nr(double v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const double y = __builtin_amdgcn_rsq(v);
+  const double g = v * y, h = 0.5 * y;
+  return fma(g, fma(-g, h, 0.5), g);
+#else
+  return sqrt(v);
+#endif
+}
+
 // Modified (PTM/PTB/PTMA) lane: p_mod = mT (ch Uc + sh Us) + (pc Vc + ps Vs)  (MomentumSpectra.cpp:932-982
-// without the iterative refinement, which only changes rounding: A is linear)
+// without the iterative refinement, which only changes rounding: A is linear).
+// f = |renorm| / (exp(E_mod/T_mod - chem) + sign) is evaluated as |renorm| en / (1 + sign en) with
+// en = exp(chem - E_mod/T_mod): u.p > 0 bounds en by e^chem and, for bosons (no baryon number),
+// below 1, so 1 + sign en lies in ~[1e-3, 2] and two points can share one reciprocal; en -> 0
+// where the reference's exp overflows to 1/inf = 0.  |renorm| is folded into p.dsigma.
 struct ModLane {
-  double mUx, mUy, mUz, D0, Dc, Ds, Vcx, Vsx, Vcy, Vsy, Vcz, Vsz, m2, invTm, chemm, rn, sign;
+  double mUx, mUy, mUz, D0, Dc, Ds, Vcx, Vsx, Vcy, Vsy, Vcz, Vsz, m2, invTm, chemm, sign;
   ExpCoef ec;    // pinned once per lane setup, reused by every phi point
   int skip;
 };
@@ -915,10 +917,10 @@ struct ModLane {
 IS3D_HD void mod_setup(const double* R, const double* Y, double mT, double m2, double pT, double sign, double baryon,
                        double renorm_abs, ModLane& L) {
   L.mUx = mT * Y[Y_MUX]; L.mUy = mT * Y[Y_MUY]; L.mUz = mT * Y[Y_MUZ];
-  L.D0 = mT * Y[Y_MD]; L.Dc = Y[Y_WDX]; L.Ds = Y[Y_WDY];
+  L.D0 = renorm_abs * (mT * Y[Y_MD]); L.Dc = renorm_abs * Y[Y_WDX]; L.Ds = renorm_abs * Y[Y_WDY];
   L.Vcx = R[R_VCX]; L.Vsx = R[R_VSX]; L.Vcy = R[R_VCY]; L.Vsy = R[R_VSY]; L.Vcz = R[R_VCZ]; L.Vsz = R[R_VSZ];
   L.m2 = m2; L.sign = sign;
-  L.invTm = R[R_INVTM]; L.chemm = baryon * R[R_CHEMM]; L.rn = renorm_abs;
+  L.invTm = R[R_INVTM]; L.chemm = baryon * R[R_CHEMM];
   L.ec = exp_coef();
   // E_mod >= | |mT U| - pT |V|max |; if even that overflows exp, every phi point is exactly 0
   const double mu = sqrt(L.mUx * L.mUx + L.mUy * L.mUy + L.mUz * L.mUz);
@@ -927,18 +929,39 @@ IS3D_HD void mod_setup(const double* R, const double* Y, double mT, double m2, d
   L.skip = (emin * L.invTm - L.chemm > kExpMax + 1.0) ? 1 : 0;
 }
 
+// en = exp(chem - E_mod / T_mod) at one phi point
+IS3D_HD double mod_en(const ModLane& L, dbl2 cs) {
+  const double qx = lin(L.mUx, L.Vcx, L.Vsx, cs), qy = lin(L.mUy, L.Vcy, L.Vsy, cs), qz = lin(L.mUz, L.Vcz, L.Vsz, cs);
+  const double Emod = sqrt_nr(fma(qx, qx, fma(qy, qy, fma(qz, qz, L.m2))));
+  return exp_clamped(L.ec, fma(-Emod, L.invTm, L.chemm));
+}
+
 template <bool OUT>
 IS3D_HD double mod_point_t(const ModLane& L, dbl2 cs) {
-  const double qx = lin(L.mUx, L.Vcx, L.Vsx, cs), qy = lin(L.mUy, L.Vcy, L.Vsy, cs), qz = lin(L.mUz, L.Vcz, L.Vsz, cs);
-  const double Emod = sqrt(fma(qx, qx, fma(qy, qy, fma(qz, qz, L.m2))));
-  const double f = L.rn * fast_rcp(exp_clamped(L.ec, Emod * L.invTm - L.chemm) + L.sign);
+  const double en = mod_en(L, cs);
   const double pds = lin(L.D0, L.Dc, L.Ds, cs);
-  const double r = pds * f;
+  const double r = pds * (en * rcp1(fma(L.sign, en, 1.0)));
   return (OUT && pds <= 0.0) ? 0.0 : r;
+}
+
+template <bool OUT>
+IS3D_HD void mod_pair_t(const ModLane& L, dbl2 c0, dbl2 c1, double& v0, double& v1) {
+  const double en0 = mod_en(L, c0), en1 = mod_en(L, c1);
+  const double q0 = fma(L.sign, en0, 1.0), q1 = fma(L.sign, en1, 1.0);
+  const double r = rcp1(q0 * q1);
+  const double pds0 = lin(L.D0, L.Dc, L.Ds, c0), pds1 = lin(L.D0, L.Dc, L.Ds, c1);
+  const double g0 = pds0 * (en0 * (r * q1)), g1 = pds1 * (en1 * (r * q0));
+  v0 = (OUT && pds0 <= 0.0) ? 0.0 : g0;
+  v1 = (OUT && pds1 <= 0.0) ? 0.0 : g1;
 }
 
 IS3D_HD double mod_point(const ModLane& L, dbl2 cs, int outflow) {
   return outflow ? mod_point_t<true>(L, cs) : mod_point_t<false>(L, cs);
+}
+
+IS3D_HD void mod_pair(const ModLane& L, dbl2 c0, dbl2 c1, int outflow, double& v0, double& v1) {
+  if (outflow) mod_pair_t<true>(L, c0, c1, v0, v1);
+  else mod_pair_t<false>(L, c0, c1, v0, v1);
 }
 
 }  // namespace is3d

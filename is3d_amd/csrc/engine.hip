@@ -232,13 +232,16 @@ __device__ __forceinline__ void sep_phi_loop(const SepLane& L, const dbl2* CS, c
 
 template <int FLAGS>
 __device__ __forceinline__ void mod_phi_loop(const ModLane& M, const dbl2* CS, double* acc) {
-  dbl2 c = CS[0];
+  constexpr bool OUT = (FLAGS & F_OUT) != 0;
+  dbl2 c0 = CS[0], c1 = CS[1];
 #pragma unroll
-  for (int jj = 0; jj < kJmax; jj++) {
-    dbl2 cn = c;
-    if (jj + 1 < kJmax) cn = CS[jj + 1];
-    acc[jj] += mod_point_t<(FLAGS & F_OUT) != 0>(M, c);
-    c = cn;
+  for (int jj = 0; jj < kJmax; jj += 2) {
+    dbl2 n0 = c0, n1 = c1;
+    if (jj + 2 < kJmax) { n0 = CS[jj + 2]; n1 = CS[jj + 3]; }
+    double v0, v1;
+    mod_pair_t<OUT>(M, c0, c1, v0, v1);
+    acc[jj] += v0; acc[jj + 1] += v1;
+    c0 = n0; c1 = n1;
   }
 }
 

@@ -160,7 +160,13 @@ extern "C" int emu_spectra(const orc_params* p, const orc_setup* su, const orc_s
               ModLane M;
               mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, M);
               if (M.skip) continue;
-              for (int j = 0; j < nphi; j++) a[j] += mod_point(M, CS[j], p->outflow);
+              int j = 0;
+              for (; j + 1 < nphi; j += 2) {
+                double v0, v1;
+                mod_pair(M, CS[j], CS[j + 1], p->outflow, v0, v1);
+                a[j] += v0; a[j + 1] += v1;
+              }
+              for (; j < nphi; j++) a[j] += mod_point(M, CS[j], p->outflow);
             }
           }
         }
