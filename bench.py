@@ -44,7 +44,7 @@ def log(*a):
 
 
 def make_surface(cfg, rank, world, dim, baryon):
-    from is3d_amd import synth
+    from is3d2_amd import synth
     if cfg["scaling"] == "strong":
         total = cfg["cells"]
         lo = rank * total // world
@@ -98,7 +98,7 @@ def main():
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
 
-    from is3d_amd import build_engine, make_spec
+    from is3d2_amd import build_engine, make_spec
 
     cfg = dict(CONFIGS[args.config])
     if args.cells:
@@ -111,7 +111,7 @@ def main():
                      dimension=cfg["dim"], df_mode=mode, **flags)
     surf = make_surface(cfg, rank, world, cfg["dim"], bool(flags.get("include_baryon", 0)))
     n_local = len(surf["tau"])
-    from is3d_amd import dist as D
+    from is3d2_amd import dist as D
     reduce = D.torch_all_reduce(dist, dev) if world > 1 else (lambda a: a)
     T_avg = D.global_averages(D.average_sums(surf, flags.get("include_baryon", 0)), reduce)[0]
 

@@ -1,6 +1,6 @@
 """ctypes binding of libis3d_amd.so (include/is3d_amd.h).
 
-The library is built in-tree by is3d_amd/csrc/Makefile (or __graft_entry__.build()).
+The library is built in-tree by is3d2_amd/csrc/Makefile (or __graft_entry__.build()).
 There is no fallback: if the HIP library is missing, importing the engine fails.
 """
 import ctypes as C
@@ -47,7 +47,7 @@ def load():
     if _lib is not None:
         return _lib
     if not os.path.exists(LIB_PATH):
-        raise ImportError("libis3d_amd.so not built (run `make -C is3d_amd/csrc` or __graft_entry__.build())")
+        raise ImportError("libis3d_amd.so not built (run `make -C is3d2_amd/csrc` or __graft_entry__.build())")
     lib = C.CDLL(LIB_PATH)
     P = C.POINTER
     d = C.c_double

@@ -13,7 +13,7 @@ def load():
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):
-            raise ImportError("libis3d_host.so not built (make -C is3d_amd/csrc/host)")
+            raise ImportError("libis3d_host.so not built (make -C is3d2_amd/csrc/host)")
         lib = C.CDLL(LIB_PATH)
         PD, PL, PI = C.POINTER(C.c_double), C.POINTER(C.c_long), C.POINTER(C.c_int)
         lib.is3d_host_run_particlization.argtypes = [C.c_char_p, C.c_int, C.c_int, PD, C.c_long, C.c_char_p, C.c_int]

@@ -11,7 +11,7 @@ the ones iS3D builds from the same files:
 * chosen particles: first PDG entry with a matching mcid
   (EmissionFunction.cpp:356-372).
 
-The numeric content of the PDG files is packed in is3d_amd/data/pdg.npz by
+The numeric content of the PDG files is packed in is3d2_amd/data/pdg.npz by
 tools/pack_reference_data.py.
 """
 import os

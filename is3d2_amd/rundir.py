@@ -1,5 +1,5 @@
 """Materialise a reference-layout iS3D run directory from the packed input tables
-(is3d_amd/data/*.npz), so the drop-in workflow (iS3D_amd / is3d_host_run_particlization)
+(is3d2_amd/data/*.npz), so the drop-in workflow (iS3D_amd / is3d_host_run_particlization)
 can be exercised anywhere, including on the GPU box where /root/reference is absent.
 
 Layout (iS3D.cpp:96-257): iS3D_parameters.dat, input/surface.dat, PDG/<pdg file>,

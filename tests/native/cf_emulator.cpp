@@ -1,6 +1,6 @@
 // cf_emulator.cpp -- TEST INFRASTRUCTURE ONLY.
 //
-// Runs the engine's device math (is3d_amd/csrc/cf_math.h, aniso_math.h) serially on
+// Runs the engine's device math (is3d2_amd/csrc/cf_math.h, aniso_math.h) serially on
 // the host, in the same order of operations per lane as k_spectra, so the
 // factorised integrand can be checked against the oracle in the CPU test tier.
 // It is never linked into the product and is not a fallback: the product path
@@ -9,9 +9,9 @@
 #include <cstring>
 #include <vector>
 
-#include "../../is3d_amd/csrc/aniso_math.h"
-#include "../../is3d_amd/csrc/cf_math.h"
-#include "../../is3d_amd/csrc/spline_host.h"
+#include "../../is3d2_amd/csrc/aniso_math.h"
+#include "../../is3d2_amd/csrc/cf_math.h"
+#include "../../is3d2_amd/csrc/spline_host.h"
 #include "../../oracle/is3d_oracle.h"
 
 using namespace is3d;

@@ -3,7 +3,7 @@
 import ctypes as C
 import re
 
-from is3d_amd import _lib
+from is3d2_amd import _lib
 
 
 def declared_symbols():

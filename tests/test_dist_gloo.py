@@ -14,7 +14,7 @@ def _worker(rank, world, port, q):
     sys.path.insert(0, ROOT)
     import torch
     import torch.distributed as dist
-    from is3d_amd import dist as D, make_spec, synth
+    from is3d2_amd import dist as D, make_spec, synth
     from oracle import oracle as O
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -33,7 +33,7 @@ def _worker(rank, world, port, q):
 
 def test_two_rank_gloo_shard_and_allreduce():
     import torch.multiprocessing as mp
-    from is3d_amd import make_spec, synth
+    from is3d2_amd import make_spec, synth
     from oracle import oracle as O
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -6,7 +6,7 @@ import numpy as np
 import pytest
 
 from helpers import parity
-from is3d_amd import IS3DError, build_engine, make_spec, surface_averages, synth
+from is3d2_amd import IS3DError, build_engine, make_spec, surface_averages, synth
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu

@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 from helpers import parity
-from is3d_amd import host, make_spec, rundir, synth
+from is3d2_amd import host, make_spec, rundir, synth
 from oracle import oracle as O
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

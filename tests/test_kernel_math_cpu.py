@@ -5,7 +5,7 @@ import numpy as np
 import pytest
 
 from helpers import emu_spectra, parity
-from is3d_amd import make_spec, synth
+from is3d2_amd import make_spec, synth
 from oracle import oracle as O
 
 CASES = [(d, m) for d in (2, 3) for m in (1, 2, 3, 4, 5)]

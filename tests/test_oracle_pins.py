@@ -13,7 +13,7 @@ import re
 import numpy as np
 import pytest
 
-from is3d_amd import make_spec, synth
+from is3d2_amd import make_spec, synth
 from oracle import oracle as O
 
 

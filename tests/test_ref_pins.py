@@ -9,7 +9,7 @@ import subprocess
 import numpy as np
 import pytest
 
-from is3d_amd import data, hrg, synth
+from is3d2_amd import data, hrg, synth
 from oracle import oracle as O
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

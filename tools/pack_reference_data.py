@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Pack the reference's physics INPUT tables (not code) into is3d_amd/data/*.npz.
+"""Pack the reference's physics INPUT tables (not code) into is3d2_amd/data/*.npz.
 
 The GPU box has no /root/reference, but the parity tests and bench need the same
 inputs the reference workflow reads: PDG hadron lists, chosen-species lists,
@@ -128,4 +128,4 @@ def main(out_dir):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "is3d_amd/data")
+    main(sys.argv[1] if len(sys.argv) > 1 else "is3d2_amd/data")
