@@ -54,21 +54,28 @@ def make_surface(cfg, rank, world, dim, baryon):
     return synth.as_read(synth.surface(cfg["cells"], seed=7 + rank, dimension=dim, baryon=baryon, full3d=(dim == 3)))
 
 
-def cpu_baseline(spec, surf, units_per_cell, target_s=15.0):
+def cpu_baseline(spec, surf, units_per_cell, target_s=15.0, operation=1):
     """Oracle ('port' of the reference loop) on the host cores, on a cell prefix of the same workload."""
     from oracle import oracle as O
     threads = int(os.environ.get("OMP_NUM_THREADS") or min(16, os.cpu_count() or 1))
     T_avg = O.averages(surf)[0]
-    n_probe = min(len(surf["tau"]), max(threads, 8))
+
+    def run(sample):
+        if operation == 0:
+            O.dndx(spec, sample, T_avg=T_avg, threads=threads, omp_threads=threads, carry=0)
+        else:
+            O.spectra(spec, sample, T_avg=T_avg, threads=threads, omp_threads=threads)
+
+    n_probe = min(len(surf["tau"]), max(2 * threads, 32))
     probe = {k: v[:n_probe] for k, v in surf.items()}
     t = time.perf_counter()
-    O.spectra(spec, probe, T_avg=T_avg, threads=threads, omp_threads=threads)
+    run(probe)
     dt = time.perf_counter() - t
     n = int(min(len(surf["tau"]), max(n_probe, n_probe * target_s / max(dt, 1e-3))))
     n = max(threads, (n // threads) * threads)
     sample = {k: v[:n] for k, v in surf.items()}
     t = time.perf_counter()
-    O.spectra(spec, sample, T_avg=T_avg, threads=threads, omp_threads=threads)
+    run(sample)
     dt = time.perf_counter() - t
     return dict(value=n * units_per_cell / dt, unit="cell-species-mom-points/s", cores=threads, kind="port",
                 sample="first %d cells of rank 0's shard, same species/grid/df mode; %.1f s with %d OpenMP threads"
@@ -83,6 +90,8 @@ def main():
     ap.add_argument("--config", default="config2", choices=sorted(CONFIGS))
     ap.add_argument("--df-mode", type=int, default=0)
     ap.add_argument("--cells", type=int, default=0, help="override cells per GPU (weak) / total (strong)")
+    ap.add_argument("--operation", type=int, default=1, choices=[0, 1],
+                    help="1 continuous spectra (default, the BASELINE metric); 0 spacetime distributions dN/dX")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     args = ap.parse_args()
@@ -127,6 +136,12 @@ def main():
     units_local = n_local * units_per_cell
 
     def step():
+        if args.operation == 0:
+            t, r, ph = eng.calculate_dN_dX()      # synchronous: device passes + small host binning epilogue
+            if world > 1:
+                binned = torch.from_numpy(np.concatenate([t.ravel(), r.ravel(), ph.ravel()])).to(dev)
+                dist.all_reduce(binned)
+            return eng.stats()
         eng.launch(out.data_ptr(), stream)
         if world > 1:
             dist.all_reduce(out)
@@ -153,6 +168,8 @@ def main():
     elapsed = tmax.item()
     total_units = units_all.item() * args.steps
 
+    if args.operation == 0 and world > 1 and spec["bins"].get("threads", 0):
+        raise SystemExit("operation 0 with reference thread emulation runs on one rank")
     ms_spectra = float(np.mean([s["ms_spectra"] for s in kstats]))
     ms_total = float(np.mean([s["ms_total"] for s in kstats]))
     flops = FLOPS_PER_NODE[mode] * neta * units_local
@@ -161,7 +178,8 @@ def main():
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
         try:
-            traffic = json.load(open(pmc)).get("%s_mode%d" % (args.config, mode))
+            key = "%s_mode%d" % (args.config, mode) if args.operation == 1 else "%s_op0_mode%d" % (args.config, mode)
+            traffic = json.load(open(pmc)).get(key)
         except Exception:
             traffic = None
 
@@ -180,23 +198,25 @@ def main():
             "dtype": "f64",
             "data": "synthetic (SURVEY.md 8d surface generator, seed 7+rank)",
             "config": {
-                "workload": "%s: %s 3+1D synthetic freeze-out cells%s x %s HRG (%d species) x %s delta-f, %d pT x %d phi x %d y%s"
-                            % (args.config, cfg["cells"], " per GPU" if cfg["scaling"] == "weak" else " total",
+                "workload": "%s%s: %s %s synthetic freeze-out cells%s x %s HRG (%d species) x %s delta-f, %d pT x %d phi x %d y%s"
+                            % (args.config, " operation 0 (dN/dX)" if args.operation == 0 else "", cfg["cells"],
+                               "3+1D" if cfg["dim"] == 3 else "2+1D", " per GPU" if cfg["scaling"] == "weak" else " total",
                                "SMASH" if cfg["hrg"] == 2 else "UrQMD", nsp, MODE_NAMES[mode], npT, nphi, ny,
                                "" if neta == 1 else " x %d eta" % neta),
+                "operation": args.operation,
                 "cells_per_gpu": n_local, "species": nsp, "grid": [npT, nphi, ny, neta], "df_mode": mode,
                 "parallelism": "dp%d (cell shards + RCCL all-reduce of spectra)" % world if world > 1 else "1 GPU",
             },
             "roofline": {
                 "bound": "mfma", "pipe": "fp64 (vector ALU; MI355X FP64 vector peak = FP64 matrix peak)",
-                "kernel": "k_spectra", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "kernel": "k_spectra" if args.operation == 1 else "k_dndx", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
                 "algorithmic_flops_per_launch": flops, "flops_per_point": FLOPS_PER_NODE[mode] * neta,
                 "kernel_ms": ms_spectra, "pass_ms": ms_total,
             },
         }
         if world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(spec, surf, units_per_cell, args.cpu_seconds)
+            res["cpu_baseline"] = cpu_baseline(spec, surf, units_per_cell, args.cpu_seconds, args.operation)
         print(json.dumps(res), flush=True)
     eng.close()
     if world > 1:

@@ -16,6 +16,10 @@
  *                                     construct_cubic_splines + compute_jonah_coefficients
  *   is3d_set_surface                  FO_surf[] -> SoA unpack                  (EmissionFunction.cpp:1049-1161)
  *   is3d_calculate_spectra            calculate_spectra, operation = 1         (EmissionFunction.cpp:1198-1226)
+ *   is3d_set_momentum_weights         pT/phi Table weight columns              (SpacetimeDistribution.cpp:57-79)
+ *   is3d_set_spacetime_bins           tau/r/phip bin parameters                (EmissionFunction.cpp:232-247)
+ *   is3d_calculate_dN_dX              calculate_spectra, operation = 0         (EmissionFunction.cpp:1165-1196)
+ *   is3d_get_cell_yields              dN_dy_cell of each freeze-out cell       (SpacetimeDistribution.cpp:374)
  *   is3d_evaluate_df_coefficients     Deltaf_Data::evaluate_df_coefficients    (DeltafData.cpp:501-519)
  *   is3d_surface_averages             ds_max-weighted averages (Plasma)        (readindata.cpp:316-366, iS3D.cpp:184-219)
  *
@@ -32,7 +36,7 @@
 extern "C" {
 #endif
 
-#define IS3D_ABI_VERSION 1
+#define IS3D_ABI_VERSION 2
 
 enum {
   IS3D_OK = 0,
@@ -46,7 +50,8 @@ enum {
 typedef struct is3d_engine is3d_engine;
 
 typedef struct {
-  int operation;                  /* must be 1 (continuous spectra) */
+  int operation;                  /* 1 continuous spectra, 0 spacetime distributions (2, the sampler, is rejected);
+                                     informs the host facade -- each compute entry point fixes its own semantics */
   int dimension;                  /* 2 = boost-invariant (eta quadrature), 3 = 3+1d (y grid) */
   int df_mode;                    /* 1 Grad, 2 RTA-CE, 3 PTM, 4 PTB, 5 PTMA */
   int include_baryon;
@@ -74,6 +79,21 @@ typedef struct {
   const double *bulkPi;
   const double *muB, *nB, *Vx, *Vy, *Vn;
 } is3d_surface;
+
+/* operation = 0 binning (iS3D_parameters.dat tau_min/tau_max/tau_bins, r_min/r_max/r_bins, phip_bins;
+ * EmissionFunction.cpp:232-247).  threads = the reference's OpenMP thread count CORES:
+ *   0      every species is binned from zero (the evident intent of the reference);
+ *   C >= 1 reproduce a reference run with OMP_NUM_THREADS = C, whose per-species reset
+ *          memset(all, 0, CORES * bins) clears BYTES, so thread-slice entries past the first
+ *          CORES*bins/8 doubles carry the previous species' sums (SpacetimeDistribution.cpp:165-167). */
+typedef struct {
+  double tau_min, tau_max;
+  int tau_bins;
+  double r_min, r_max;
+  int r_bins;
+  int phip_bins;
+  int threads;
+} is3d_spacetime_bins;
 
 typedef struct {
   long cells;                     /* cells processed in the last call */
@@ -121,6 +141,17 @@ int is3d_launch(is3d_engine *e, double *dev_out, void *stream);
 int is3d_finish(is3d_engine *e);
 int is3d_get_stats(const is3d_engine *e, is3d_stats *out);
 long is3d_output_size(const is3d_engine *e);
+
+/* operation = 0, spacetime distributions dN/dX (EmissionFunction.cpp:1165-1196 ->
+ * calculate_dN_dX / calculate_dN_dX_feqmod, SpacetimeDistribution.cpp:31-1250; df_mode 1-4, PTMA is
+ * rejected as in the reference).  Needs the pT / phi quadrature weights (Table column 2) and the bins.
+ * Outputs [species][bins] are the values the reference writes to results/continuous/dN_taudtaudy_<MCID>.dat,
+ * dN_2pirdrdy_<MCID>.dat and dN_dphidy_<MCID>.dat (already divided by tau dtau, 2 pi r dr, dphi). */
+int is3d_set_momentum_weights(is3d_engine *e, const double *pT_weight, const double *phi_weight);
+int is3d_set_spacetime_bins(is3d_engine *e, const is3d_spacetime_bins *bins);
+int is3d_calculate_dN_dX(is3d_engine *e, double *dN_taudtaudy, double *dN_2pirdrdy, double *dN_dphidy);
+/* dN_dy_cell[species][cell] of the last is3d_calculate_dN_dX call (SpacetimeDistribution.cpp:374). */
+int is3d_get_cell_yields(const is3d_engine *e, double *dN_dy_cell);
 
 /* Test hooks mirroring reference services. out[15] = c0 c1 c2 c3 c4 shear14 F G
  * betabulk betaV betapi lambda z delta_lambda delta_z (evaluated on the GPU). */

@@ -2,7 +2,7 @@
  * is3d_host.h -- C ABI of the C++ host layer (libis3d_host.so): the iS3D2 drop-in
  * workflow around the engine (include/is3d_amd.h).
  *
- *   is3d_host_run_particlization   IS3D::run_particlization(1) for operation = 1      (iS3D.cpp:81-282)
+ *   is3d_host_run_particlization   IS3D::run_particlization(1) for operation = 1 or 0 (iS3D.cpp:81-282)
  *                                  reading <workdir>/iS3D_parameters.dat, input/surface.dat, PDG/,
  *                                  deltaf_coefficients/, tables/ and writing results/continuous/
  *   is3d_host_read_surface         FO_data_reader::read_freezeout_surface modes 1/5/6/7 (readindata.cpp:149-731)
@@ -16,7 +16,8 @@ extern "C" {
 #endif
 
 /* Runs the whole workflow on HIP devices [device, device + num_devices) (cells sharded);
- * dN_out (optional, capacity doubles) receives dN/(pT dpT dphi dy)[species][pT][phi][y]. */
+ * dN_out (optional, capacity doubles) receives dN/(pT dpT dphi dy)[species][pT][phi][y] (operation 1)
+ * or, per species, [dN_taudtaudy (tau_bins) | dN_2pirdrdy (r_bins) | dN_dphidy (phip_bins)] (operation 0). */
 int is3d_host_run_particlization(const char *workdir, int device, int num_devices, double *dN_out,
                                  long out_capacity, char *err, int errlen);
 /* Returns the number of cells (or < 0); fields (optional) receives [25][n] in is3d_surface order,

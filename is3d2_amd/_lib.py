@@ -19,7 +19,8 @@ EXPORTS = ["is3d_abi_version", "is3d_create", "is3d_destroy", "is3d_last_error",
            "is3d_set_species", "is3d_set_pdg", "is3d_set_momentum_grid", "is3d_set_gauss_laguerre",
            "is3d_set_df_tables", "is3d_set_surface", "is3d_set_surface_device", "is3d_calculate_spectra",
            "is3d_launch", "is3d_finish", "is3d_get_stats", "is3d_output_size", "is3d_evaluate_df_coefficients",
-           "is3d_surface_averages", "is3d_get_jonah_table"]
+           "is3d_surface_averages", "is3d_get_jonah_table", "is3d_set_momentum_weights", "is3d_set_spacetime_bins",
+           "is3d_calculate_dN_dX", "is3d_get_cell_yields"]
 
 
 class Params(C.Structure):
@@ -27,6 +28,12 @@ class Params(C.Structure):
                 ("include_bulk_deltaf", C.c_int), ("include_shear_deltaf", C.c_int),
                 ("include_baryondiff_deltaf", C.c_int), ("regulate_deltaf", C.c_int), ("outflow", C.c_int),
                 ("famod_chains", C.c_int), ("deta_min", C.c_double), ("mass_pion0", C.c_double)]
+
+
+class SpacetimeBins(C.Structure):
+    _fields_ = [("tau_min", C.c_double), ("tau_max", C.c_double), ("tau_bins", C.c_int),
+                ("r_min", C.c_double), ("r_max", C.c_double), ("r_bins", C.c_int), ("phip_bins", C.c_int),
+                ("threads", C.c_int)]
 
 
 class Surface(C.Structure):
@@ -75,5 +82,9 @@ def load():
     lib.is3d_evaluate_df_coefficients.argtypes = [C.c_void_p, d, d, d, d, d, pd]
     lib.is3d_surface_averages.argtypes = [C.c_long, P(Surface), C.c_int, pd]
     lib.is3d_get_jonah_table.argtypes = [C.c_void_p, pd, pd, pd, pd]
+    lib.is3d_set_momentum_weights.argtypes = [C.c_void_p, pd, pd]
+    lib.is3d_set_spacetime_bins.argtypes = [C.c_void_p, P(SpacetimeBins)]
+    lib.is3d_calculate_dN_dX.argtypes = [C.c_void_p, pd, pd, pd]
+    lib.is3d_get_cell_yields.argtypes = [C.c_void_p, pd]
     _lib = lib
     return lib

@@ -332,6 +332,7 @@ IS3D_HD PiLRF boost_pi(const Milne& b, double tau2, double pitt, double pitx, do
 // Run-level constants for the prepass
 // ---------------------------------------------------------------------------
 struct PrepConsts {
+  int operation;   // 1 continuous spectra, 0 spacetime distributions (differences: see yterms / prep_*)
   int df_mode, dim, include_baryon, include_bulk, include_shear, include_diff;
   double deta_min, mass_pion0;
   int gla_pts;
@@ -389,7 +390,8 @@ IS3D_HD int prep_grad_ce(const PrepConsts& k, const DfTables& tb, const double* 
   R[R_VT] = Vt; R[R_TVN] = tau * Vn; R[R_VX] = Vx; R[R_VY] = Vy;
   R[R_CHEM] = alphaB;
   if (k.df_mode == GRAD) {
-    R[R_SHEAR] = 1.0 / df.shear14;
+    // 1 / (2 T^2 (E+P)) written as in each path (MomentumSpectra.cpp:215, SpacetimeDistribution.cpp:269)
+    R[R_SHEAR] = (k.operation == 0) ? 0.5 / (T * T * (E + P)) : 1.0 / df.shear14;
     R[R_BULK0] = (df.c0 - df.c2) * bulkPi; R[R_BULK1] = df.c1 * bulkPi; R[R_BULK2] = (4. * df.c2 - df.c0) * bulkPi;
     R[R_DIFF0] = df.c3; R[R_DIFF1] = df.c4;
   } else {
@@ -436,9 +438,11 @@ IS3D_HD int prep_feqmod(const PrepConsts& k, const DfTables& tb, const double* s
     alphaB = muB / T;
     ber = nB / (E + P);
   }
-  if (k.df_mode == PTB) {
-    if (bulkPi < -P) bulkPi = -(1.0 - 1.e-5) * P;
-    else if (bulkPi / P > tb.bulk_over_P_max) bulkPi = P * (tb.bulk_over_P_max - 1.e-5);
+  if (k.df_mode == PTB) {   // MomentumSpectra.cpp:603-615 (< / >); SpacetimeDistribution.cpp:766-772 (<= / >=)
+    const bool lo = (k.operation == 0) ? (bulkPi <= -P) : (bulkPi < -P);
+    const bool hi = (k.operation == 0) ? (bulkPi / P >= tb.bulk_over_P_max) : (bulkPi / P > tb.bulk_over_P_max);
+    if (lo) bulkPi = -(1.0 - 1.e-5) * P;
+    else if (hi) bulkPi = P * (tb.bulk_over_P_max - 1.e-5);
   }
   const double zt = tau * un / utperp, zn = ut / (tau * utperp);
   const double pl = P + bulkPi + zt * zt * pitt + tau2 * tau2 * zn * zn * pinn + 2. * tau2 * zt * zn * pitn;
@@ -610,7 +614,9 @@ enum SepFlavor : int { SEP_GRAD = 0, SEP_CE = 1, SEP_PTB = 2, SEP_FEQ = 3 };
 
 // mode -> (separable flavour, use cosh() instead of sqrt(1+sinh^2), w_eta only on the non-eta part of p.dsigma)
 IS3D_HD int sep_flavor(int mode) { return mode == GRAD ? SEP_GRAD : (mode == CE || mode == PTM) ? SEP_CE : mode == PTB ? SEP_PTB : SEP_FEQ; }
-IS3D_HD int quirk_pds(int mode) { return (mode == PTM || mode == PTB) ? 1 : 0; }
+// spectra PTM/PTB: w_eta multiplies only the non-eta part of p.dsigma (MomentumSpectra.cpp:936); the
+// spacetime path weights all of it (SpacetimeDistribution.cpp:1026, 1076)
+IS3D_HD int quirk_pds(int mode, int op) { return (op != 0 && (mode == PTM || mode == PTB)) ? 1 : 0; }
 
 // Species- and y-independent pieces of the separable lane coefficients, per cell (record
 // fields R_S0M2 .. R_LS; see yterms / sep_setup for the factorisation).
@@ -641,11 +647,12 @@ IS3D_HD void sep_cell_consts(int mode, double* R) {
 //   Q1 = pi^tt ch^2 + tau^2 pi^ee sh^2 - 2 tau pi^te ch sh,  W = V^t ch - tau V^e sh
 // and the separable delta-f coefficients factor as  S0 = mT^2 S2 + mT b S1 + m^2 R_S0M2,
 // Sc = mT SC1 + b R_SCB,  Ss = mT SS1 + b R_SSB,  L0 = mT L1 + b R_L0B  (see sep_setup).
-IS3D_HD void yterms(int mode, const double* R, double y, double eta, double w, double* Y) {
-  const int quirk = quirk_pds(mode);
-  // separable part: p^tau = mT cosh(y-eta) (Grad/CE: sqrt(1+sinh^2), :307-308)
+IS3D_HD void yterms(int mode, int op, const double* R, double y, double eta, double w, double* Y) {
+  const int quirk = quirk_pds(mode, op);
+  // separable part: p^tau = mT cosh(y-eta) (spectra Grad/CE: sqrt(1+sinh^2), MomentumSpectra.cpp:307-308;
+  // the spacetime path uses cosh, SpacetimeDistribution.cpp:313)
   const double sh = sinh(y - eta);
-  const double ch = (mode <= CE) ? sqrt(1.0 + sh * sh) : cosh(y - eta);
+  const double ch = (mode <= CE && op != 0) ? sqrt(1.0 + sh * sh) : cosh(y - eta);
   const double A = ch * R[R_UT] - sh * R[R_TAUUN];
   Y[Y_A] = A;
   Y[Y_AT] = A * R[R_INVT];

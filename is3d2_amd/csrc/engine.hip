@@ -192,6 +192,7 @@ struct SpecArgs {
   int nbx, nsplit;            // lane groups per pT, cell splits (1-D grid of nbx * npT * nsplit)
   long sstride;               // doubles per slab: npT * nbx * kJmax * kBlock
   int regulate, outflow, dim;
+  int op;                     // 1 spectra / 0 spacetime (yterms variants)
 };
 
 // flag bits of the spectra kernel instantiation
@@ -360,7 +361,7 @@ __global__ __launch_bounds__(kBlock, MODE >= PTM ? IS3D_SPECTRA_WAVES_MOD : IS3D
         const double y = s_grid[kk];
         const double eta = (A.dim == 3) ? R[R_ETA] : s_grid[A.nk + l];
         const double w = s_grid[A.nk + A.nl + l];
-        yterms(MODE, R, y, eta, w, s_y + ((long)t * A.nq + q) * NYT);
+        yterms(MODE, A.op, R, y, eta, w, s_y + ((long)t * A.nq + q) * NYT);
       }
     }
     lds_barrier();
@@ -433,6 +434,248 @@ __global__ __launch_bounds__(256) void k_reduce(ReduceArgs A) {
   A.out[(((long)so * A.npT + ipt) * A.nphi + j) * A.ny_out + k] = A.prefactor * A.degen_orig[so] * acc;
 }
 
+// ------------------------------------------------------------------------------------------
+// operation = 0: spacetime distributions dN/dX (SpacetimeDistribution.cpp:31-1250)
+// ------------------------------------------------------------------------------------------
+// Weighted phi sums: sum_j w_phi[j] x (w_eta p.dsigma f)(phi_j) for one lane and cell, with the
+// same per-point arithmetic as k_spectra (W = phi weights as {w_j, w_j+1} pairs, 0 in the padding).
+template <int MODE, int FLAGS, bool FAST>
+__device__ __forceinline__ double sep_phi_wsum(const SepLane& L, const dbl2* CS, const dbl2* BP, const dbl2* W) {
+  constexpr int FL = (MODE == GRAD) ? SEP_GRAD : (MODE == CE || MODE == PTM) ? SEP_CE : (MODE == PTB) ? SEP_PTB : SEP_FEQ;
+  constexpr bool REG = (FLAGS & F_REG) != 0, OUT = (FLAGS & F_OUT) != 0;
+  double a0 = 0.0, a1 = 0.0;
+  if (FAST && IS3D_PAIR_RCP) {
+    dbl2 c0 = CS[0], b0 = BP[0], c1 = CS[1], b1 = BP[1];
+#pragma unroll
+    for (int jj = 0; jj < kJmax; jj += 2) {
+      dbl2 n0 = c0, m0 = b0, n1 = c1, m1 = b1;
+      if (jj + 2 < kJmax) { n0 = CS[jj + 2]; m0 = BP[jj + 2]; n1 = CS[jj + 3]; m1 = BP[jj + 3]; }
+      const dbl2 w = W[jj >> 1];
+      double v0, v1;
+      sep_pair_t<FL, REG, OUT>(L, c0, b0, c1, b1, v0, v1);
+      a0 = fma(w.x, v0, a0); a1 = fma(w.y, v1, a1);
+      c0 = n0; b0 = m0; c1 = n1; b1 = m1;
+    }
+    return a0 + a1;
+  }
+#pragma unroll
+  for (int jj = 0; jj < kJmax; jj += 2) {
+    const dbl2 w = W[jj >> 1];
+    a0 = fma(w.x, sep_point_t<FL, REG, OUT, FAST>(L, CS[jj], BP[jj]), a0);
+    a1 = fma(w.y, sep_point_t<FL, REG, OUT, FAST>(L, CS[jj + 1], BP[jj + 1]), a1);
+  }
+  return a0 + a1;
+}
+
+template <int FLAGS>
+__device__ __forceinline__ double mod_phi_wsum(const ModLane& M, const dbl2* CS, const dbl2* W) {
+  constexpr bool OUT = (FLAGS & F_OUT) != 0;
+  double a0 = 0.0, a1 = 0.0;
+  dbl2 c0 = CS[0], c1 = CS[1];
+#pragma unroll
+  for (int jj = 0; jj < kJmax; jj += 2) {
+    dbl2 n0 = c0, n1 = c1;
+    if (jj + 2 < kJmax) { n0 = CS[jj + 2]; n1 = CS[jj + 3]; }
+    const dbl2 w = W[jj >> 1];
+    double v0, v1;
+    mod_pair_t<OUT>(M, c0, c1, v0, v1);
+    a0 = fma(w.x, v0, a0); a1 = fma(w.y, v1, a1);
+    c0 = n0; c1 = n1;
+  }
+  return a0 + a1;
+}
+
+struct DndxArgs {
+  const double* rec; long n;
+  const double* renorm;       // PTM: [c][s_sorted]
+  double* ycell;              // [npart (sorted)][n]: sum over (pT, phi, y, eta) of w_pT w_phi w_eta p.dsigma f
+  const double *smass, *ssign, *sbaryon;
+  const double *pT, *pTw, *cphi, *sphi, *phiw, *yv, *etav, *etaw;
+  int npart, npT, nphi, nk, nl, nq, njb;
+  int Sl, Yl, ntask, nbx;     // species per wavefront, task slots per wavefront, tasks per species
+                              // (y x phi block x eta node), species groups
+  long cells_per_wg, nchunk;
+  int dim;
+};
+
+// One workgroup = (species group of Sl mass-sorted species, cell chunk).  Lane = (species s_l, slot); the
+// 4 Yl slots of a workgroup stride over the species' tasks (y, phi block, eta node), so every wavefront
+// evaluates one task for Sl neighbouring species at a time -- the exp-underflow skip stays coherent as in
+// k_spectra.  The momentum loop (pT) is inside: per (cell tile, pT) the {b', Phi} phi-terms are rebuilt
+// in LDS and every lane adds w_pT x sum_phi w_phi (point) into its column of s_red; after the pT loop a
+// species' slot columns are summed in slot order.  No atomics: bit-reproducible.
+template <int MODE, int FLAGS>
+__global__ __launch_bounds__(kBlock, MODE >= PTM ? IS3D_SPECTRA_WAVES_MOD : IS3D_SPECTRA_WAVES_SEP) void k_dndx(DndxArgs A) {
+  extern __shared__ double smem[];
+  const int nphp = A.njb * kJmax;
+  double* s_rec = smem;                                   // [kTile][NREC]
+  dbl2* s_trig = (dbl2*)(s_rec + kTile * NREC);           // [nphp] {cos, sin}
+  dbl2* s_cs = s_trig + nphp;                             // [nphp] {pT cos, pT sin} of the current pT
+  double* s_w = (double*)(s_cs + nphp);                   // [nphp] phi weights (0 in the padding)
+  dbl2* s_bp = (dbl2*)(s_w + nphp);                       // [kTile][nphp] {b', Phi} of the current pT
+  double* s_red = (double*)(s_bp + kTile * nphp);         // [kTile][kBlock] per-lane cell sums
+  double* s_grid = s_red + kTile * kBlock;                // y[nk] | eta[nl] | eta_w[nl]
+  double* s_y = s_grid + A.nk + 2 * A.nl;                 // [kTile][nq][NYT]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const long nwg = (long)A.nbx * A.nchunk;
+  const long bid = blockIdx.x, q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
+  const long lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int grp = (int)(lid % A.nbx);
+  const long ch = lid / A.nbx;
+  const int s_l = lane % A.Sl, y_l = lane / A.Sl;
+  const int slot = wave * A.Yl + y_l, nslot = 4 * A.Yl;
+  const bool active = y_l < A.Yl && grp * A.Sl + s_l < A.npart;
+  const int s = active ? grp * A.Sl + s_l : 0;
+  const double mass = A.smass[s], m2 = mass * mass, sign = A.ssign[s], baryon = A.sbaryon[s];
+
+  for (int j = tid; j < nphp; j += kBlock) {
+    const bool in = j < A.nphi;
+    dbl2 v; v.x = in ? A.cphi[j] : 0.0; v.y = in ? A.sphi[j] : 0.0;
+    s_trig[j] = v;
+    s_w[j] = in ? A.phiw[j] : 0.0;
+  }
+  for (int i = tid; i < A.nk; i += kBlock) s_grid[i] = (A.dim == 3) ? A.yv[i] : 0.0;
+  for (int i = tid; i < A.nl; i += kBlock) {
+    s_grid[A.nk + i] = (A.dim == 3) ? 0.0 : A.etav[i];
+    s_grid[A.nk + A.nl + i] = (A.dim == 3) ? 1.0 : A.etaw[i];
+  }
+
+  const long c_begin = ch * A.cells_per_wg;
+  const long c_end = min(A.n, c_begin + A.cells_per_wg);
+  for (long cb = c_begin; cb < c_end; cb += kTile) {
+    const int nt = (int)min((long)kTile, c_end - cb);
+    __syncthreads();                                       // previous tile fully consumed
+    for (int i = tid; i < nt * NREC; i += kBlock) s_rec[i] = A.rec[cb * NREC + i];
+#pragma unroll
+    for (int t = 0; t < kTile; t++) s_red[t * kBlock + tid] = 0.0;
+    __syncthreads();
+    for (int idx = tid; idx < nt * A.nq; idx += kBlock) {
+      const int t = idx / A.nq, q = idx % A.nq;
+      const double* R = s_rec + t * NREC;
+      if (R[R_KIND] != 0.0) {
+        const int ky = q / A.nl, l = q % A.nl;
+        const double y = s_grid[ky];
+        const double eta = (A.dim == 3) ? R[R_ETA] : s_grid[A.nk + l];
+        const double w = s_grid[A.nk + A.nl + l];
+        yterms(MODE, 0, R, y, eta, w, s_y + ((long)t * A.nq + q) * NYT);
+      }
+    }
+    for (int ipt = 0; ipt < A.npT; ipt++) {
+      const double pT = A.pT[ipt], wpT = A.pTw[ipt];
+      const double mT = sqrt(m2 + pT * pT), mT2 = mT * mT, mTb = mT * baryon;
+      __syncthreads();                                     // y-terms ready / previous pT's phi-terms consumed
+      for (int j = tid; j < nphp; j += kBlock) {
+        const dbl2 tr = s_trig[j];
+        dbl2 v; v.x = pT * tr.x; v.y = pT * tr.y;
+        s_cs[j] = v;
+      }
+      for (int idx = tid; idx < nt * nphp; idx += kBlock) {
+        const int t = idx / nphp, j = idx % nphp;
+        const double* R = s_rec + t * NREC;
+        dbl2 v; v.x = 0.0; v.y = 0.0;
+        if (j < A.nphi && R[R_KIND] != 0.0) {
+          const dbl2 tr = s_trig[j];
+          v = phiterms(MODE, R, pT, tr.x, tr.y);
+        }
+        s_bp[t * nphp + j] = v;
+      }
+      __syncthreads();
+      if (!active) continue;
+      for (int t = 0; t < nt; t++) {
+        const double* R = s_rec + t * NREC;
+        const double kind = R[R_KIND];
+        if (kind == 0.0) continue;
+        double rn_abs = R[R_RENORM];
+        if (MODE == PTM || MODE == PTB) {
+          const double rn = (MODE == PTM) ? A.renorm[(cb + t) * A.npart + s] : R[R_RENORM];
+          if (!isfinite(rn)) continue;    // cell skipped for this species (SpacetimeDistribution.cpp:972-976)
+          rn_abs = fabs(rn);
+        }
+        double cell = 0.0;
+        for (int task = slot; task < A.ntask; task += nslot) {
+          const int kk = task / A.nl, l = task % A.nl;
+          const int k = kk % A.nk, jb = kk / A.nk, j0 = jb * kJmax;
+          const double* Y = s_y + ((long)t * A.nq + k * A.nl + l) * NYT;
+          const dbl2* BP = s_bp + t * nphp + j0;
+          const dbl2* W = (const dbl2*)(s_w + j0);
+          const bool sep = (MODE <= CE) || kind == 1.0 || Y[Y_NARROW] != 0.0;
+          if (sep) {
+            SepLane L;
+            sep_setup(sep_flavor(MODE), R, Y, mT, mT2, m2, mTb, pT, sign, baryon, L);
+            if (L.skip) continue;
+            cell += L.fast ? sep_phi_wsum<MODE, FLAGS, true>(L, s_cs + j0, BP, W)
+                           : sep_phi_wsum<MODE, FLAGS, false>(L, s_cs + j0, BP, W);
+          } else if (MODE >= PTM) {
+            ModLane M;
+            mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, M);
+            if (M.skip) continue;
+            cell += mod_phi_wsum<FLAGS>(M, s_cs + j0, W);
+          }
+        }
+        s_red[t * kBlock + tid] = fma(wpT, cell, s_red[t * kBlock + tid]);
+      }
+    }
+    __syncthreads();
+    // per (species, cell): sum of the species' slot columns in slot order (idle slots hold 0)
+    for (int idx = tid; idx < A.Sl * nt; idx += kBlock) {
+      const int sl = idx % A.Sl, t = idx / A.Sl;
+      const int s2 = grp * A.Sl + sl;
+      if (s2 >= A.npart) continue;
+      double acc = 0.0;
+      for (int w = 0; w < 4; w++)
+        for (int yl = 0; yl < A.Yl; yl++) acc += s_red[t * kBlock + w * 64 + yl * A.Sl + sl];
+      A.ycell[(long)s2 * A.n + cb + t] = acc;
+    }
+  }
+}
+
+// per-cell spacetime bin indices (SpacetimeDistribution.cpp:380-392): keys[0..2][c] = itau, ir, iphi (-1 outside)
+struct KeyArgs {
+  const double *tau, *x, *y; long n;
+  double tau_min, tau_width, r_min, r_width, phip_width;
+  int tau_bins, r_bins, phip_bins;
+  int* keys;
+};
+
+__global__ __launch_bounds__(256) void k_stkeys(KeyArgs A) {
+  const long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= A.n) return;
+  const double two_pi = 2.0 * M_PI;
+  const double x = A.x[c], y = A.y[c], tau = A.tau[c];
+  const double r = sqrt(x * x + y * y);
+  double phi = atan2(y, x);
+  if (phi < 0.0) phi += two_pi;
+  const long itau = (int)floor((tau - A.tau_min) / A.tau_width);
+  const long ir = (int)floor((r - A.r_min) / A.r_width);
+  const long iphi = (int)floor(phi / A.phip_width);
+  A.keys[c] = (itau >= 0 && itau < A.tau_bins) ? (int)itau : -1;
+  A.keys[A.n + c] = (ir >= 0 && ir < A.r_bins) ? (int)ir : -1;
+  A.keys[2 * A.n + c] = (iphi >= 0 && iphi < A.phip_bins) ? (int)iphi : -1;
+}
+
+// part[s_orig][e] = prefactor g_s x sum over the cells of entry e = (distribution, thread slice n, bin),
+// cells in ascending order (the reference's per-thread order); perm/offs: CSR built on the host
+struct BinArgs {
+  const double* ycell; long n; int npart;
+  const int *perm; const long* offs; long nent;
+  const int* sorig; const double* sdegen; double prefactor;
+  double* part;
+};
+
+__global__ __launch_bounds__(256) void k_stbin(BinArgs A) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= A.nent * A.npart) return;
+  const int s = (int)(idx / A.nent);
+  const long e = idx % A.nent;
+  const double f = A.prefactor * A.sdegen[s];
+  double acc = 0.0;
+  for (long i = A.offs[e]; i < A.offs[e + 1]; i++) {
+    acc += f * A.ycell[(long)s * A.n + A.perm[i]];
+  }
+  A.part[(long)A.sorig[s] * A.nent + e] = acc;
+}
+
 __global__ void k_df_eval(DfTables tb, double T, double muB, double E, double P, double bulkPi, double* out, int* err) {
   DfCoef df;
   *err = df_eval(tb, T, muB, E, P, bulkPi, df);
@@ -464,6 +707,9 @@ struct is3d_engine {
   std::vector<int> order;
   std::vector<double> pdg_mass, pdg_sign, pdg_degen, pdg_baryon;
   std::vector<double> pT, phi, y, eta, eta_w;
+  std::vector<double> pT_w, phi_w;       // operation 0 quadrature weights
+  bool have_weights = false, have_bins = false;
+  is3d_spacetime_bins bins{};
   int gla_alpha = 0, gla_pts = 0;
   std::vector<double> gla_r, gla_w;
   int nT = 0, nmuB = 0;
@@ -479,12 +725,18 @@ struct is3d_engine {
   double* d_const = nullptr; size_t const_len = 0;    // species, grids, gla, pdg
   const double *d_smass = nullptr, *d_ssign = nullptr, *d_sbaryon = nullptr, *d_sdegen = nullptr, *d_degen_orig = nullptr;
   const double *d_pT = nullptr, *d_cphi = nullptr, *d_sphi = nullptr, *d_y = nullptr, *d_eta = nullptr, *d_etaw = nullptr;
+  const double *d_pTw = nullptr, *d_phiw = nullptr;
   const double *d_gla = nullptr;
   const double *d_pdg = nullptr;
   int* d_sorig = nullptr;
   double* d_surf = nullptr; bool surf_owned = false; long ncell = 0; long surf_cap = 0;
   double *d_rec = nullptr, *d_aux = nullptr, *d_sol = nullptr, *d_renorm = nullptr, *d_slab = nullptr, *d_out = nullptr;
   long rec_cap = 0, aux_cap = 0, sol_cap = 0, renorm_cap = 0, slab_cap = 0, out_cap = 0;
+  // operation 0
+  double *d_ycell = nullptr, *d_part = nullptr; long ycell_cap = 0, part_cap = 0;
+  int *d_keys = nullptr, *d_perm = nullptr; long keys_cap = 0, perm_cap = 0;
+  long* d_offs = nullptr; long offs_cap = 0;
+  long ycell_n = -1;
   int* d_err = nullptr;
   unsigned long long* d_cnt = nullptr;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -528,6 +780,7 @@ extern "C" void is3d_destroy(is3d_engine* e) {
   dfree(e->d_tables); dfree(e->d_const);
   if (e->surf_owned) dfree(e->d_surf);
   dfree(e->d_rec); dfree(e->d_aux); dfree(e->d_sol); dfree(e->d_renorm); dfree(e->d_slab); dfree(e->d_out);
+  dfree(e->d_ycell); dfree(e->d_part); dfree(e->d_keys); dfree(e->d_perm); dfree(e->d_offs);
   dfree(e->d_err); dfree(e->d_cnt);
   for (auto& v : e->ev) if (v) (void)hipEventDestroy(v);
   delete e;
@@ -537,7 +790,8 @@ extern "C" const char* is3d_last_error(const is3d_engine* e) { return e ? e->err
 
 extern "C" int is3d_set_params(is3d_engine* e, const is3d_params* p) {
   if (!e || !p) return IS3D_ERR_ARG;
-  if (p->operation != 1) return e->fail(IS3D_ERR_UNSUPPORTED, "calculate_spectra: only operation = 1 (continuous spectra) is on this path");
+  if (p->operation != 0 && p->operation != 1)
+    return e->fail(IS3D_ERR_UNSUPPORTED, "calculate_spectra: operation = 2 (particle sampler) is not on this path; use 0 or 1");
   if (p->dimension != 2 && p->dimension != 3) return e->fail(IS3D_ERR_ARG, "EmissionFunctionArray error: need to set dimension = (2,3)");
   if (p->df_mode < 1 || p->df_mode > 5) return e->fail(IS3D_ERR_ARG, "EmissionFunctionArray error: need to set df_mode = (1,2,3,4,5)");
   if (p->df_mode == PTB && p->include_baryon) return e->fail(IS3D_ERR_UNSUPPORTED, "Bilinear interpolation error: Jonah df doesn't work for nonzero muB. Exiting..");
@@ -583,6 +837,27 @@ extern "C" int is3d_set_momentum_grid(is3d_engine* e, int npT, const double* pT,
   e->eta_w.assign(eta_weight ? eta_weight : pT, eta_weight ? eta_weight + std::max(neta, 0) : pT);
   e->have_grid = true;
   e->tables_dirty = true;
+  return IS3D_OK;
+}
+
+extern "C" int is3d_set_momentum_weights(is3d_engine* e, const double* pT_weight, const double* phi_weight) {
+  if (!e) return IS3D_ERR_ARG;
+  if (!e->have_grid) return e->fail(IS3D_ERR_STATE, "is3d_set_momentum_grid not called");
+  if (!pT_weight || !phi_weight) return e->fail(IS3D_ERR_ARG, "null pT/phi weights");
+  e->pT_w.assign(pT_weight, pT_weight + e->pT.size());
+  e->phi_w.assign(phi_weight, phi_weight + e->phi.size());
+  e->have_weights = true;
+  e->tables_dirty = true;
+  return IS3D_OK;
+}
+
+extern "C" int is3d_set_spacetime_bins(is3d_engine* e, const is3d_spacetime_bins* b) {
+  if (!e || !b) return IS3D_ERR_ARG;
+  if (b->tau_bins <= 0 || b->r_bins <= 0 || b->phip_bins <= 0) return e->fail(IS3D_ERR_ARG, "spacetime bins must be positive");
+  if (!(b->tau_max > b->tau_min) || !(b->r_max > b->r_min)) return e->fail(IS3D_ERR_ARG, "spacetime bin ranges must be increasing");
+  if (b->threads < 0) return e->fail(IS3D_ERR_ARG, "spacetime threads must be >= 0");
+  e->bins = *b;
+  e->have_bins = true;
   return IS3D_OK;
 }
 
@@ -685,6 +960,9 @@ static int finalize_tables(is3d_engine* e) {
   for (size_t j = 0; j < e->phi.size(); j++) { cph[j] = std::cos(e->phi[j]); sph[j] = std::sin(e->phi[j]); }
   const size_t oc = cput(cph.data(), cph.size()), os = cput(sph.data(), sph.size());
   const size_t oy = cput(e->y.data(), e->y.size()), oe = cput(e->eta.data(), e->eta.size()), ow = cput(e->eta_w.data(), e->eta_w.size());
+  std::vector<double> pTw(e->pT.size(), 0.0), phiw(e->phi.size(), 0.0);
+  if (e->have_weights) { pTw = e->pT_w; phiw = e->phi_w; }
+  const size_t opw = cput(pTw.data(), pTw.size()), ophw = cput(phiw.data(), phiw.size());
   const size_t og = cput(e->gla_r.data(), e->gla_r.size());
   cput(e->gla_w.data(), e->gla_w.size());
   const size_t opd = cput(e->pdg_mass.data(), e->pdg_mass.size());
@@ -704,6 +982,7 @@ static int finalize_tables(is3d_engine* e) {
   e->d_degen_orig = e->d_const + odg; e->d_pT = e->d_const + opt; e->d_cphi = e->d_const + oc; e->d_sphi = e->d_const + os;
   e->d_y = e->d_const + oy; e->d_eta = e->d_const + oe; e->d_etaw = e->d_const + ow;
   e->d_gla = e->d_const + og; e->d_pdg = e->d_const + opd;
+  e->d_pTw = e->d_const + opw; e->d_phiw = e->d_const + ophw;
   e->tables_dirty = false;
   return IS3D_OK;
 }
@@ -760,6 +1039,7 @@ static bool ensure(T*& p, long& cap, long need) {
 
 static PrepConsts make_consts(const is3d_engine* e) {
   PrepConsts k{};
+  k.operation = 1;
   k.df_mode = e->p.df_mode; k.dim = e->p.dimension; k.include_baryon = e->p.include_baryon;
   k.include_bulk = e->p.include_bulk_deltaf; k.include_shear = e->p.include_shear_deltaf;
   k.include_diff = e->p.include_baryondiff_deltaf;
@@ -873,7 +1153,7 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   sa.pT = e->d_pT; sa.cphi = e->d_cphi; sa.sphi = e->d_sphi; sa.yv = e->d_y; sa.etav = e->d_eta; sa.etaw = e->d_etaw;
   sa.npart = np; sa.npT = npT; sa.nphi = nphi; sa.ny_out = ny_out; sa.nk = nk; sa.nl = nl; sa.nq = nk * nl; sa.njb = njb;
   sa.ntask = ntask; sa.cells_per_split = cps; sa.nbx = (int)bx; sa.nsplit = (int)nsplit; sa.sstride = sstride;
-  sa.regulate = e->p.regulate_deltaf; sa.outflow = e->p.outflow; sa.dim = dim;
+  sa.regulate = e->p.regulate_deltaf; sa.outflow = e->p.outflow; sa.dim = dim; sa.op = 1;
   const size_t shmem = sizeof(double) * (2 * (size_t)kTile * NREC + 2 * (size_t)(kTile + 2) * njb * kJmax + (size_t)(nk + 2 * nl) +
                                          (size_t)kTile * sa.nq * NYT);
   if (shmem > 160 * 1024) return e->fail(IS3D_ERR_ARG, "momentum grid too large for the LDS tile");
@@ -935,6 +1215,212 @@ extern "C" int is3d_calculate_spectra(is3d_engine* e, double* dN_out) {
   rc = is3d_finish(e);
   if (rc) return rc;
   HIPCHK(e, hipMemcpy(dN_out, e->d_out, outsize * sizeof(double), hipMemcpyDeviceToHost));
+  return IS3D_OK;
+}
+
+template <int MODE>
+static void launch_dndx(dim3 grid, size_t shmem, hipStream_t st, const DndxArgs& a, int flags) {
+  switch (flags) {
+    case 0: hipLaunchKernelGGL((k_dndx<MODE, 0>), grid, dim3(kBlock), shmem, st, a); break;
+    case 1: hipLaunchKernelGGL((k_dndx<MODE, 1>), grid, dim3(kBlock), shmem, st, a); break;
+    case 2: hipLaunchKernelGGL((k_dndx<MODE, 2>), grid, dim3(kBlock), shmem, st, a); break;
+    default: hipLaunchKernelGGL((k_dndx<MODE, 3>), grid, dim3(kBlock), shmem, st, a); break;
+  }
+}
+
+// operation = 0 (SpacetimeDistribution.cpp:31-1250): device prepass + per-(species, cell) yields + binning
+// into thread slices; the host then applies the reference's per-species reset (byte-count memset,
+// :165-167 / :628-630) and writes the bin-normalised distributions (:407-440).
+extern "C" int is3d_calculate_dN_dX(is3d_engine* e, double* dN_taudtaudy, double* dN_2pirdrdy, double* dN_dphidy) {
+  if (!e) return IS3D_ERR_ARG;
+  if (!dN_taudtaudy || !dN_2pirdrdy || !dN_dphidy) return e->fail(IS3D_ERR_ARG, "null output");
+  if (!e->have_params) return e->fail(IS3D_ERR_STATE, "is3d_set_params not called");
+  if (e->p.df_mode == PTMA) return e->fail(IS3D_ERR_UNSUPPORTED, "calculate_spectra error: no spacetime distribution routine for famod yet");
+  if (!e->have_weights) return e->fail(IS3D_ERR_STATE, "is3d_set_momentum_weights not called");
+  if (!e->have_bins) return e->fail(IS3D_ERR_STATE, "is3d_set_spacetime_bins not called");
+  int rc = finalize_tables(e);
+  if (rc) return rc;
+  HIPCHK(e, hipSetDevice(e->device));
+  hipStream_t st = nullptr;
+  const long n = e->ncell;
+  const int mode = e->p.df_mode, dim = e->p.dimension;
+  const int np = (int)e->mass.size(), npT = (int)e->pT.size(), nphi = (int)e->phi.size();
+  const int nk = (dim == 3) ? (int)e->y.size() : 1, nl = (dim == 3) ? 1 : (int)e->eta.size();
+  const is3d_spacetime_bins& B = e->bins;
+  const long C = std::max(1, B.threads);
+  const int carry = B.threads >= 1;
+  const long nb[3] = {B.tau_bins, B.r_bins, B.phip_bins};
+  const long nent = C * (nb[0] + nb[1] + nb[2]);
+  e->st = is3d_stats{};
+  e->st.cells = n;
+  std::vector<double> part((size_t)np * nent, 0.0);
+  HIPCHK(e, hipMemsetAsync(e->d_err, 0, sizeof(int), st));
+  HIPCHK(e, hipMemsetAsync(e->d_cnt, 0, 8 * sizeof(unsigned long long), st));
+  HIPCHK(e, hipEventRecord(e->ev[0], st));
+  if (n > 0) {
+    if (!ensure(e->d_rec, e->rec_cap, (long)NREC * n)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(records) failed");
+    if (!ensure(e->d_aux, e->aux_cap, 9L * n)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(aux) failed");
+    PrepArgs pa{};
+    pa.k = make_consts(e); pa.k.operation = 0;
+    pa.tb = e->dtb; pa.surf = e->d_surf; pa.rec = e->d_rec; pa.aux = e->d_aux; pa.n = n;
+    pa.err = e->d_err; pa.cnt = e->d_cnt;
+    const dim3 g1((unsigned)((n + 255) / 256)), b1(256);
+    switch (mode) {
+      case GRAD: hipLaunchKernelGGL(k_prep<GRAD>, g1, b1, 0, st, pa); break;
+      case CE: hipLaunchKernelGGL(k_prep<CE>, g1, b1, 0, st, pa); break;
+      case PTM: hipLaunchKernelGGL(k_prep<PTM>, g1, b1, 0, st, pa); break;
+      default: hipLaunchKernelGGL(k_prep<PTB>, g1, b1, 0, st, pa); break;
+    }
+    HIPCHK(e, hipGetLastError());
+    if (mode == PTM) {
+      if (!ensure(e->d_renorm, e->renorm_cap, n * (long)np)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(renorm) failed");
+      RenormArgs ra{};
+      ra.k = pa.k; ra.rec = e->d_rec; ra.aux = e->d_aux; ra.renorm = e->d_renorm;
+      ra.mass = e->d_smass; ra.sign = e->d_ssign; ra.degen = e->d_sdegen; ra.baryon = e->d_sbaryon; ra.n = n; ra.npart = np;
+      const long tot = n * (long)np;
+      hipLaunchKernelGGL(k_renorm, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, ra);
+      HIPCHK(e, hipGetLastError());
+    }
+  }
+  HIPCHK(e, hipEventRecord(e->ev[1], st));
+  if (n > 0) {
+    // --- per-(species, cell) yields
+    const int njb = (nphi + kJmax - 1) / kJmax;
+    DndxArgs da{};
+    da.ntask = nk * njb * nl;
+    da.Sl = std::min(np, 64);
+    da.Yl = 64 / da.Sl;
+    da.nbx = (np + da.Sl - 1) / da.Sl;
+    long cpw = 4L * kTile;
+    if ((long)da.nbx * ((n + cpw - 1) / cpw) < 4096) cpw = kTile;
+    da.cells_per_wg = cpw;
+    da.nchunk = (n + cpw - 1) / cpw;
+    if (!ensure(e->d_ycell, e->ycell_cap, (long)np * n)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(cell yields) failed");
+    da.rec = e->d_rec; da.n = n; da.renorm = e->d_renorm; da.ycell = e->d_ycell;
+    da.smass = e->d_smass; da.ssign = e->d_ssign; da.sbaryon = e->d_sbaryon;
+    da.pT = e->d_pT; da.pTw = e->d_pTw; da.cphi = e->d_cphi; da.sphi = e->d_sphi; da.phiw = e->d_phiw;
+    da.yv = e->d_y; da.etav = e->d_eta; da.etaw = e->d_etaw;
+    da.npart = np; da.npT = npT; da.nphi = nphi; da.nk = nk; da.nl = nl; da.nq = nk * nl; da.njb = njb; da.dim = dim;
+    const size_t nphp = (size_t)njb * kJmax;
+    const size_t shmem = sizeof(double) * ((size_t)kTile * NREC + 2 * nphp + 2 * nphp + nphp + 2 * (size_t)kTile * nphp +
+                                           (size_t)kTile * kBlock + (size_t)(nk + 2 * nl) + (size_t)kTile * da.nq * NYT);
+    if (shmem > 160 * 1024) return e->fail(IS3D_ERR_ARG, "momentum grid too large for the LDS tile");
+    const long nwg = (long)da.nbx * da.nchunk;
+    if (nwg > 0x7fffffffL) return e->fail(IS3D_ERR_ARG, "surface too large for one dN/dX launch");
+    const int kflags = (e->p.regulate_deltaf ? F_REG : 0) | (e->p.outflow ? F_OUT : 0);
+    switch (mode) {
+      case GRAD: launch_dndx<GRAD>(dim3((unsigned)nwg), shmem, st, da, kflags); break;
+      case CE: launch_dndx<CE>(dim3((unsigned)nwg), shmem, st, da, kflags); break;
+      case PTM: launch_dndx<PTM>(dim3((unsigned)nwg), shmem, st, da, kflags); break;
+      default: launch_dndx<PTB>(dim3((unsigned)nwg), shmem, st, da, kflags); break;
+    }
+    HIPCHK(e, hipGetLastError());
+    e->ycell_n = n;
+  } else {
+    e->ycell_n = 0;
+  }
+  HIPCHK(e, hipEventRecord(e->ev[2], st));
+  if (n > 0) {
+    // --- bin keys on the device, CSR (thread slice, bin) -> cells on the host, sums on the device
+    if (!ensure(e->d_keys, e->keys_cap, 3 * n)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(keys) failed");
+    KeyArgs ka{};
+    ka.tau = e->d_surf; ka.x = e->d_surf + n; ka.y = e->d_surf + 2 * n; ka.n = n;
+    ka.tau_min = B.tau_min; ka.tau_width = (B.tau_max - B.tau_min) / (double)B.tau_bins;
+    ka.r_min = B.r_min; ka.r_width = (B.r_max - B.r_min) / (double)B.r_bins;
+    ka.phip_width = 2.0 * M_PI / (double)B.phip_bins;
+    ka.tau_bins = B.tau_bins; ka.r_bins = B.r_bins; ka.phip_bins = B.phip_bins; ka.keys = e->d_keys;
+    hipLaunchKernelGGL(k_stkeys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, ka);
+    HIPCHK(e, hipGetLastError());
+    std::vector<int> keys((size_t)3 * n);
+    HIPCHK(e, hipMemcpy(keys.data(), e->d_keys, keys.size() * sizeof(int), hipMemcpyDeviceToHost));
+    std::vector<long> offs((size_t)nent + 1, 0);
+    long off_d[3] = {0, C * nb[0], C * (nb[0] + nb[1])};
+    for (int d = 0; d < 3; d++)
+      for (long c = 0; c < n; c++) {
+        const int kb = keys[(size_t)d * n + c];
+        if (kb >= 0) offs[off_d[d] + (c % C) * nb[d] + kb + 1]++;
+      }
+    for (long i = 0; i < nent; i++) offs[i + 1] += offs[i];
+    std::vector<int> perm((size_t)std::max(offs[nent], 1L));
+    std::vector<long> fill(offs.begin(), offs.end() - 1);
+    for (int d = 0; d < 3; d++)
+      for (long c = 0; c < n; c++) {
+        const int kb = keys[(size_t)d * n + c];
+        if (kb >= 0) perm[fill[off_d[d] + (c % C) * nb[d] + kb]++] = (int)c;
+      }
+    if (!ensure(e->d_perm, e->perm_cap, (long)perm.size())) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(perm) failed");
+    if (!ensure(e->d_offs, e->offs_cap, nent + 1)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(offsets) failed");
+    if (!ensure(e->d_part, e->part_cap, (long)np * nent)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(bins) failed");
+    HIPCHK(e, hipMemcpy(e->d_perm, perm.data(), perm.size() * sizeof(int), hipMemcpyHostToDevice));
+    HIPCHK(e, hipMemcpy(e->d_offs, offs.data(), offs.size() * sizeof(long), hipMemcpyHostToDevice));
+    BinArgs ba{};
+    ba.ycell = e->d_ycell; ba.n = n; ba.npart = np;
+    ba.perm = e->d_perm; ba.offs = e->d_offs; ba.nent = nent;
+    ba.sorig = e->d_sorig; ba.sdegen = e->d_sdegen; ba.prefactor = std::pow(2.0 * M_PI * kHbarC, -3);
+    ba.part = e->d_part;
+    const long nthr = nent * np;
+    hipLaunchKernelGGL(k_stbin, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, st, ba);
+    HIPCHK(e, hipGetLastError());
+  }
+  HIPCHK(e, hipEventRecord(e->ev[3], st));
+  HIPCHK(e, hipEventSynchronize(e->ev[3]));
+  int derr = 0;
+  HIPCHK(e, hipMemcpy(&derr, e->d_err, sizeof(int), hipMemcpyDeviceToHost));
+  if (n > 0) HIPCHK(e, hipMemcpy(part.data(), e->d_part, part.size() * sizeof(double), hipMemcpyDeviceToHost));
+  float ms = 0.f;
+  if (hipEventElapsedTime(&ms, e->ev[0], e->ev[1]) == hipSuccess) e->st.ms_prepass = ms;
+  if (hipEventElapsedTime(&ms, e->ev[1], e->ev[2]) == hipSuccess) e->st.ms_spectra = ms;
+  if (hipEventElapsedTime(&ms, e->ev[0], e->ev[3]) == hipSuccess) e->st.ms_total = ms;
+  switch (derr) {
+    case DF_OK: break;
+    case DF_SPLINE_RANGE: return e->fail(IS3D_ERR_DF_RANGE, "gsl: interp.c: interpolation error (df coefficient spline evaluated outside its table)");
+    case DF_TABLE_RANGE: return e->fail(IS3D_ERR_DF_RANGE, "Error: (T,muB) outside df coefficient table. Exiting...");
+    case DF_PTB_BARYON: return e->fail(IS3D_ERR_UNSUPPORTED, "Bilinear interpolation error: Jonah df doesn't work for nonzero muB. Exiting..");
+    default: return e->fail(IS3D_ERR_ARG, "Error: set df_mode = (1,2) in parameters.dat");
+  }
+  // --- the reference's per-species thread-slice reset and bin normalisation
+  const double two_pi = 2.0 * M_PI;
+  const double width[3] = {(B.tau_max - B.tau_min) / (double)B.tau_bins, (B.r_max - B.r_min) / (double)B.r_bins,
+                           two_pi / (double)B.phip_bins};
+  double* outs[3] = {dN_taudtaudy, dN_2pirdrdy, dN_dphidy};
+  long off = 0;
+  for (int d = 0; d < 3; d++) {
+    const long bins = nb[d];
+    std::vector<double> all((size_t)C * bins, 0.0);
+    for (int k = 0; k < np; k++) {
+      if (carry) std::memset(all.data(), 0, (size_t)(C * bins));   // bytes, not doubles (:165-167)
+      else std::fill(all.begin(), all.end(), 0.0);
+      const double* pk = part.data() + (size_t)k * nent + off;
+      for (long t = 0; t < C; t++)
+        for (long i = 0; i < bins; i++) all[i + t * bins] += pk[t * bins + i];
+      for (long i = 0; i < bins; i++) {
+        double acc = 0.0;
+        for (long t = 0; t < C; t++) acc += all[i + t * bins];
+        double norm = width[d];
+        if (d == 0) norm = (B.tau_min + width[0] * ((double)i + 0.5)) * width[0];
+        else if (d == 1) norm = two_pi * (B.r_min + width[1] * ((double)i + 0.5)) * width[1];
+        outs[d][(size_t)k * bins + i] = acc / norm;
+      }
+    }
+    off += C * bins;
+  }
+  return IS3D_OK;
+}
+
+extern "C" int is3d_get_cell_yields(const is3d_engine* e, double* dN_dy_cell) {
+  if (!e || !dN_dy_cell) return IS3D_ERR_ARG;
+  if (e->ycell_n < 0) return IS3D_ERR_STATE;
+  const long n = e->ycell_n;
+  const int np = (int)e->mass.size();
+  if (n == 0) return IS3D_OK;
+  std::vector<double> y((size_t)np * n);
+  if (hipSetDevice(e->device) != hipSuccess) return IS3D_ERR_DEVICE;
+  if (hipMemcpy(y.data(), e->d_ycell, y.size() * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) return IS3D_ERR_DEVICE;
+  const double pref = std::pow(2.0 * M_PI * kHbarC, -3);
+  for (int s = 0; s < np; s++) {
+    const int so = e->order[s];
+    for (long c = 0; c < n; c++) dN_dy_cell[(size_t)so * n + c] = pref * e->degen[so] * y[(size_t)s * n + c];
+  }
   return IS3D_OK;
 }
 

@@ -502,5 +502,32 @@ std::string write_spectra_files(const std::string& dir, const SpectraView& v) {
   return "";
 }
 
+std::string write_spacetime_files(const std::string& dir, const SpacetimeView& v) {
+  const std::string out = join(dir, "results/continuous");
+  mkdirs(out);
+  const double two_pi = 2.0 * M_PI;
+  const double tau_w = (v.tau_max - v.tau_min) / (double)v.tau_bins, r_w = (v.r_max - v.r_min) / (double)v.r_bins;
+  const double phi_w = two_pi / (double)v.phip_bins;
+  for (long ipart = 0; ipart < v.npart; ipart++) {
+    const long mc = (*v.mcid)[ipart];
+    char ft[512], fr[512], fp[512];
+    std::snprintf(ft, sizeof(ft), "%s/dN_taudtaudy_%ld.dat", out.c_str(), mc);
+    std::snprintf(fr, sizeof(fr), "%s/dN_2pirdrdy_%ld.dat", out.c_str(), mc);
+    std::snprintf(fp, sizeof(fp), "%s/dN_dphidy_%ld.dat", out.c_str(), mc);
+    std::ofstream t(ft, std::ios_base::app), r(fr, std::ios_base::app), a(fp, std::ios_base::app);   // appended, as the reference
+    if (!t || !r || !a) return std::string("cannot write spacetime distributions of ") + std::to_string(mc);
+    for (long ir = 0; ir < v.r_bins; ir++)
+      r << std::setprecision(6) << std::scientific << v.r_min + r_w * ((double)ir + 0.5) << "\t"
+        << v.dN_2pirdrdy[ipart * v.r_bins + ir] << "\n";
+    for (long it = 0; it < v.tau_bins; it++)
+      t << std::setprecision(6) << std::scientific << v.tau_min + tau_w * ((double)it + 0.5) << "\t"
+        << v.dN_taudtaudy[ipart * v.tau_bins + it] << "\n";
+    for (long ip = 0; ip < v.phip_bins; ip++)
+      a << std::setprecision(6) << std::scientific << phi_w * ((double)ip + 0.5) << "\t"
+        << v.dN_dphidy[ipart * v.phip_bins + ip] << "\n";
+  }
+  return "";
+}
+
 }  // namespace host
 }  // namespace is3d

@@ -81,5 +81,18 @@ struct SpectraView {
 };
 std::string write_spectra_files(const std::string& dir, const SpectraView& v);
 
+// operation = 0 writers (SpacetimeDistribution.cpp:138-145, 407-440): dN_taudtaudy_<mcid>.dat,
+// dN_2pirdrdy_<mcid>.dat, dN_dphidy_<mcid>.dat under <dir>/results/continuous/, opened in append mode,
+// "bin midpoint \t value" with setprecision(6) scientific.
+struct SpacetimeView {
+  const double *dN_taudtaudy, *dN_2pirdrdy, *dN_dphidy;   // [species][bins], bin-normalised
+  int npart;
+  double tau_min, tau_max; int tau_bins;
+  double r_min, r_max; int r_bins;
+  int phip_bins;
+  const std::vector<long>* mcid;
+};
+std::string write_spacetime_files(const std::string& dir, const SpacetimeView& v);
+
 }  // namespace host
 }  // namespace is3d

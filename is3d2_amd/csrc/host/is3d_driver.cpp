@@ -60,24 +60,43 @@ static void set_or_throw(is3d_engine* e, int rc) {
   if (rc != IS3D_OK) throw std::runtime_error(std::string("is3d engine: ") + is3d_last_error(e));
 }
 
-void EmissionFunctionArray::calculate_spectra(const RunOptions& opt) {
+static is3d_params engine_params(const ParameterReader& p, int operation, int dimension) {
   is3d_params prm{};
-  prm.operation = 1;
-  prm.dimension = dimension_;
-  prm.df_mode = (int)p_.get("df_mode");
-  prm.include_baryon = (int)p_.get("include_baryon");
-  prm.include_bulk_deltaf = (int)p_.get("include_bulk_deltaf");
-  prm.include_shear_deltaf = (int)p_.get("include_shear_deltaf");
-  prm.include_baryondiff_deltaf = (int)p_.get("include_baryondiff_deltaf");
-  prm.regulate_deltaf = (int)p_.get("regulate_deltaf");
-  prm.outflow = (int)p_.get("outflow");
-  prm.deta_min = p_.get("deta_min");
-  prm.mass_pion0 = p_.get("mass_pion0");
-  prm.famod_chains = (int)p_.get("famod_chains", 0.0);
+  prm.operation = operation;
+  prm.dimension = dimension;
+  prm.df_mode = (int)p.get("df_mode");
+  prm.include_baryon = (int)p.get("include_baryon");
+  prm.include_bulk_deltaf = (int)p.get("include_bulk_deltaf");
+  prm.include_shear_deltaf = (int)p.get("include_shear_deltaf");
+  prm.include_baryondiff_deltaf = (int)p.get("include_baryondiff_deltaf");
+  prm.regulate_deltaf = (int)p.get("regulate_deltaf");
+  prm.outflow = (int)p.get("outflow");
+  prm.deta_min = p.get("deta_min");
+  prm.mass_pion0 = p.get("mass_pion0");
+  prm.famod_chains = (int)p.get("famod_chains", 0.0);
+  return prm;
+}
+
+// operation = 0 binning from the parameter file (EmissionFunction.cpp:232-247); spacetime_threads (ours,
+// default 0) = the reference run's OpenMP thread count to reproduce its memset carry (is3d_amd.h)
+static is3d_spacetime_bins spacetime_bins(const ParameterReader& p) {
+  is3d_spacetime_bins b{};
+  b.tau_min = p.get("tau_min", 0.0); b.tau_max = p.get("tau_max", 12.0); b.tau_bins = (int)p.get("tau_bins", 120.0);
+  b.r_min = p.get("r_min", 0.0); b.r_max = p.get("r_max", 12.0); b.r_bins = (int)p.get("r_bins", 60.0);
+  b.phip_bins = (int)p.get("phip_bins", 100.0);
+  b.threads = (int)p.get("spacetime_threads", 0.0);
+  return b;
+}
+
+void EmissionFunctionArray::run_sharded(const RunOptions& opt, int operation) {
+  const is3d_params prm = engine_params(p_, operation, dimension_);
+  const is3d_spacetime_bins bins = spacetime_bins(p_);
   const int ndev = std::max(1, opt.num_devices);
   std::vector<double> pTv(pT_.cols[0]), phiv(phi_.cols[0]), yv(y_.cols[0]), etav(eta_.cols[0]), etaw(eta_.cols[1]);
+  std::vector<double> pTw(pT_.ncols() > 1 ? pT_.cols[1] : std::vector<double>(pTv.size(), 0.0));
+  std::vector<double> phiw(phi_.ncols() > 1 ? phi_.cols[1] : std::vector<double>(phiv.size(), 0.0));
   const long n = surf_.size();
-  long outsize = 0;
+  const int np = (int)mass_.size();
   std::vector<std::vector<double>> parts(ndev);
   std::vector<std::string> errs(ndev);
   auto t0 = std::chrono::steady_clock::now();
@@ -86,13 +105,13 @@ void EmissionFunctionArray::calculate_spectra(const RunOptions& opt) {
     if (!e) { errs[k] = "is3d_create(" + std::to_string(opt.device + k) + ") failed"; return; }
     try {
       set_or_throw(e, is3d_set_params(e, &prm));
-      set_or_throw(e, is3d_set_species(e, (int)mass_.size(), mass_.data(), sign_.data(), degen_.data(), baryon_.data()));
+      set_or_throw(e, is3d_set_species(e, np, mass_.data(), sign_.data(), degen_.data(), baryon_.data()));
       set_or_throw(e, is3d_set_pdg(e, (int)pdg_mass_.size(), pdg_mass_.data(), pdg_sign_.data(), pdg_degen_.data(), pdg_baryon_.data()));
       set_or_throw(e, is3d_set_momentum_grid(e, (int)pTv.size(), pTv.data(), (int)phiv.size(), phiv.data(), (int)yv.size(),
                                              yv.data(), (int)etav.size(), etav.data(), etaw.data()));
       set_or_throw(e, is3d_set_gauss_laguerre(e, galpha_, gpts_, gr_.data(), gw_.data()));
       set_or_throw(e, is3d_set_df_tables(e, df_.nT, df_.nmuB, df_.T.data(), df_.muB.data(), df_.tab.data(), plasma_.T));
-      // contiguous cell shard k (PTMA warm-start chains need the reference's striding: one device then)
+      // contiguous cell shard k (PTMA warm-start chains and the dN/dX thread emulation need the whole surface)
       const long lo = n * k / ndev, hi = n * (k + 1) / ndev;
       auto sl = [&](const std::vector<double>& v) { return v.empty() ? nullptr : v.data() + lo; };
       is3d_surface s{sl(surf_.tau), sl(surf_.x), sl(surf_.y), sl(surf_.eta), sl(surf_.dat), sl(surf_.dax), sl(surf_.day),
@@ -100,8 +119,16 @@ void EmissionFunctionArray::calculate_spectra(const RunOptions& opt) {
                      sl(surf_.pixx), sl(surf_.pixy), sl(surf_.pixn), sl(surf_.piyy), sl(surf_.piyn), sl(surf_.bulkPi),
                      sl(surf_.muB), sl(surf_.nB), sl(surf_.Vx), sl(surf_.Vy), sl(surf_.Vn)};
       set_or_throw(e, is3d_set_surface(e, hi - lo, &s));
-      parts[k].assign(is3d_output_size(e), 0.0);
-      set_or_throw(e, is3d_calculate_spectra(e, parts[k].data()));
+      if (operation == 1) {
+        parts[k].assign(is3d_output_size(e), 0.0);
+        set_or_throw(e, is3d_calculate_spectra(e, parts[k].data()));
+      } else {
+        set_or_throw(e, is3d_set_momentum_weights(e, pTw.data(), phiw.data()));
+        set_or_throw(e, is3d_set_spacetime_bins(e, &bins));
+        const long nt = (long)np * bins.tau_bins, nr = (long)np * bins.r_bins;
+        parts[k].assign(nt + nr + (long)np * bins.phip_bins, 0.0);
+        set_or_throw(e, is3d_calculate_dN_dX(e, parts[k].data(), parts[k].data() + nt, parts[k].data() + nt + nr));
+      }
     } catch (const std::exception& ex) {
       errs[k] = ex.what();
     }
@@ -109,15 +136,36 @@ void EmissionFunctionArray::calculate_spectra(const RunOptions& opt) {
   };
   if (prm.df_mode == 5 && prm.famod_chains > 0 && ndev > 1)
     throw std::runtime_error("famod_chains > 0 (reference warm-start emulation) runs on one device");
+  if (operation == 0 && bins.threads > 0 && ndev > 1)
+    throw std::runtime_error("spacetime_threads > 0 (reference thread-slice emulation) runs on one device");
   std::vector<std::thread> th;
   for (int k = 0; k < ndev; k++) th.emplace_back(work, k);
   for (auto& t : th) t.join();
   for (int k = 0; k < ndev; k++) if (!errs[k].empty()) throw std::runtime_error(errs[k]);
-  outsize = (long)parts[0].size();
-  dN_.assign(outsize, 0.0);
+  std::vector<double> sum(parts[0].size(), 0.0);
   for (int k = 0; k < ndev; k++)
-    for (long i = 0; i < outsize; i++) dN_[i] += parts[k][i];
+    for (size_t i = 0; i < sum.size(); i++) sum[i] += parts[k][i];
+  if (operation == 1) {
+    dN_ = std::move(sum);
+  } else {
+    const long nt = (long)np * bins.tau_bins, nr = (long)np * bins.r_bins;
+    bins_ = bins;
+    dNtau_.assign(sum.begin(), sum.begin() + nt);
+    dNr_.assign(sum.begin() + nt, sum.begin() + nt + nr);
+    dNphi_.assign(sum.begin() + nt + nr, sum.end());
+  }
   seconds_ = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
+void EmissionFunctionArray::calculate_spectra(const RunOptions& opt) { run_sharded(opt, 1); }
+
+void EmissionFunctionArray::calculate_dN_dX(const RunOptions& opt) { run_sharded(opt, 0); }
+
+void EmissionFunctionArray::write_spacetime_files(const std::string& dir) const {
+  SpacetimeView v{dNtau_.data(), dNr_.data(), dNphi_.data(), (int)mass_.size(), bins_.tau_min, bins_.tau_max,
+                  bins_.tau_bins, bins_.r_min, bins_.r_max, bins_.r_bins, bins_.phip_bins, &mcid_};
+  const std::string err = host::write_spacetime_files(dir, v);
+  if (!err.empty()) throw std::runtime_error(err);
 }
 
 void EmissionFunctionArray::write_files(const std::string& dir) const {
@@ -152,8 +200,8 @@ void IS3D::run_particlization(int fo_from_file, const RunOptions& opt) {
   ParameterReader prm;
   check(prm.read_file(path_in(dir_, "iS3D_parameters.dat")), "ParameterReader::readFromFile error: file iS3D_parameters.dat does not exist.");
   const int operation = (int)prm.get("operation");
-  check(operation == 1, "operation = " + std::to_string(operation) +
-                            " is not on this engine's path (continuous spectra, operation = 1, only)");
+  check(operation == 0 || operation == 1, "operation = " + std::to_string(operation) +
+                            " is not on this engine's path (0 spacetime distributions, 1 continuous spectra)");
   const int mode = (int)prm.get("mode"), dimension = (int)prm.get("dimension"), hrg = (int)prm.get("hrg_eos");
   const int include_baryon = (int)prm.get("include_baryon");
   Surface file_surf;
@@ -187,10 +235,24 @@ void IS3D::run_particlization(int fo_from_file, const RunOptions& opt) {
   err = read_gauss_laguerre(path_in(dir_, "tables/gauss/gla_roots_weights.txt"), galpha, gpts, gr, gw);
   check(err.empty(), err);
   EmissionFunctionArray efa(prm, chosen, pT, phi, y, eta, parts, *surf, df, avg, gr, gw, galpha, gpts);
-  efa.calculate_spectra(opt);
-  if (opt.write_files) efa.write_files(dir_);
-  if (!opt.quiet) std::printf("\nSpectra calculation took %g seconds\n\n", efa.seconds());
-  dN_ = efa.spectra();
+  if (operation == 1) {
+    efa.calculate_spectra(opt);
+    if (opt.write_files) efa.write_files(dir_);
+    if (!opt.quiet) std::printf("\nSpectra calculation took %g seconds\n\n", efa.seconds());
+    dN_ = efa.spectra();
+  } else {
+    efa.calculate_dN_dX(opt);
+    if (opt.write_files) efa.write_spacetime_files(dir_);
+    if (!opt.quiet) std::printf("\nSpacetime distributions took %g seconds\n\n", efa.seconds());
+    const int np = (int)efa.mcid().size();
+    const is3d_spacetime_bins b = efa.bins();
+    dN_.clear();
+    for (int k = 0; k < np; k++) {   // per species [tau bins | r bins | phip bins]
+      dN_.insert(dN_.end(), efa.dN_taudtaudy().begin() + (long)k * b.tau_bins, efa.dN_taudtaudy().begin() + (long)(k + 1) * b.tau_bins);
+      dN_.insert(dN_.end(), efa.dN_2pirdrdy().begin() + (long)k * b.r_bins, efa.dN_2pirdrdy().begin() + (long)(k + 1) * b.r_bins);
+      dN_.insert(dN_.end(), efa.dN_dphidy().begin() + (long)k * b.phip_bins, efa.dN_dphidy().begin() + (long)(k + 1) * b.phip_bins);
+    }
+  }
 }
 
 }  // namespace host

@@ -1,17 +1,19 @@
 // is3d_driver.h -- drop-in C++ facade of iS3D2's particlization plug-in surface for
-// operation = 1, running the MI355X engine (libis3d_amd.so) underneath.
+// operations 1 (continuous spectra) and 0 (spacetime distributions), running the MI355X engine
+// (libis3d_amd.so) underneath.
 //
 //   class IS3D                (iS3D.h:25-104)   read_fo_surf_from_memory + run_particlization
 //   class EmissionFunctionArray (EmissionFunction.h:135-140) ctor + calculate_spectra
 //
 // Same inputs (iS3D_parameters.dat, input/surface.dat, PDG/, deltaf_coefficients/, tables/
 // relative to a working directory) and the same outputs (results/continuous/*.dat).
-// Differences from the reference: errors are returned / thrown instead of exit(); only
-// operation = 1 is on this path; cells may be sharded over several GPUs in one process.
+// Differences from the reference: errors are returned / thrown instead of exit(); operation = 2
+// (the sampler) is not on this path; cells may be sharded over several GPUs in one process.
 #pragma once
 #include <string>
 #include <vector>
 
+#include "../../../include/is3d_amd.h"
 #include "host_io.h"
 
 namespace is3d {
@@ -31,10 +33,17 @@ class EmissionFunctionArray {
                         const Table& y, const Table& eta, const std::vector<Particle>& particles, const Surface& surf,
                         const DfTablesData& df, const Averages& plasma, const std::vector<double>& gla_roots,
                         const std::vector<double>& gla_weights, int gla_alpha, int gla_points);
-  // computes dN/(pT dpT dphi dy) [species][pT][phi][y]; throws std::runtime_error on failure
+  // operation = 1: dN/(pT dpT dphi dy) [species][pT][phi][y]; throws std::runtime_error on failure
   void calculate_spectra(const RunOptions& opt);
   void write_files(const std::string& dir) const;
   const std::vector<double>& spectra() const { return dN_; }
+  // operation = 0 (SpacetimeDistribution.cpp): dN/(tau dtau dy), dN/(2 pi r dr dy), dN/(dphi dy) [species][bins]
+  void calculate_dN_dX(const RunOptions& opt);
+  void write_spacetime_files(const std::string& dir) const;
+  const std::vector<double>& dN_taudtaudy() const { return dNtau_; }
+  const std::vector<double>& dN_2pirdrdy() const { return dNr_; }
+  const std::vector<double>& dN_dphidy() const { return dNphi_; }
+  is3d_spacetime_bins bins() const { return bins_; }
   const std::vector<long>& mcid() const { return mcid_; }
   double seconds() const { return seconds_; }
 
@@ -51,7 +60,10 @@ class EmissionFunctionArray {
   std::vector<double> pdg_mass_, pdg_sign_, pdg_degen_, pdg_baryon_;
   std::vector<long> mcid_;
   std::vector<double> dN_;
+  std::vector<double> dNtau_, dNr_, dNphi_;
+  is3d_spacetime_bins bins_{};
   double seconds_ = 0.0;
+  void run_sharded(const RunOptions& opt, int operation);
 };
 
 class IS3D {
@@ -65,7 +77,8 @@ class IS3D {
                                 std::vector<double> uy, std::vector<double> un, std::vector<double> pixx,
                                 std::vector<double> pixy, std::vector<double> pixn, std::vector<double> piyy,
                                 std::vector<double> piyn, std::vector<double> pinn, std::vector<double> Pi);
-  // iS3D.cpp:81-282 restricted to operation = 1; throws std::runtime_error
+  // iS3D.cpp:81-282 for operation = 1 and 0; throws std::runtime_error.  spectra() = the momentum
+  // spectra (operation 1) or, per species, [dN_taudtaudy | dN_2pirdrdy | dN_dphidy] bins (operation 0)
   void run_particlization(int fo_from_file, const RunOptions& opt = RunOptions());
   const std::vector<double>& spectra() const { return dN_; }
 

@@ -1,5 +1,6 @@
 // iS3D_amd -- drop-in replacement of the reference executable (src/cpp/Main.cpp) for
-// operation = 1: run in a directory laid out like the reference's (iS3D_parameters.dat,
+// operations 1 (continuous spectra) and 0 (spacetime distributions): run in a directory laid out
+// like the reference's (iS3D_parameters.dat,
 // input/surface.dat, PDG/, deltaf_coefficients/, tables/, results/continuous/).
 // Environment: IS3D_DEVICE (first GPU, default 0), IS3D_NUM_GPUS (cells sharded, default 1).
 #include <cstdio>

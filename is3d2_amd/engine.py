@@ -20,6 +20,13 @@ _DEFAULTS = dict(operation=1, dimension=2, df_mode=1, include_baryon=0, include_
                  famod_chains=0, deta_min=1.e-5, mass_pion0=0.138)
 
 
+# operation = 0 binning (iS3D_parameters.dat defaults; EmissionFunction.cpp:232-247).  `threads` is the
+# reference's CORES: 0 bins every species from zero; C >= 1 reproduces a reference run with
+# OMP_NUM_THREADS = C, including its per-species byte-count memset carry (SpacetimeDistribution.cpp:165-167)
+SPACETIME_BINS = dict(tau_min=0.0, tau_max=12.0, tau_bins=120, r_min=0.0, r_max=12.0, r_bins=60, phip_bins=100,
+                      threads=0)
+
+
 def _dp(a):
     return a.ctypes.data_as(C.POINTER(C.c_double))
 
@@ -78,6 +85,16 @@ class Engine:
         self._chk(self.lib.is3d_set_momentum_grid(self._e, len(a[0]), _dp(a[0]), len(a[1]), _dp(a[1]),
                                                   len(a[2]), _dp(a[2]), len(a[3]), _dp(a[3]), _dp(a[4])))
 
+    def set_momentum_weights(self, pT_w, phi_w):
+        a, b = _arr(pT_w), _arr(phi_w)
+        self._chk(self.lib.is3d_set_momentum_weights(self._e, _dp(a), _dp(b)))
+
+    def set_spacetime_bins(self, **kw):
+        b = dict(SPACETIME_BINS)
+        b.update({k: v for k, v in kw.items() if k in SPACETIME_BINS})
+        self.bins = b
+        self._chk(self.lib.is3d_set_spacetime_bins(self._e, C.byref(_lib.SpacetimeBins(**b))))
+
     def set_gauss_laguerre(self, roots, weights):
         r, w = _arr(roots), _arr(weights)
         self._chk(self.lib.is3d_set_gauss_laguerre(self._e, r.shape[0], r.shape[1], _dp(r), _dp(w)))
@@ -105,6 +122,20 @@ class Engine:
     def calculate_spectra(self):
         out = np.zeros(self.output_size(), dtype=np.float64)
         self._chk(self.lib.is3d_calculate_spectra(self._e, _dp(out)))
+        return out
+
+    def calculate_dN_dX(self):
+        """operation = 0: (dN_taudtaudy, dN_2pirdrdy, dN_dphidy), each [species][bins]."""
+        b = self.bins
+        t = np.zeros((self.npart, b["tau_bins"])); r = np.zeros((self.npart, b["r_bins"]))
+        ph = np.zeros((self.npart, b["phip_bins"]))
+        self._chk(self.lib.is3d_calculate_dN_dX(self._e, _dp(t), _dp(r), _dp(ph)))
+        return t, r, ph
+
+    def cell_yields(self):
+        """dN_dy_cell [species][cell] of the last calculate_dN_dX."""
+        out = np.zeros((self.npart, self.ncell))
+        self._chk(self.lib.is3d_get_cell_yields(self._e, _dp(out)))
         return out
 
     def launch(self, dev_out_ptr, stream_ptr=None):
@@ -152,8 +183,8 @@ def make_spec(hrg_eos=2, chosen="pikp", pT="pT24", phi="phi24", y="y21", eta="et
     parts = _hrg.pdg_particles(hrg_eos)
     mcids = _hrg.chosen_mcids(chosen) if isinstance(chosen, str) else np.asarray(chosen, dtype=np.int64)
     sp = _hrg.chosen_species(parts, mcids)
-    pTv, _ = _data.grid(pT)
-    phiv, _ = _data.grid(phi)
+    pTv, pTw = _data.grid(pT)
+    phiv, phiw = _data.grid(phi)
     yv, _ = _data.grid(y)
     etav, etaw = _data.grid(eta)
     roots, weights = _data.gauss_laguerre(gla_points)
@@ -161,8 +192,10 @@ def make_spec(hrg_eos=2, chosen="pikp", pT="pT24", phi="phi24", y="y21", eta="et
     params = dict(_DEFAULTS)
     params.update(dimension=dimension, df_mode=df_mode)
     params.update({k: v for k, v in flags.items() if k in _DEFAULTS})
+    bins = dict(SPACETIME_BINS)
+    bins.update({k: v for k, v in flags.items() if k in SPACETIME_BINS})
     return dict(params=params, species=sp, pdg=parts, pT=pTv, phi=phiv, y=yv, eta=etav, eta_w=etaw,
-                gla=(roots, weights), df=(T, muB, tab), hrg_eos=hrg_eos)
+                pT_w=pTw, phi_w=phiw, bins=bins, gla=(roots, weights), df=(T, muB, tab), hrg_eos=hrg_eos)
 
 
 def build_engine(spec, surf, T_avg=None, device=0):
@@ -174,6 +207,9 @@ def build_engine(spec, surf, T_avg=None, device=0):
     pdg = spec["pdg"]
     e.set_pdg(pdg["mass"], pdg["sign"], pdg["gspin"], pdg["baryon"])
     e.set_momentum_grid(spec["pT"], spec["phi"], spec["y"], spec["eta"], spec["eta_w"])
+    if "pT_w" in spec:
+        e.set_momentum_weights(spec["pT_w"], spec["phi_w"])
+    e.set_spacetime_bins(**spec.get("bins", {}))
     e.set_gauss_laguerre(*spec["gla"])
     if T_avg is None:
         T_avg = surface_averages(surf, p["include_baryon"])[0]

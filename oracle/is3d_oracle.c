@@ -1112,6 +1112,373 @@ static void spectra_famod(const orc_params *p, const orc_setup *s, const orc_sur
 }
 
 /* ------------------------------------------------------------------------- */
+/* operation = 0: spacetime distributions dN/dX                               */
+/* SpacetimeDistribution.cpp:31-518 (calculate_dN_dX, df_mode 1/2) and        */
+/* :520-1250 (calculate_dN_dX_feqmod, df_mode 3/4).  The reference loops       */
+/* species -> threads -> cells and recomputes the (species-independent) cell   */
+/* prologue for every species; here the prologue is computed once per cell and */
+/* the species loop is inside -- same arithmetic, same values.  Output: the    */
+/* per-(species, cell) dN/dy of the cell (dN_dy_cell, :374 / :1131), 0 for     */
+/* skipped cells.                                                              */
+/* ------------------------------------------------------------------------- */
+static void dndx_cell_grad_ce(const orc_params *p, const orc_setup *s, const orc_surface *S, const dfdata *df_data,
+                              const grid *g, const double *pTw, const double *phiw, long ic, long ncell,
+                              double *cy, char *valid, int *err) {
+  const double prefactor = pow(2.0 * M_PI * HBARC, -3);
+  const long npart = s->npart, npT = g->npT, nphi = g->nphi, ny = g->ny, neta = g->neta;
+  const int DF_MODE = p->df_mode;
+  double tau = S->tau[ic], tau2 = tau * tau;
+  double eta0 = (p->dimension == 3) ? S->eta[ic] : 0.0;     /* :181-184, thread-local (race fix) */
+  double dat = S->dat[ic], dax = S->dax[ic], day = S->day[ic], dan = S->dan[ic];
+  double ux = S->ux[ic], uy = S->uy[ic], un = S->un[ic];
+  double ut = sqrt(1.0 + ux * ux + uy * uy + tau2 * un * un);
+  if (ut * dat + ux * dax + uy * day + un * dan <= 0.0) return;   /* :197 */
+  double ux2 = ux * ux, uy2 = uy * uy, ut2 = ut * ut, utperp = sqrt(1.0 + ux * ux + uy * uy);
+  double T = S->T[ic], P = S->P[ic], E = S->E[ic];
+  double pitt = 0, pitx = 0, pity = 0, pitn = 0, pixx = 0, pixy = 0, pixn = 0, piyy = 0, piyn = 0, pinn = 0;
+  if (p->include_shear_deltaf) {
+    pixx = S->pixx[ic]; pixy = S->pixy[ic]; pixn = S->pixn[ic]; piyy = S->piyy[ic]; piyn = S->piyn[ic];
+    pinn = (pixx * (ux2 - ut2) + piyy * (uy2 - ut2) + 2.0 * (pixy * ux * uy + tau2 * un * (pixn * ux + piyn * uy))) / (tau2 * utperp * utperp);
+    pitn = (pixn * ux + piyn * uy + tau2 * pinn * un) / ut;
+    pity = (pixy * ux + piyy * uy + tau2 * piyn * un) / ut;
+    pitx = (pixx * ux + pixy * uy + tau2 * pixn * un) / ut;
+    pitt = (pitx * ux + pity * uy + tau2 * pitn * un) / ut;
+  }
+  double bulkPi = 0.0;
+  if (p->include_bulk_deltaf) bulkPi = S->bulkPi[ic];
+  double muB = 0, alphaB = 0, nB = 0, Vt = 0, Vx = 0, Vy = 0, Vn = 0, ber = 0;
+  if (p->include_baryon && p->include_baryondiff_deltaf) {
+    muB = S->muB[ic]; nB = S->nB[ic]; Vx = S->Vx[ic]; Vy = S->Vy[ic]; Vn = S->Vn[ic];
+    Vt = (Vx * ux + Vy * uy + tau2 * Vn * un) / ut;
+    alphaB = muB / T;
+    ber = nB / (E + P);
+  }
+  dfcoef df;
+  int rc = df_eval(df_data, T, muB, E, P, bulkPi, &df);
+  if (rc) { *err = rc; return; }
+  double c3 = df.c3, c4 = df.c4, betaV = df.betaV;
+  double shear_coeff = 0, bulk0 = 0, bulk1 = 0, bulk2 = 0;       /* :266-290 */
+  if (DF_MODE == 1) {
+    shear_coeff = 0.5 / (T * T * (E + P));
+    bulk0 = df.c0 - df.c2; bulk1 = df.c1; bulk2 = 4.0 * df.c2 - df.c0;
+  } else {
+    shear_coeff = 0.5 / (df.betapi * T);
+    bulk0 = df.F / (T * T * df.betabulk); bulk1 = df.G / df.betabulk; bulk2 = 1.0 / (3.0 * T * df.betabulk);
+  }
+  for (long ipart = 0; ipart < npart; ipart++) {
+    double mass = s->mass[ipart], mass2 = mass * mass, sign = s->sign[ipart];
+    double degeneracy = s->degen[ipart], baryon = s->baryon[ipart];
+    double chem = baryon * alphaB;
+    double dN_dy_cell = 0.0;
+    for (long ipT = 0; ipT < npT; ipT++) {                         /* :296-378 */
+      double pT = g->pT[ipT], mT = sqrt(mass2 + pT * pT), mT_over_tau = mT / tau;
+      double pT_weight = pTw[ipT];
+      for (long iphip = 0; iphip < nphi; iphip++) {
+        double px = pT * g->cosphi[iphip], py = pT * g->sinphi[iphip];
+        double phi_weight = phiw[iphip];
+        for (long iy = 0; iy < ny; iy++) {
+          double y = g->yv[iy];
+          double eta_integral = 0.0;
+          for (long ieta = 0; ieta < neta; ieta++) {
+            double eta = (p->dimension == 3) ? eta0 : g->etav[ieta];
+            double eta_weight = g->etaw[ieta];
+            double pt = mT * cosh(y - eta), pn = mT_over_tau * sinh(y - eta), tau2_pn = tau2 * pn;
+            double pdotdsigma = eta_weight * (pt * dat + px * dax + py * day + pn * dan);
+            if (p->outflow && pdotdsigma <= 0.0) continue;
+            double pdotu = pt * ut - px * ux - py * uy - tau2_pn * un;
+            double feq = 1.0 / (exp(pdotu / T - chem) + sign);
+            double feqbar = 1.0 - sign * feq;
+            double pimunu_pmu_pnu = pitt * pt * pt + pixx * px * px + piyy * py * py + pinn * tau2_pn * tau2_pn
+                + 2.0 * (-(pitx * px + pity * py) * pt + pixy * px * py + tau2_pn * (pixn * px + piyn * py - pitn * pt));
+            double Vmu_pmu = Vt * pt - Vx * px - Vy * py - Vn * tau2_pn;
+            double dfv;
+            if (DF_MODE == 1) {
+              double df_shear = shear_coeff * pimunu_pmu_pnu;
+              double df_bulk = (bulk0 * mass2 + (bulk1 * baryon + bulk2 * pdotu) * pdotu) * bulkPi;
+              double df_diff = (c3 * baryon + c4 * pdotu) * Vmu_pmu;
+              dfv = feqbar * (df_shear + df_bulk + df_diff);
+            } else {
+              double df_shear = shear_coeff * pimunu_pmu_pnu / pdotu;
+              double df_bulk = (bulk0 * pdotu + bulk1 * baryon + bulk2 * (pdotu - mass2 / pdotu)) * bulkPi;
+              double df_diff = (ber - baryon / pdotu) * Vmu_pmu / betaV;
+              dfv = feqbar * (df_shear + df_bulk + df_diff);
+            }
+            if (p->regulate_deltaf) dfv = fmax(-1.0, fmin(dfv, 1.0));
+            double f = feq * (1.0 + dfv);
+            eta_integral += (pdotdsigma * f);
+          }
+          dN_dy_cell += (pT_weight * phi_weight * prefactor * degeneracy * eta_integral);
+        }
+      }
+    }
+    cy[ipart * ncell + ic] = dN_dy_cell;
+    valid[ipart * ncell + ic] = 1;
+  }
+}
+
+static void dndx_cell_feqmod(const orc_params *p, const orc_setup *s, const orc_surface *S, const dfdata *df_data,
+                             const grid *g, const double *pTw, const double *phiw, long ic, long ncell,
+                             double *cy, char *valid, long *skipped, int *err) {
+  const double prefactor = pow(2.0 * M_PI * HBARC, -3);
+  const long npart = s->npart, npT = g->npT, nphi = g->nphi, ny = g->ny, neta = g->neta;
+  const int DF_MODE = p->df_mode, DIMENSION = p->dimension;
+  const double detA_min = p->deta_min;
+  const int pts = s->gla_points;
+  const double *r1 = s->gla_root + pts, *r2 = s->gla_root + 2 * pts;
+  const double *w1 = s->gla_weight + pts, *w2 = s->gla_weight + 2 * pts;
+  double A_copy[3][3], A_inv[3][3];
+  double tau = S->tau[ic], tau2 = tau * tau;
+  double eta0 = (DIMENSION == 3) ? S->eta[ic] : 0.0;
+  double dat = S->dat[ic], dax = S->dax[ic], day = S->day[ic], dan = S->dan[ic];
+  double ux = S->ux[ic], uy = S->uy[ic], un = S->un[ic];
+  double ut = sqrt(1.0 + ux * ux + uy * uy + tau2 * un * un);
+  double udsigma = ut * dat + ux * dax + uy * day + un * dan;
+  if (udsigma <= 0.0) return;                                      /* :695 */
+  double ux2 = ux * ux, uy2 = uy * uy, ut2 = ut * ut;
+  double uperp = sqrt(ux * ux + uy * uy), utperp = sqrt(1.0 + ux * ux + uy * uy);
+  double T = S->T[ic], P = S->P[ic], E = S->E[ic];
+  double pitt = 0, pitx = 0, pity = 0, pitn = 0, pixx = 0, pixy = 0, pixn = 0, piyy = 0, piyn = 0, pinn = 0;
+  if (p->include_shear_deltaf) {
+    pixx = S->pixx[ic]; pixy = S->pixy[ic]; pixn = S->pixn[ic]; piyy = S->piyy[ic]; piyn = S->piyn[ic];
+    pinn = (pixx * (ux2 - ut2) + piyy * (uy2 - ut2) + 2.0 * (pixy * ux * uy + tau2 * un * (pixn * ux + piyn * uy))) / (tau2 * utperp * utperp);
+    pitn = (pixn * ux + piyn * uy + tau2 * pinn * un) / ut;
+    pity = (pixy * ux + piyy * uy + tau2 * piyn * un) / ut;
+    pitx = (pixx * ux + pixy * uy + tau2 * pixn * un) / ut;
+    pitt = (pitx * ux + pity * uy + tau2 * pitn * un) / ut;
+  }
+  double bulkPi = 0.0;
+  if (p->include_bulk_deltaf) bulkPi = S->bulkPi[ic];
+  double muB = 0, alphaB = 0, nB = 0, Vt = 0, Vx = 0, Vy = 0, Vn = 0, ber = 0;
+  if (p->include_baryon && p->include_baryondiff_deltaf) {
+    muB = S->muB[ic]; nB = S->nB[ic]; Vx = S->Vx[ic]; Vy = S->Vy[ic]; Vn = S->Vn[ic];
+    Vt = (Vx * ux + Vy * uy + tau2 * Vn * un) / ut;
+    alphaB = muB / T;
+    ber = nB / (E + P);
+  }
+  if (DF_MODE == 4) {   /* :766-772 (note <= / >=, the spectra path uses < / >) */
+    double bulkPi_over_Peq_max = df_data->bulkPi_over_Peq_max;
+    if (bulkPi <= -P) bulkPi = -(1.0 - 1.e-5) * P;
+    else if (bulkPi / P >= bulkPi_over_Peq_max) bulkPi = P * (bulkPi_over_Peq_max - 1.e-5);
+  }
+  dfcoef df;
+  int rc = df_eval(df_data, T, muB, E, P, bulkPi, &df);
+  if (rc) { *err = rc; return; }
+  double F = df.F, G = df.G, betabulk = df.betabulk, betaV = df.betaV, betapi = df.betapi;
+  double lambda = df.lambda, z = df.z, delta_lambda = df.delta_lambda, delta_z = df.delta_z;
+  milne b = milne_basis(ut, ux, uy, un, uperp, utperp, tau);
+  pilrf pl_ = boost_pimunu(b, tau2, pitt, pitx, pity, pitn, pixx, pixy, pixn, piyy, piyn, pinn);
+  double T_mod = T, alphaB_mod = alphaB;
+  if (DF_MODE == 3) { T_mod = T + bulkPi * F / betabulk; alphaB_mod = alphaB + bulkPi * G / betabulk; }
+  double shear_coeff = 0.5 / (betapi * T);
+  double bulk0 = F / (T * T * betabulk), bulk1 = G / betabulk, bulk2 = 1.0 / (3.0 * T * betabulk);
+  double shear_mod = 0.5 / betapi, bulk_mod = bulkPi / (3.0 * betabulk);
+  if (DF_MODE == 4) bulk_mod = lambda;
+  double Axx = 1.0 + pl_.xx * shear_mod + bulk_mod, Axy = pl_.xy * shear_mod, Axz = pl_.xz * shear_mod;
+  double Ayy = 1.0 + pl_.yy * shear_mod + bulk_mod, Ayz = pl_.yz * shear_mod, Azz = 1.0 + pl_.zz * shear_mod + bulk_mod;
+  double detA = Axx * (Ayy * Azz - Ayz * Ayz) - Axy * (Axy * Azz - Ayz * Axz) + Axz * (Axy * Ayz - Ayy * Axz);
+  double detA_b23 = pow(1.0 + bulk_mod, 2);
+  int breaks = feqmod_breaks_down(p->mass_pion0, T, F, bulkPi, betabulk, detA, detA_min, z, s, DF_MODE);
+  double A[9] = {Axx, Axy, Axz, Axy, Ayy, Ayz, Axz, Ayz, Azz};
+  for (int i = 0; i < 3; i++) for (int j = 0; j < 3; j++) A_copy[i][j] = A[3 * i + j];
+  inverse3(A, A_inv);
+  double neq_fact = T * T * T / two_pi2_hbarC3();
+  double dn_fact = bulkPi / betabulk, J20_fact = T * neq_fact, N10_fact = neq_fact;
+  double nmod_fact = T_mod * T_mod * T_mod / two_pi2_hbarC3();
+  double eta_scale = 1.0;
+  if (detA > detA_min && DIMENSION == 2) eta_scale = detA / detA_b23;
+  for (long ipart = 0; ipart < npart; ipart++) {
+    double mass = s->mass[ipart], mass2 = mass * mass, sign = s->sign[ipart];
+    double degeneracy = s->degen[ipart], baryon = s->baryon[ipart];
+    double chem = baryon * alphaB, chem_mod = baryon * alphaB_mod;
+    double renorm = 1.0;                                            /* :932-970 */
+    if (p->include_bulk_deltaf) {
+      if (DF_MODE == 3) {
+        double mbar = mass / T, mbar_mod = mass / T_mod;
+        double neq = neq_fact * degeneracy * orc_gauss_thermal(GT_NEQ, r1, w1, pts, mbar, alphaB, baryon, sign);
+        double N10 = baryon * N10_fact * degeneracy * orc_gauss_thermal(GT_J10, r1, w1, pts, mbar, alphaB, baryon, sign);
+        double J20 = J20_fact * degeneracy * orc_gauss_thermal(GT_J20, r2, w2, pts, mbar, alphaB, baryon, sign);
+        double n_linear = neq + dn_fact * (neq + N10 * G + J20 * F / T / T);
+        double n_mod = nmod_fact * degeneracy * orc_gauss_thermal(GT_NEQ, r1, w1, pts, mbar_mod, alphaB_mod, baryon, sign);
+        renorm = n_linear / n_mod;
+      } else if (DF_MODE == 4) {
+        renorm = z;
+      }
+    }
+    if (DIMENSION == 2) renorm /= detA_b23; else renorm /= detA;
+    if (isnan(renorm) || isinf(renorm)) { (*skipped)++; continue; }   /* :972-976: cell not binned */
+    double dN_dy_cell = 0.0;
+    for (long ipT = 0; ipT < npT; ipT++) {
+      double pT = g->pT[ipT], mT = sqrt(mass2 + pT * pT), mT_over_tau = mT / tau;
+      double pT_weight = pTw[ipT];
+      for (long iphip = 0; iphip < nphi; iphip++) {
+        double px = pT * g->cosphi[iphip], py = pT * g->sinphi[iphip];
+        double phi_weight = phiw[iphip];
+        for (long iy = 0; iy < ny; iy++) {
+          double y = g->yv[iy];
+          double eta_integral = 0.0;
+          for (long ieta = 0; ieta < neta; ieta++) {
+            double eta = (DIMENSION == 3) ? eta0 : g->etav[ieta];
+            double eta_weight = g->etaw[ieta];
+            int narrow = 0;
+            if (DIMENSION == 3 && !breaks) { if (detA < 0.01 && fabs(y - eta) < detA) narrow = 1; }
+            double pdotdsigma, f;
+            if (breaks || narrow) {                                 /* :1015-1071 */
+              double pt = mT * cosh(y - eta), pn = mT_over_tau * sinh(y - eta), tau2_pn = tau2 * pn;
+              pdotdsigma = eta_weight * (pt * dat + px * dax + py * day + pn * dan);
+              if (p->outflow && pdotdsigma <= 0.0) continue;
+              double pdotu = pt * ut - px * ux - py * uy - tau2_pn * un;
+              double ppp = pitt * pt * pt + pixx * px * px + piyy * py * py + pinn * tau2_pn * tau2_pn
+                  + 2.0 * (-(pitx * px + pity * py) * pt + pixy * px * py + tau2_pn * (pixn * px + piyn * py - pitn * pt));
+              if (DF_MODE == 3) {
+                double feq = 1.0 / (exp(pdotu / T - chem) + sign);
+                double feqbar = 1.0 - sign * feq;
+                double Vp = Vt * pt - Vx * px - Vy * py - Vn * tau2_pn;
+                double df_shear = shear_coeff * ppp / pdotu;
+                double df_bulk = (bulk0 * pdotu + bulk1 * baryon + bulk2 * (pdotu - mass2 / pdotu)) * bulkPi;
+                double df_diff = (ber - baryon / pdotu) * Vp / betaV;
+                double dfv = feqbar * (df_shear + df_bulk + df_diff);
+                if (p->regulate_deltaf) dfv = fmax(-1.0, fmin(dfv, 1.0));
+                f = feq * (1.0 + dfv);
+              } else {
+                double feq = 1.0 / (exp(pdotu / T) + sign);
+                double feqbar = 1.0 - sign * feq;
+                double df_shear = feqbar * shear_coeff * ppp / pdotu;
+                double df_bulk = delta_z - 3.0 * delta_lambda + feqbar * delta_lambda * (pdotu - mass2 / pdotu) / T;
+                double dfv = df_shear + df_bulk;
+                if (p->regulate_deltaf) dfv = fmax(-1.0, fmin(dfv, 1.0));
+                f = feq * (1.0 + dfv);
+              }
+            } else {                                                /* :1073-1122 */
+              double pt = mT * cosh(y - eta_scale * eta), pn = mT_over_tau * sinh(y - eta_scale * eta), tau2_pn = tau2 * pn;
+              pdotdsigma = eta_weight * (pt * dat + px * dax + py * day + pn * dan);
+              if (p->outflow && pdotdsigma <= 0.0) continue;
+              double pLRF[3] = {-b.Xt * pt + b.Xx * px + b.Xy * py + b.Xn * tau2_pn, b.Yx * px + b.Yy * py, -b.Zt * pt + b.Zn * tau2_pn};
+              double pm[3], pmp[3], pp[3], dpv[3], dpm[3];
+              matvec3(A_inv, pLRF, pm);
+              for (int it = 0; it < 5; it++) {
+                for (int q = 0; q < 3; q++) pmp[q] = pm[q];
+                matvec3(A_copy, pmp, pp);
+                for (int q = 0; q < 3; q++) dpv[q] = pLRF[q] - pp[q];
+                double dp = sqrt(dpv[0] * dpv[0] + dpv[1] * dpv[1] + dpv[2] * dpv[2]);
+                if (dp <= 1.e-16) break;
+                matvec3(A_inv, dpv, dpm);
+                for (int q = 0; q < 3; q++) pm[q] = pmp[q] + dpm[q];
+              }
+              double E_mod = sqrt(mass2 + pm[0] * pm[0] + pm[1] * pm[1] + pm[2] * pm[2]);
+              f = fabs(renorm) / (exp(E_mod / T_mod - chem_mod) + sign);
+            }
+            eta_integral += (pdotdsigma * f);
+          }
+          dN_dy_cell += (pT_weight * phi_weight * prefactor * degeneracy * eta_integral);
+        }
+      }
+    }
+    cy[ipart * ncell + ic] = dN_dy_cell;
+    valid[ipart * ncell + ic] = 1;
+  }
+}
+
+/* The reference's per-species binning (:380-404 / :1136-1160) into thread slices all[i + n*bins],
+ * the per-species reset memset(all, 0, C*bins) -- a BYTE count, so only the first C*bins/8 doubles
+ * (and the low bytes of the next one) are cleared and the rest carries over from the previous
+ * species when carry != 0 -- and the per-bin sum over threads + bin-width normalisation written to
+ * the files (:407-440 / :1163-1194). */
+static void dndx_bin(const orc_surface *S, const orc_bins *B, long C, int carry, long npart, const double *cy,
+                     const char *valid, double *tau_out, double *r_out, double *phi_out) {
+  const double two_pi = 2.0 * M_PI;
+  const long taubins = B->tau_bins, rbins = B->r_bins, phibins = B->phip_bins;
+  const double TAU_WIDTH = (B->tau_max - B->tau_min) / (double)B->tau_bins;
+  const double R_WIDTH = (B->r_max - B->r_min) / (double)B->r_bins;
+  const double PHIP_WIDTH = two_pi / (double)B->phip_bins;
+  double *at = (double *)calloc((size_t)C * taubins, sizeof(double));
+  double *ar = (double *)calloc((size_t)C * rbins, sizeof(double));
+  double *ap = (double *)calloc((size_t)C * phibins, sizeof(double));
+  const long n_cells = S->n;
+  for (long ipart = 0; ipart < npart; ipart++) {
+    if (carry) {
+      memset(at, 0, (size_t)(C * taubins)); memset(ar, 0, (size_t)(C * rbins)); memset(ap, 0, (size_t)(C * phibins));
+    } else {
+      memset(at, 0, sizeof(double) * C * taubins); memset(ar, 0, sizeof(double) * C * rbins);
+      memset(ap, 0, sizeof(double) * C * phibins);
+    }
+    for (long n = 0; n < C; n++) {
+      CELL_LOOP_BEGIN(n, C, n_cells, ic)
+        if (!valid[ipart * n_cells + ic]) continue;
+        double dN_dy_cell = cy[ipart * n_cells + ic];
+        double x_pos = S->x[ic], y_pos = S->y[ic], tau = S->tau[ic];
+        double r = sqrt(x_pos * x_pos + y_pos * y_pos);
+        double phi = atan2(y_pos, x_pos);
+        if (phi < 0.0) phi += two_pi;
+        long itau = (int)floor((tau - B->tau_min) / TAU_WIDTH);
+        long ir = (int)floor((r - B->r_min) / R_WIDTH);
+        long iphi = (int)floor(phi / PHIP_WIDTH);
+        if (itau >= 0 && itau < taubins) at[itau + n * taubins] += dN_dy_cell;
+        if (ir >= 0 && ir < rbins) ar[ir + n * rbins] += dN_dy_cell;
+        if (iphi >= 0 && iphi < phibins) ap[iphi + n * phibins] += dN_dy_cell;
+      CELL_LOOP_END
+    }
+    for (long ir = 0; ir < rbins; ir++) {
+      double acc = 0.0;
+      for (long n = 0; n < C; n++) acc += ar[ir + n * rbins];
+      double r_mid = B->r_min + R_WIDTH * ((double)ir + 0.5);
+      r_out[ipart * rbins + ir] = acc / (two_pi * r_mid * R_WIDTH);
+    }
+    for (long itau = 0; itau < taubins; itau++) {
+      double acc = 0.0;
+      for (long n = 0; n < C; n++) acc += at[itau + n * taubins];
+      double tau_mid = B->tau_min + TAU_WIDTH * ((double)itau + 0.5);
+      tau_out[ipart * taubins + itau] = acc / (tau_mid * TAU_WIDTH);
+    }
+    for (long iphi = 0; iphi < phibins; iphi++) {
+      double acc = 0.0;
+      for (long n = 0; n < C; n++) acc += ap[iphi + n * phibins];
+      phi_out[ipart * phibins + iphi] = acc / PHIP_WIDTH;
+    }
+  }
+  free(at); free(ar); free(ap);
+}
+
+int orc_dndx(const orc_params *p, const orc_setup *s, const orc_surface *surf, const orc_bins *B,
+             double *cell_yield, double *tau_out, double *r_out, double *phi_out, long *stats, char *err, int errlen) {
+  if (p->dimension != 2 && p->dimension != 3) { seterr(err, errlen, "EmissionFunctionArray error: need to set dimension = (2,3)"); return 1; }
+  if (p->df_mode == 5) { seterr(err, errlen, "calculate_spectra error: no spacetime distribution routine for famod yet"); return 1; }
+  if (p->df_mode < 1 || p->df_mode > 5) { seterr(err, errlen, "calculate_spectra error: need to set df_mode = (1, 2, 3, 4, 5)"); return 1; }
+  if (B->tau_bins <= 0 || B->r_bins <= 0 || B->phip_bins <= 0) { seterr(err, errlen, "spacetime bins must be positive"); return 1; }
+  dfdata d;
+  if (df_setup(&d, p, s, 1)) { seterr(err, errlen, "gsl: x values must be strictly increasing (Jonah table)"); df_free(&d); return 1; }
+  grid g;
+  grid_setup(&g, p, s);
+  const long n_cells = surf->n, npart = s->npart;
+  const long C = p->threads > 0 ? p->threads : 1;
+  double *pTw = (double *)malloc(sizeof(double) * (g.npT + 1)), *phiw = (double *)malloc(sizeof(double) * (g.nphi + 1));
+  for (long i = 0; i < g.npT; i++) pTw[i] = s->pT_w ? s->pT_w[i] : 0.0;
+  for (long j = 0; j < g.nphi; j++) phiw[j] = s->phi_w ? s->phi_w[j] : 0.0;
+  double *cy = (double *)calloc((size_t)npart * (n_cells > 0 ? n_cells : 1), sizeof(double));
+  int *cerr = (int *)calloc((size_t)(n_cells > 0 ? n_cells : 1), sizeof(int));
+  long *cskip = (long *)calloc((size_t)(n_cells > 0 ? n_cells : 1), sizeof(long));
+  /* valid[ipart][cell]: the cell passed u.dsigma > 0 (and a finite renorm); skipped cells are never binned */
+  char *valid = (char *)calloc((size_t)npart * (n_cells > 0 ? n_cells : 1), 1);
+#ifdef _OPENMP
+  int nthr = p->omp_threads > 0 ? p->omp_threads : omp_get_max_threads();
+#pragma omp parallel for schedule(dynamic, 16) num_threads(nthr)
+#endif
+  for (long ic = 0; ic < n_cells; ic++) {
+    if (p->df_mode <= 2) dndx_cell_grad_ce(p, s, surf, &d, &g, pTw, phiw, ic, n_cells, cy, valid, &cerr[ic]);
+    else dndx_cell_feqmod(p, s, surf, &d, &g, pTw, phiw, ic, n_cells, cy, valid, &cskip[ic], &cerr[ic]);
+  }
+  int rc = 0;
+  long skipped = 0;
+  for (long ic = 0; ic < n_cells; ic++) { if (cerr[ic] && !rc) rc = cerr[ic]; skipped += cskip[ic]; }
+  if (rc) seterr(err, errlen, df_errmsg(rc));
+  else dndx_bin(surf, B, C, B->carry, npart, cy, valid, tau_out, r_out, phi_out);
+  if (cell_yield) memcpy(cell_yield, cy, sizeof(double) * npart * n_cells);
+  if (stats) { for (int i = 0; i < ORC_NSTATS; i++) stats[i] = 0; stats[4] = skipped; }
+  free(pTw); free(phiw); free(cy); free(cerr); free(cskip); free(valid);
+  grid_free(&g); df_free(&d);
+  return rc ? 1 : 0;
+}
+
+/* ------------------------------------------------------------------------- */
 /* drivers                                                                    */
 /* ------------------------------------------------------------------------- */
 int orc_spectra(const orc_params *p, const orc_setup *s, const orc_surface *surf,

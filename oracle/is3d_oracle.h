@@ -7,6 +7,7 @@
  * path never links or calls it.
  *
  * What it restates (reference = xyw2016/iS3D2 @ 2025-01-17, src/cpp/):
+ *   SpacetimeDistribution.cpp:31-1250 calculate_dN_dX(_feqmod)   (operation 0, df_mode 1-4)
  *   MomentumSpectra.cpp:32-415    calculate_dN_pTdpTdphidy        (df_mode 1 Grad, 2 RTA-CE)
  *   MomentumSpectra.cpp:419-1044  calculate_dN_pTdpTdphidy_feqmod (df_mode 3 PTM, 4 PTB)
  *   MomentumSpectra.cpp:1049-1682 calculate_dN_pTdpTdphidy_famod  (df_mode 5 PTMA)
@@ -66,7 +67,20 @@ typedef struct {
   const double *Tarr, *muBarr;
   const double *dftab;           /* [10][nmuB][nT]: c0 c1 c2 c3 c4 F G betabulk betaV betapi */
   double T_avg;                  /* Plasma::temperature (15-digit file round trip) */
+  const double *pT_w, *phi_w;    /* pT / phi quadrature weights (operation 0 only; may be NULL otherwise) */
 } orc_setup;
+
+/* operation = 0 spacetime bins (EmissionFunction.cpp:232-247, iS3D_parameters.dat tau_* r_* phip_bins) */
+typedef struct {
+  double tau_min, tau_max;
+  int tau_bins;
+  double r_min, r_max;
+  int r_bins;
+  int phip_bins;
+  int carry;                     /* 1 = the reference's byte-count memset (values carry over between
+                                    species in all but the first C*bins/8 thread-slice entries);
+                                    0 = every species binned from zero */
+} orc_bins;
 
 /* canonical surface field order (shared with include/is3d_amd.h) */
 typedef struct {
@@ -89,6 +103,15 @@ typedef struct {
  * would abort (GSL range error, bad df_mode, table out of range). */
 int orc_spectra(const orc_params *p, const orc_setup *s, const orc_surface *surf,
                 double *out, long *stats, char *err, int errlen);
+
+/* operation = 0: dN/dX (SpacetimeDistribution.cpp:31-1250).  Outputs are the values the
+ * reference writes to results/continuous/dN_taudtaudy_<MCID>.dat, dN_2pirdrdy_, dN_dphidy_
+ * ([species][bins], already divided by the bin measure); cell_yield (optional, [species][cell])
+ * is dN_dy_cell, 0 for skipped cells.  p->threads = the reference's CORES (cell striding and
+ * thread slices of the binning). */
+int orc_dndx(const orc_params *p, const orc_setup *s, const orc_surface *surf, const orc_bins *bins,
+             double *cell_yield, double *tau_out, double *r_out, double *phi_out, long *stats,
+             char *err, int errlen);
 
 /* --- pieces exposed for pinning tests --- */
 double orc_gauss_thermal(int kind, const double *root, const double *weight, int pts,

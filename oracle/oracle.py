@@ -30,7 +30,13 @@ class OrcSetup(C.Structure):
                 ("pT", PD), ("phi", PD), ("y", PD), ("eta", PD), ("eta_w", PD),
                 ("gla_alpha", C.c_int), ("gla_points", C.c_int), ("gla_root", PD), ("gla_weight", PD),
                 ("nT", C.c_int), ("nmuB", C.c_int), ("Tarr", PD), ("muBarr", PD), ("dftab", PD),
-                ("T_avg", C.c_double)]
+                ("T_avg", C.c_double), ("pT_w", PD), ("phi_w", PD)]
+
+
+class OrcBins(C.Structure):
+    _fields_ = [("tau_min", C.c_double), ("tau_max", C.c_double), ("tau_bins", C.c_int),
+                ("r_min", C.c_double), ("r_max", C.c_double), ("r_bins", C.c_int), ("phip_bins", C.c_int),
+                ("carry", C.c_int)]
 
 
 class OrcSurface(C.Structure):
@@ -52,6 +58,8 @@ def load():
         lib = C.CDLL(LIB)
         lib.orc_spectra.argtypes = [C.POINTER(OrcParams), C.POINTER(OrcSetup), C.POINTER(OrcSurface), PD,
                                     C.POINTER(C.c_long), C.c_char_p, C.c_int]
+        lib.orc_dndx.argtypes = [C.POINTER(OrcParams), C.POINTER(OrcSetup), C.POINTER(OrcSurface),
+                                 C.POINTER(OrcBins), PD, PD, PD, PD, C.POINTER(C.c_long), C.c_char_p, C.c_int]
         lib.orc_gauss_thermal.restype = C.c_double
         lib.orc_gauss_thermal.argtypes = [C.c_int, PD, PD, C.c_int, C.c_double, C.c_double, C.c_double, C.c_double]
         lib.orc_gauss1d_mod.restype = C.c_double
@@ -87,7 +95,8 @@ class _Inputs:
         self.keep = [_a(sp["mass"]), _a(sp["sign"]), _a(sp["degen"]), _a(sp["baryon"]),
                      _a(pdg["mass"]), _a(pdg["sign"]), _a(pdg["gspin"]), _a(pdg["baryon"]),
                      _a(spec["pT"]), _a(spec["phi"]), _a(spec["y"]), _a(spec["eta"]), _a(spec["eta_w"]),
-                     _a(spec["gla"][0]), _a(spec["gla"][1]), _a(spec["df"][0]), _a(spec["df"][1]), _a(spec["df"][2])]
+                     _a(spec["gla"][0]), _a(spec["gla"][1]), _a(spec["df"][0]), _a(spec["df"][1]), _a(spec["df"][2]),
+                     _a(spec.get("pT_w", np.zeros(len(spec["pT"])))), _a(spec.get("phi_w", np.zeros(len(spec["phi"]))))]
         k = self.keep
         self.surf = None
         if surf is not None:
@@ -103,7 +112,7 @@ class _Inputs:
                               _p(k[8]), _p(k[9]), _p(k[10]), _p(k[11]), _p(k[12]),
                               k[13].shape[0], k[13].shape[1], _p(k[13]), _p(k[14]),
                               len(k[15]), len(k[16]), _p(k[15]), _p(k[16]), _p(k[17]),
-                              float(T_avg) if T_avg is not None else 0.0)
+                              float(T_avg) if T_avg is not None else 0.0, _p(k[18]), _p(k[19]))
 
 
 def averages(surf, include_baryon=0):
@@ -150,3 +159,31 @@ def jonah_table(spec, T_avg):
     l2, z, bp, mx = np.zeros(301), np.zeros(301), np.zeros(301), np.zeros(1)
     rc = lib.orc_jonah_table(C.byref(inp.setup), _p(l2), _p(z), _p(bp), _p(mx))
     return rc, l2, z, bp, mx[0]
+
+
+def dndx(spec, surf, T_avg=None, threads=1, omp_threads=0, carry=None, return_cells=False):
+    """operation = 0 (SpacetimeDistribution.cpp): (dN_taudtaudy, dN_2pirdrdy, dN_dphidy), each
+    [species][bins] as written to results/continuous/, and optionally dN_dy_cell [species][cell].
+    `threads` = the reference's CORES; carry (default: threads > 1... see orc_bins) = reproduce the
+    byte-count memset carry between species."""
+    lib = load()
+    inp = _Inputs(spec, surf, T_avg, threads, omp_threads)
+    b = spec["bins"]
+    if carry is None:
+        carry = 1
+    bins = OrcBins(b["tau_min"], b["tau_max"], b["tau_bins"], b["r_min"], b["r_max"], b["r_bins"],
+                   b["phip_bins"], int(carry))
+    npart = len(spec["species"]["mass"])
+    n = len(surf["tau"])
+    t = np.zeros(npart * b["tau_bins"]); r = np.zeros(npart * b["r_bins"]); ph = np.zeros(npart * b["phip_bins"])
+    cy = np.zeros(max(1, npart * n))
+    stats = (C.c_long * 8)()
+    err = C.create_string_buffer(256)
+    rc = lib.orc_dndx(C.byref(inp.params), C.byref(inp.setup), C.byref(inp.surf), C.byref(bins), _p(cy),
+                      _p(t), _p(r), _p(ph), stats, err, 256)
+    if rc:
+        raise RuntimeError("oracle: " + err.value.decode())
+    out = (t.reshape(npart, -1), r.reshape(npart, -1), ph.reshape(npart, -1))
+    if return_cells:
+        return out + (cy[:npart * n].reshape(npart, n),)
+    return out

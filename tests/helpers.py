@@ -22,14 +22,19 @@ def emulator():
     return lib
 
 
-def emu_spectra(spec, surf, chains=1, T_avg=None):
+def emu_spectra(spec, surf, chains=1, T_avg=None, op=1):
+    """op = 1: spectra [species][pT][phi][y]; op = 0: dN_dy_cell [species][cell]."""
     lib = emulator()
     inp = O._Inputs(spec, surf, T_avg, 1)
     p = spec["params"]
     ny = len(spec["y"]) if p["dimension"] == 3 else 1
-    out = np.zeros(len(spec["species"]["mass"]) * len(spec["pT"]) * len(spec["phi"]) * ny)
+    if op == 0:
+        out = np.zeros(len(spec["species"]["mass"]) * len(surf["tau"]))
+    else:
+        out = np.zeros(len(spec["species"]["mass"]) * len(spec["pT"]) * len(spec["phi"]) * ny)
     st = (C.c_long * 4)()
-    rc = lib.emu_spectra(C.byref(inp.params), C.byref(inp.setup), C.byref(inp.surf), int(chains), O._p(out), st)
+    rc = lib.emu_spectra(C.byref(inp.params), C.byref(inp.setup), C.byref(inp.surf), int(chains), int(op),
+                         O._p(out), st)
     if rc:
         raise RuntimeError("emulator rc=%d" % rc)
     return out, list(st)

@@ -16,8 +16,10 @@
 
 using namespace is3d;
 
-extern "C" int emu_spectra(const orc_params* p, const orc_setup* su, const orc_surface* S, int chains, double* out,
-                           long* stats) {
+// op = 1: out = dN/(pT dpT dphi dy)[species][pT][phi][y];  op = 0: out = dN_dy_cell[species][cell]
+// (sum over pT, phi, y of w_pT w_phi (w_eta p.dsigma f) x prefactor g, as k_dndx)
+extern "C" int emu_spectra(const orc_params* p, const orc_setup* su, const orc_surface* S, int chains, int op,
+                           double* out, long* stats) {
   const int mode = p->df_mode, dim = p->dimension;
   const long n = S->n;
   const int np = su->npart, npT = su->npT, nphi = su->nphi;
@@ -51,6 +53,7 @@ extern "C" int emu_spectra(const orc_params* p, const orc_setup* su, const orc_s
   }
   tb.bulk_over_P_max = bpmax;
   PrepConsts k{};
+  k.operation = op;
   k.df_mode = mode; k.dim = dim; k.include_baryon = p->include_baryon; k.include_bulk = p->include_bulk_deltaf;
   k.include_shear = p->include_shear_deltaf; k.include_diff = p->include_baryondiff_deltaf;
   k.deta_min = p->deta_min; k.mass_pion0 = p->mass_pion0; k.gla_pts = su->gla_points;
@@ -124,8 +127,9 @@ extern "C" int emu_spectra(const orc_params* p, const orc_setup* su, const orc_s
         const double y = (dim == 3) ? su->y[kk] : 0.0;
         const double eta = (dim == 3) ? R[R_ETA] : su->eta[l];
         const double w = (dim == 3) ? 1.0 : su->eta_w[l];
-        yterms(mode, R, y, eta, w, &Yall[(size_t)q * NYT]);
+        yterms(mode, op, R, y, eta, w, &Yall[(size_t)q * NYT]);
       }
+      if (op == 0) std::fill(acc.begin(), acc.end(), 0.0);
       for (int s = 0; s < np; s++) {
         const double mass = su->mass[s], m2 = mass * mass, sign = su->sign[s], baryon = su->baryon[s];
         const double mT = sqrt(m2 + pT * pT);
@@ -171,11 +175,28 @@ extern "C" int emu_spectra(const orc_params* p, const orc_setup* su, const orc_s
           }
         }
       }
+      if (op == 0) {   // fold this cell's points with the pT / phi weights (k_dndx order: phi, then y, then pT)
+        for (int s = 0; s < np; s++) {
+          double cell = 0.0;
+          for (int kk = 0; kk < nk; kk++) {
+            double sj = 0.0;
+            for (int j = 0; j < nphi; j++) sj += su->phi_w[j] * acc[((size_t)s * nk + kk) * nphi + j];
+            cell += sj;
+          }
+          out[(size_t)s * n + c] += su->pT_w[i] * cell;
+        }
+      }
     }
+    if (op != 0) {
+      for (int s = 0; s < np; s++)
+        for (int kk = 0; kk < nk; kk++)
+          for (int j = 0; j < nphi; j++)
+            out[(((size_t)s * npT + i) * nphi + j) * ny_out + kk] = prefactor * su->degen[s] * acc[((size_t)s * nk + kk) * nphi + j];
+    }
+  }
+  if (op == 0) {
     for (int s = 0; s < np; s++)
-      for (int kk = 0; kk < nk; kk++)
-        for (int j = 0; j < nphi; j++)
-          out[(((size_t)s * npT + i) * nphi + j) * ny_out + kk] = prefactor * su->degen[s] * acc[((size_t)s * nk + kk) * nphi + j];
+      for (long c = 0; c < n; c++) out[(size_t)s * n + c] *= prefactor * su->degen[s];
   }
   if (stats) { stats[0] = st_break; stats[1] = st_pl; stats[2] = st_fail; stats[3] = st_it; }
   return 0;

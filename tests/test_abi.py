@@ -9,7 +9,7 @@ from is3d2_amd import _lib
 def declared_symbols():
     hdr = open("include/is3d_amd.h").read()
     hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
-    return sorted(set(re.findall(r"\b(is3d_[a-z_0-9]+)\s*\(", hdr)))
+    return sorted(set(re.findall(r"\b(is3d_[A-Za-z_0-9]+)\s*\(", hdr)))
 
 
 def test_header_and_binding_agree():
@@ -24,4 +24,4 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version():
     lib = _lib.load()
-    assert lib.is3d_abi_version() == 1
+    assert lib.is3d_abi_version() == 2

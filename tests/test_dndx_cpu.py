@@ -1,0 +1,100 @@
+"""CPU tier for operation = 0 (spacetime distributions dN/dX, SpacetimeDistribution.cpp):
+the engine's device math for the per-cell yields (emulator, k_dndx order) against the
+oracle restatement, and the oracle's own reference semantics (bin normalisation, the
+per-species byte-count memset carry, PTMA rejection)."""
+import numpy as np
+import pytest
+
+from helpers import emu_spectra, parity
+from is3d2_amd import make_spec, synth
+from oracle import oracle as O
+
+CASES = [(d, m) for d in (2, 3) for m in (1, 2, 3, 4)]
+
+
+@pytest.mark.parametrize("dim,mode", CASES)
+def test_cell_yield_math_matches_oracle(dim, mode):
+    s = synth.as_read(synth.surface(60, seed=13, dimension=dim, full3d=(dim == 3)))
+    spec = make_spec(hrg_eos=2, chosen="pikp", df_mode=mode, dimension=dim)
+    _, _, _, cy = O.dndx(spec, s, threads=1, return_cells=True)
+    got, _ = emu_spectra(spec, s, op=0)
+    assert parity(got, cy.ravel())[0] < 1e-12
+
+
+@pytest.mark.parametrize("mode", [1, 2, 3])
+def test_cell_yield_baryon_flags(mode):
+    s = synth.as_read(synth.surface(40, seed=5, dimension=3, baryon=True, full3d=True))
+    spec = make_spec(hrg_eos=2, chosen="pikp", df_mode=mode, dimension=3, include_baryon=1,
+                     include_baryondiff_deltaf=1, regulate_deltaf=1, outflow=1)
+    _, _, _, cy = O.dndx(spec, s, return_cells=True)
+    got, _ = emu_spectra(spec, s, op=0)
+    assert parity(got, cy.ravel())[0] < 1e-12
+
+
+def _bin_sums(spec, s, cy):
+    """Independent numpy binning of dN_dy_cell (reference bin formulas, no thread slices)."""
+    b = spec["bins"]
+    tw = (b["tau_max"] - b["tau_min"]) / b["tau_bins"]
+    rw = (b["r_max"] - b["r_min"]) / b["r_bins"]
+    pw = 2 * np.pi / b["phip_bins"]
+    r = np.sqrt(s["x"] ** 2 + s["y"] ** 2)
+    phi = np.arctan2(s["y"], s["x"])
+    phi = np.where(phi < 0, phi + 2 * np.pi, phi)
+    out = []
+    for key, nb, norm in ((np.floor((s["tau"] - b["tau_min"]) / tw), b["tau_bins"],
+                           (b["tau_min"] + tw * (np.arange(b["tau_bins"]) + 0.5)) * tw),
+                          (np.floor((r - b["r_min"]) / rw), b["r_bins"],
+                           2 * np.pi * (b["r_min"] + rw * (np.arange(b["r_bins"]) + 0.5)) * rw),
+                          (np.floor(phi / pw), b["phip_bins"], np.full(b["phip_bins"], pw))):
+        key = key.astype(np.int64)
+        m = (key >= 0) & (key < nb)
+        h = np.zeros((cy.shape[0], nb))
+        for i in range(cy.shape[0]):
+            h[i] = np.bincount(key[m], weights=cy[i][m], minlength=nb)
+        out.append(h / norm)
+    return out
+
+
+def test_binning_matches_numpy():
+    s = synth.as_read(synth.surface(300, seed=21))
+    spec = make_spec(hrg_eos=2, chosen="pikp", df_mode=2, dimension=2)
+    t, r, ph, cy = O.dndx(spec, s, threads=1, carry=0, return_cells=True)
+    for got, ref in zip((t, r, ph), _bin_sums(spec, s, cy)):
+        np.testing.assert_allclose(got, ref, rtol=1e-12, atol=0)
+
+
+@pytest.mark.parametrize("C", [1, 3, 8])
+def test_memset_carry_semantics(C):
+    # reference: memset(all, 0, C*bins) clears C*bins BYTES of a double array; thread-slice entries
+    # from index C*bins/8 on keep the previous species' sums (SpacetimeDistribution.cpp:165-167)
+    s = synth.as_read(synth.surface(300, seed=22))
+    spec = make_spec(hrg_eos=2, chosen="pikp", df_mode=1, dimension=2, tau_bins=120, r_bins=64, phip_bins=96)
+    fixed = O.dndx(spec, s, threads=C, carry=0)
+    carried = O.dndx(spec, s, threads=C, carry=1)
+    b = spec["bins"]
+    for d, nb in enumerate((b["tau_bins"], b["r_bins"], b["phip_bins"])):
+        np.testing.assert_array_equal(carried[d][0], fixed[d][0])     # first species: calloc'd
+        z = C * nb // 8                                               # doubles cleared per species
+        if C == 1:
+            for k in (1, 2):
+                prev = fixed[d][:k].sum(axis=0)
+                np.testing.assert_allclose(carried[d][k][:z], fixed[d][k][:z], rtol=1e-14)
+                np.testing.assert_allclose(carried[d][k][z:], fixed[d][k][z:] + prev[z:], rtol=1e-12)
+        else:
+            assert not np.allclose(carried[d][1:], fixed[d][1:], rtol=1e-9)
+
+
+def test_thread_count_invariance_without_carry():
+    s = synth.as_read(synth.surface(200, seed=23))
+    spec = make_spec(hrg_eos=2, chosen="pikp", df_mode=3, dimension=2)
+    a = O.dndx(spec, s, threads=1, carry=0)
+    b = O.dndx(spec, s, threads=7, carry=0)
+    for x, y in zip(a, b):
+        np.testing.assert_allclose(x, y, rtol=1e-12)
+
+
+def test_ptma_has_no_spacetime_routine():
+    s = synth.as_read(synth.surface(10, seed=1))
+    spec = make_spec(hrg_eos=2, chosen="pikp", df_mode=5)
+    with pytest.raises(RuntimeError, match="no spacetime distribution routine for famod"):
+        O.dndx(spec, s)

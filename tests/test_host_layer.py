@@ -102,3 +102,30 @@ def test_dropin_workflow_matches_oracle(tmp_path, fmt, dim, mode):
     vals = np.array([float(ln.split("\t")[3]) for ln in lines[1:] if ln])
     last = ref.reshape(3, npT, nphi, ny)[2]          # file order: y, phi, pT
     np.testing.assert_allclose(vals, np.transpose(last, (2, 1, 0)).ravel(), rtol=5e-9)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dim,mode,threads", [(2, 1, 0), (3, 3, 0), (2, 4, 4)])
+def test_dropin_spacetime_workflow_matches_oracle(tmp_path, dim, mode, threads):
+    # operation = 0: results/continuous/dN_taudtaudy_, dN_2pirdrdy_, dN_dphidy_<MCID>.dat (appended)
+    s = synth.surface(150, seed=41, dimension=dim, full3d=(dim == 3))
+    params = dict(operation=0, dimension=dim, df_mode=mode, include_baryon=0, include_bulk_deltaf=1,
+                  include_shear_deltaf=1, include_baryondiff_deltaf=0, regulate_deltaf=0, outflow=0, deta_min=1e-5,
+                  mass_pion0=0.138, tau_min=0.0, tau_max=12.0, tau_bins=60, r_min=0.0, r_max=15.0, r_bins=30,
+                  phip_bins=50, spacetime_threads=threads)
+    d = rundir.write_run_dir(str(tmp_path), s, params, hrg_eos=2, chosen="pikp", surface_format=1)
+    spec = make_spec(hrg_eos=2, chosen="pikp", pT="pT24", phi="phi24",
+                     **{k: v for k, v in params.items() if k != "operation"})
+    fields, avg = host.read_surface(d, 1, dim, 0)
+    surf = {k: fields[i] for i, k in enumerate(synth.FIELDS)}
+    t, r, ph = O.dndx(spec, surf, T_avg=avg[0], threads=max(threads, 1), carry=int(threads > 0))
+    ref = np.concatenate([t, r, ph], axis=1).ravel()
+    got = host.run_particlization(d, len(ref))
+    assert parity(got, ref)[0] < 1e-9
+    for k, mc in enumerate(spec["species"]["mcid"]):
+        rows = np.loadtxt(os.path.join(d, "results/continuous/dN_2pirdrdy_%d.dat" % mc))
+        assert rows.shape == (30, 2)
+        np.testing.assert_allclose(rows[:, 0], 0.25 + 0.5 * np.arange(30), rtol=1e-6)
+        np.testing.assert_allclose(rows[:, 1], r[k], rtol=1e-6, atol=1e-300)
+    host.run_particlization(d, len(ref))            # the reference opens the files in append mode
+    assert np.loadtxt(os.path.join(d, "results/continuous/dN_taudtaudy_%d.dat" % mc)).shape == (120, 2)
