@@ -36,6 +36,9 @@ CONFIGS = {
     "config3": dict(cells=100000, hrg=2, chosen="smash", pT="pT48", phi="phi32", dim=3, mode=2,
                     flags=dict(include_baryon=1, include_baryondiff_deltaf=1), scaling="weak"),
     "config4": dict(cells=1000000, hrg=2, chosen="smash", pT="pT48", phi="phi32", dim=3, mode=2, flags={}, scaling="strong"),
+    # HBM stress case: UrQMD HRG, PTMA + baryon, 64-pt Gauss-Laguerre tables for the thermal integrals
+    "config5": dict(cells=5000000, hrg=1, chosen="urqmd", pT="pT48", phi="phi32", dim=3, mode=5, gla=64,
+                    flags=dict(include_baryon=1, include_baryondiff_deltaf=1), scaling="strong"),
 }
 
 
@@ -117,7 +120,7 @@ def main():
     if mode == 4:
         flags.pop("include_baryon", None); flags.pop("include_baryondiff_deltaf", None)
     spec = make_spec(hrg_eos=cfg["hrg"], chosen=cfg["chosen"], pT=cfg["pT"], phi=cfg["phi"], y="y21", eta="eta24",
-                     dimension=cfg["dim"], df_mode=mode, **flags)
+                     dimension=cfg["dim"], df_mode=mode, gla_points=cfg.get("gla", 32), **flags)
     surf = make_surface(cfg, rank, world, cfg["dim"], bool(flags.get("include_baryon", 0)))
     n_local = len(surf["tau"])
     from is3d2_amd import dist as D
