@@ -33,8 +33,11 @@
 namespace is3d {
 
 // exp(x) for |x| <= 690 (the fast-path domain: no overflow, no subnormal result).
-// Cody-Waite reduction x = k ln2 + r, |r| <= ln2/2, degree-13 Taylor polynomial (truncation
-// < 5e-18 relative), 2^k by ldexp; max error measured ~1 ulp against glibc (test_kernel_math_cpu).
+// Reduction x = k ln2 + r with k = rint(x log2 e) taken from the low word of x log2 e + 1.5 2^52
+// (one FMA gives both k as a double and k as an int, no conversion), Cody-Waite r in two FMAs,
+// e^r = 1 + r + r^2 g(r) with g a degree-9 near-minimax (Chebyshev) fit on |r| <= ln2/2
+// (tools/fit_exp.py; 1.5e-16 relative measured in double Horner), 2^k by ldexp: 16 VALU ops,
+// max error ~1 ulp against glibc (test_kernel_math_cpu).
 // On the device each coefficient passes through an empty asm that pins it to an SGPR pair at
 // the point of use: otherwise the compiler hoists all of them out of the cell loop into VGPRs
 // and spills them to scratch (one serialized reload per coefficient per lane setup).
@@ -45,36 +48,39 @@ IS3D_HD double kconst(double v) {
   return v;
 }
 
-struct ExpCoef { double l2e, ln2hi, ln2lo, c[11]; };   // c: 1/13! ... 1/3!
+struct ExpCoef { double l2e, shift, ln2hi, ln2lo, c[10]; };   // c: g(r) coefficients, r^9 first
 
 IS3D_HD ExpCoef exp_coef() {
   ExpCoef e;
   e.l2e = kconst(1.4426950408889634);
+  e.shift = kconst(6755399441055744.0);                  // 1.5 * 2^52
   e.ln2hi = kconst(6.93147180369123816490e-01);    // low 32 bits zero
   e.ln2lo = kconst(1.90821492927058770002e-10);
-  const double f[11] = {1.0 / 6227020800.0, 1.0 / 479001600.0, 1.0 / 39916800.0, 1.0 / 3628800.0, 1.0 / 362880.0,
-                        1.0 / 40320.0, 1.0 / 5040.0, 1.0 / 720.0, 1.0 / 120.0, 1.0 / 24.0, 1.0 / 6.0};
-  for (int i = 0; i < 11; i++) e.c[i] = kconst(f[i]);
+  const double f[10] = {2.510038549551032e-08, 2.7620088445409746e-07, 2.7557268459997064e-06,
+                        2.4801521295954376e-05, 0.00019841269863053618, 0.0013888888917213717,
+                        0.008333333333330062, 0.04166666666662413, 0.16666666666666669, 0.5000000000000001};
+  for (int i = 0; i < 10; i++) e.c[i] = kconst(f[i]);
   return e;
 }
 
+// valid for |x| < 2^30 (k must fit the low word); exp_clamped handles everything else
 IS3D_HD double exp_poly(const ExpCoef& E, double x) {
-  const double k = rint(x * E.l2e);
+  const double t = fma(x, E.l2e, E.shift);
+  const double k = t - E.shift;
   double r = fma(-k, E.ln2hi, x);
   r = fma(-k, E.ln2lo, r);
   double p = E.c[0];
-  for (int i = 1; i < 11; i++) p = fma(p, r, E.c[i]);
-  p = fma(p, r, 0.5);
+  for (int i = 1; i < 10; i++) p = fma(p, r, E.c[i]);
   p = fma(p, r, 1.0);
   p = fma(p, r, 1.0);
-  return ldexp(p, (int)k);
+  return ldexp(p, (int)(unsigned)__builtin_bit_cast(unsigned long long, t));
 }
 
 IS3D_HD double exp_dom690(double x) { return exp_poly(exp_coef(), x); }
 
-// exp(x) for any x: clamped into [-746, 710] so that k fits an int; ldexp saturates to +inf
-// above 709.78 (the reference's exp overflow, after which 1/(inf + sign) = 0) and rounds to
-// subnormal / zero below -708.4
+// exp(x) for any x: clamped into [-746, 710] first; ldexp saturates to +inf above 709.78 (the
+// reference's exp overflow, after which 1/(inf + sign) = 0) and rounds to subnormal / zero below
+// -708.4
 IS3D_HD double exp_clamped(const ExpCoef& E, double x) { return exp_poly(E, fmin(fmax(x, -746.0), 710.0)); }
 
 // 16-byte pair for ds_read_b128 of the phi-term rows (96-byte, 16-byte aligned)
@@ -910,50 +916,72 @@ IS3D_HD double sqrt_nr(double v) {
 }
 
 // Modified (PTM/PTB/PTMA) lane: p_mod = mT (ch Uc + sh Us) + (pc Vc + ps Vs)  (MomentumSpectra.cpp:932-982
-// without the iterative refinement, which only changes rounding: A is linear).
+// without the iterative refinement, which only changes rounding: A is linear).  Writing
+// p_mod = mT U + W with U = ch Uc + sh Us per (cell, y) and W = pc Vc + ps Vs per (cell, phi),
+//   E_mod^2 = m^2 + mT^2 |U|^2 + 2 mT (U.Vc) pc + 2 mT (U.Vs) ps + |W|^2
+// so a point needs the lane's linear form E0 + Ec pc + Es ps plus Qv = |W|^2 from the per-(cell, phi)
+// LDS table (modqv) instead of rebuilding the 3-vector (E_mod^2 >= m^2 >= 0.019 GeV^2 for every
+// hadron, so the expanded form loses nothing measurable to cancellation).
 // f = |renorm| / (exp(E_mod/T_mod - chem) + sign) is evaluated as |renorm| en / (1 + sign en) with
 // en = exp(chem - E_mod/T_mod): u.p > 0 bounds en by e^chem and, for bosons (no baryon number),
 // below 1, so 1 + sign en lies in ~[1e-3, 2] and two points can share one reciprocal; en -> 0
 // where the reference's exp overflows to 1/inf = 0.  |renorm| is folded into p.dsigma.
 struct ModLane {
-  double mUx, mUy, mUz, D0, Dc, Ds, Vcx, Vsx, Vcy, Vsy, Vcz, Vsz, m2, invTm, chemm, sign;
+  double E0, Ec, Es, D0, Dc, Ds, invTm, chemm, sign;
   ExpCoef ec;    // pinned once per lane setup, reused by every phi point
-  int skip;
+  int skip, clamp;   // clamp: some point's exp argument may leave exp_poly's domain
 };
+
+// Qv = |pc Vc + ps Vs|^2 for one (cell, phi)
+IS3D_HD double modqv(const double* R, dbl2 cs) {
+  const double wx = fma(cs.x, R[R_VCX], cs.y * R[R_VSX]);
+  const double wy = fma(cs.x, R[R_VCY], cs.y * R[R_VSY]);
+  const double wz = fma(cs.x, R[R_VCZ], cs.y * R[R_VSZ]);
+  return fma(wx, wx, fma(wy, wy, wz * wz));
+}
 
 IS3D_HD void mod_setup(const double* R, const double* Y, double mT, double m2, double pT, double sign, double baryon,
                        double renorm_abs, ModLane& L) {
-  L.mUx = mT * Y[Y_MUX]; L.mUy = mT * Y[Y_MUY]; L.mUz = mT * Y[Y_MUZ];
+  const double ux = Y[Y_MUX], uy = Y[Y_MUY], uz = Y[Y_MUZ];
+  const double u2 = fma(ux, ux, fma(uy, uy, uz * uz));
+  L.E0 = fma(mT * mT, u2, m2);
+  const double tm = 2.0 * mT;
+  L.Ec = tm * fma(ux, R[R_VCX], fma(uy, R[R_VCY], uz * R[R_VCZ]));
+  L.Es = tm * fma(ux, R[R_VSX], fma(uy, R[R_VSY], uz * R[R_VSZ]));
   L.D0 = renorm_abs * (mT * Y[Y_MD]); L.Dc = renorm_abs * Y[Y_WDX]; L.Ds = renorm_abs * Y[Y_WDY];
-  L.Vcx = R[R_VCX]; L.Vsx = R[R_VSX]; L.Vcy = R[R_VCY]; L.Vsy = R[R_VSY]; L.Vcz = R[R_VCZ]; L.Vsz = R[R_VSZ];
-  L.m2 = m2; L.sign = sign;
+  L.sign = sign;
   L.invTm = R[R_INVTM]; L.chemm = baryon * R[R_CHEMM];
   L.ec = exp_coef();
-  // E_mod >= | |mT U| - pT |V|max |; if even that overflows exp, every phi point is exactly 0
-  const double mu = sqrt(L.mUx * L.mUx + L.mUy * L.mUy + L.mUz * L.mUz);
-  const double lo = mu - pT * R[R_VB];
+  // | |mT U| - pT |V|max | <= |p_mod| <= |mT U| + pT |V|max: if even the smallest E_mod overflows
+  // exp, every phi point is exactly 0; if the largest could push the exp argument out of
+  // exp_poly's domain the lane takes the clamped exp
+  const double mu = mT * sqrt(u2);
+  const double lo = mu - pT * R[R_VB], hi = mu + pT * R[R_VB];
   const double emin = (lo > 0.0) ? sqrt(m2 + lo * lo) * (1.0 - 1e-12) : 0.0;
   L.skip = (emin * L.invTm - L.chemm > kExpMax + 1.0) ? 1 : 0;
+  const double xlo = L.chemm - sqrt(m2 + hi * hi) * L.invTm;
+  L.clamp = (xlo > -1.0e6 && L.chemm < 700.0) ? 0 : 1;
 }
 
-// en = exp(chem - E_mod / T_mod) at one phi point
-IS3D_HD double mod_en(const ModLane& L, dbl2 cs) {
-  const double qx = lin(L.mUx, L.Vcx, L.Vsx, cs), qy = lin(L.mUy, L.Vcy, L.Vsy, cs), qz = lin(L.mUz, L.Vcz, L.Vsz, cs);
-  const double Emod = sqrt_nr(fma(qx, qx, fma(qy, qy, fma(qz, qz, L.m2))));
-  return exp_clamped(L.ec, fma(-Emod, L.invTm, L.chemm));
+// en = exp(chem - E_mod / T_mod) at one phi point (qv = modqv of the cell at this phi)
+template <bool CLAMP>
+IS3D_HD double mod_en(const ModLane& L, dbl2 cs, double qv) {
+  const double Emod = sqrt_nr(fma(L.Ec, cs.x, fma(L.Es, cs.y, L.E0 + qv)));
+  const double x = fma(-Emod, L.invTm, L.chemm);
+  return CLAMP ? exp_clamped(L.ec, x) : exp_poly(L.ec, x);
 }
 
-template <bool OUT>
-IS3D_HD double mod_point_t(const ModLane& L, dbl2 cs) {
-  const double en = mod_en(L, cs);
+template <bool OUT, bool CLAMP>
+IS3D_HD double mod_point_t(const ModLane& L, dbl2 cs, double qv) {
+  const double en = mod_en<CLAMP>(L, cs, qv);
   const double pds = lin(L.D0, L.Dc, L.Ds, cs);
   const double r = pds * (en * rcp1(fma(L.sign, en, 1.0)));
   return (OUT && pds <= 0.0) ? 0.0 : r;
 }
 
-template <bool OUT>
-IS3D_HD void mod_pair_t(const ModLane& L, dbl2 c0, dbl2 c1, double& v0, double& v1) {
-  const double en0 = mod_en(L, c0), en1 = mod_en(L, c1);
+template <bool OUT, bool CLAMP>
+IS3D_HD void mod_pair_t(const ModLane& L, dbl2 c0, dbl2 c1, dbl2 qv, double& v0, double& v1) {
+  const double en0 = mod_en<CLAMP>(L, c0, qv.x), en1 = mod_en<CLAMP>(L, c1, qv.y);
   const double q0 = fma(L.sign, en0, 1.0), q1 = fma(L.sign, en1, 1.0);
   const double r = rcp1(q0 * q1);
   const double pds0 = lin(L.D0, L.Dc, L.Ds, c0), pds1 = lin(L.D0, L.Dc, L.Ds, c1);
@@ -962,13 +990,19 @@ IS3D_HD void mod_pair_t(const ModLane& L, dbl2 c0, dbl2 c1, double& v0, double& 
   v1 = (OUT && pds1 <= 0.0) ? 0.0 : g1;
 }
 
-IS3D_HD double mod_point(const ModLane& L, dbl2 cs, int outflow) {
-  return outflow ? mod_point_t<true>(L, cs) : mod_point_t<false>(L, cs);
+IS3D_HD double mod_point(const ModLane& L, dbl2 cs, double qv, int outflow) {
+  if (L.clamp) return outflow ? mod_point_t<true, true>(L, cs, qv) : mod_point_t<false, true>(L, cs, qv);
+  return outflow ? mod_point_t<true, false>(L, cs, qv) : mod_point_t<false, false>(L, cs, qv);
 }
 
-IS3D_HD void mod_pair(const ModLane& L, dbl2 c0, dbl2 c1, int outflow, double& v0, double& v1) {
-  if (outflow) mod_pair_t<true>(L, c0, c1, v0, v1);
-  else mod_pair_t<false>(L, c0, c1, v0, v1);
+IS3D_HD void mod_pair(const ModLane& L, dbl2 c0, dbl2 c1, dbl2 qv, int outflow, double& v0, double& v1) {
+  if (L.clamp) {
+    if (outflow) mod_pair_t<true, true>(L, c0, c1, qv, v0, v1);
+    else mod_pair_t<false, true>(L, c0, c1, qv, v0, v1);
+  } else {
+    if (outflow) mod_pair_t<true, false>(L, c0, c1, qv, v0, v1);
+    else mod_pair_t<false, false>(L, c0, c1, qv, v0, v1);
+  }
 }
 
 }  // namespace is3d

@@ -231,18 +231,18 @@ __device__ __forceinline__ void sep_phi_loop(const SepLane& L, const dbl2* CS, c
   }
 }
 
-template <int FLAGS>
-__device__ __forceinline__ void mod_phi_loop(const ModLane& M, const dbl2* CS, double* acc) {
+template <int FLAGS, bool CLAMP>
+__device__ __forceinline__ void mod_phi_loop(const ModLane& M, const dbl2* CS, const dbl2* QV, double* acc) {
   constexpr bool OUT = (FLAGS & F_OUT) != 0;
-  dbl2 c0 = CS[0], c1 = CS[1];
+  dbl2 c0 = CS[0], c1 = CS[1], q = QV[0];
 #pragma unroll
   for (int jj = 0; jj < kJmax; jj += 2) {
-    dbl2 n0 = c0, n1 = c1;
-    if (jj + 2 < kJmax) { n0 = CS[jj + 2]; n1 = CS[jj + 3]; }
+    dbl2 n0 = c0, n1 = c1, nq = q;
+    if (jj + 2 < kJmax) { n0 = CS[jj + 2]; n1 = CS[jj + 3]; nq = QV[(jj >> 1) + 1]; }
     double v0, v1;
-    mod_pair_t<OUT>(M, c0, c1, v0, v1);
+    mod_pair_t<OUT, CLAMP>(M, c0, c1, q, v0, v1);
     acc[jj] += v0; acc[jj + 1] += v1;
-    c0 = n0; c1 = n1;
+    c0 = n0; c1 = n1; q = nq;
   }
 }
 
@@ -284,7 +284,8 @@ __global__ __launch_bounds__(kBlock, MODE >= PTM ? IS3D_SPECTRA_WAVES_MOD : IS3D
   dbl2* s_trig = (dbl2*)(s_recb + 2 * kTile * NREC);      // [nphp]        {cos, sin}
   dbl2* s_cs = s_trig + nphp;                             // [nphp]        {pT cos, pT sin}
   dbl2* s_bp = s_cs + nphp;                               // [kTile][nphp] {b', Phi}
-  double* s_grid = (double*)(s_bp + kTile * nphp);        // y[nk] | eta[nl] | eta_w[nl]
+  double* s_qv = (double*)(s_bp + kTile * nphp);         // [kTile][nphp]  Qv (modified path)
+  double* s_grid = s_qv + kTile * nphp;                   // y[nk] | eta[nl] | eta_w[nl]
   double* s_y = s_grid + A.nk + 2 * A.nl;                 // [kTile][nq][NYT]
 
   const int tid = threadIdx.x;
@@ -347,11 +348,14 @@ __global__ __launch_bounds__(kBlock, MODE >= PTM ? IS3D_SPECTRA_WAVES_MOD : IS3D
       const int t = idx / nphp, j = idx % nphp;
       const double* R = s_rec + t * NREC;
       dbl2 v; v.x = 0.0; v.y = 0.0;                        // padding: finite, never written out
+      double qv = 0.0;
       if (j < A.nphi && R[R_KIND] != 0.0) {
         const dbl2 tr = s_trig[j];
         v = phiterms(MODE, R, pT, tr.x, tr.y);
+        if (MODE >= PTM && R[R_KIND] == 2.0) qv = modqv(R, s_cs[j]);
       }
       s_bp[t * nphp + j] = v;
+      if (MODE >= PTM) s_qv[t * nphp + j] = qv;
     }
     for (int idx = tid; idx < nt * A.nq; idx += kBlock) {
       const int t = idx / A.nq, q = idx % A.nq;
@@ -391,7 +395,9 @@ __global__ __launch_bounds__(kBlock, MODE >= PTM ? IS3D_SPECTRA_WAVES_MOD : IS3D
             ModLane M;
             mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, M);
             if (M.skip) continue;
-            mod_phi_loop<FLAGS>(M, s_cs + j0, acc);
+            const dbl2* QV = (const dbl2*)(s_qv + t * nphp + j0);
+            if (M.clamp) mod_phi_loop<FLAGS, true>(M, s_cs + j0, QV, acc);
+            else mod_phi_loop<FLAGS, false>(M, s_cs + j0, QV, acc);
           }
         }
       }
@@ -467,20 +473,20 @@ __device__ __forceinline__ double sep_phi_wsum(const SepLane& L, const dbl2* CS,
   return a0 + a1;
 }
 
-template <int FLAGS>
-__device__ __forceinline__ double mod_phi_wsum(const ModLane& M, const dbl2* CS, const dbl2* W) {
+template <int FLAGS, bool CLAMP>
+__device__ __forceinline__ double mod_phi_wsum(const ModLane& M, const dbl2* CS, const dbl2* QV, const dbl2* W) {
   constexpr bool OUT = (FLAGS & F_OUT) != 0;
   double a0 = 0.0, a1 = 0.0;
-  dbl2 c0 = CS[0], c1 = CS[1];
+  dbl2 c0 = CS[0], c1 = CS[1], q = QV[0];
 #pragma unroll
   for (int jj = 0; jj < kJmax; jj += 2) {
-    dbl2 n0 = c0, n1 = c1;
-    if (jj + 2 < kJmax) { n0 = CS[jj + 2]; n1 = CS[jj + 3]; }
+    dbl2 n0 = c0, n1 = c1, nq = q;
+    if (jj + 2 < kJmax) { n0 = CS[jj + 2]; n1 = CS[jj + 3]; nq = QV[(jj >> 1) + 1]; }
     const dbl2 w = W[jj >> 1];
     double v0, v1;
-    mod_pair_t<OUT>(M, c0, c1, v0, v1);
+    mod_pair_t<OUT, CLAMP>(M, c0, c1, q, v0, v1);
     a0 = fma(w.x, v0, a0); a1 = fma(w.y, v1, a1);
-    c0 = n0; c1 = n1;
+    c0 = n0; c1 = n1; q = nq;
   }
   return a0 + a1;
 }
@@ -513,7 +519,8 @@ __global__ __launch_bounds__(kBlock, MODE >= PTM ? IS3D_SPECTRA_WAVES_MOD : IS3D
   dbl2* s_cs = s_trig + nphp;                             // [nphp] {pT cos, pT sin} of the current pT
   double* s_w = (double*)(s_cs + nphp);                   // [nphp] phi weights (0 in the padding)
   dbl2* s_bp = (dbl2*)(s_w + nphp);                       // [kTile][nphp] {b', Phi} of the current pT
-  double* s_red = (double*)(s_bp + kTile * nphp);         // [kTile][kBlock] per-lane cell sums
+  double* s_qv = (double*)(s_bp + kTile * nphp);         // [kTile][nphp] Qv of the current pT (modified path)
+  double* s_red = s_qv + kTile * nphp;                    // [kTile][kBlock] per-lane cell sums
   double* s_grid = s_red + kTile * kBlock;                // y[nk] | eta[nl] | eta_w[nl]
   double* s_y = s_grid + A.nk + 2 * A.nl;                 // [kTile][nq][NYT]
 
@@ -574,11 +581,17 @@ __global__ __launch_bounds__(kBlock, MODE >= PTM ? IS3D_SPECTRA_WAVES_MOD : IS3D
         const int t = idx / nphp, j = idx % nphp;
         const double* R = s_rec + t * NREC;
         dbl2 v; v.x = 0.0; v.y = 0.0;
+        double qv = 0.0;
         if (j < A.nphi && R[R_KIND] != 0.0) {
           const dbl2 tr = s_trig[j];
           v = phiterms(MODE, R, pT, tr.x, tr.y);
+          if (MODE >= PTM && R[R_KIND] == 2.0) {
+            dbl2 c; c.x = pT * tr.x; c.y = pT * tr.y;
+            qv = modqv(R, c);
+          }
         }
         s_bp[t * nphp + j] = v;
+        if (MODE >= PTM) s_qv[t * nphp + j] = qv;
       }
       __syncthreads();
       if (!active) continue;
@@ -610,7 +623,8 @@ __global__ __launch_bounds__(kBlock, MODE >= PTM ? IS3D_SPECTRA_WAVES_MOD : IS3D
             ModLane M;
             mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, M);
             if (M.skip) continue;
-            cell += mod_phi_wsum<FLAGS>(M, s_cs + j0, W);
+            const dbl2* QV = (const dbl2*)(s_qv + t * nphp + j0);
+            cell += M.clamp ? mod_phi_wsum<FLAGS, true>(M, s_cs + j0, QV, W) : mod_phi_wsum<FLAGS, false>(M, s_cs + j0, QV, W);
           }
         }
         s_red[t * kBlock + tid] = fma(wpT, cell, s_red[t * kBlock + tid]);
@@ -1154,7 +1168,8 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   sa.npart = np; sa.npT = npT; sa.nphi = nphi; sa.ny_out = ny_out; sa.nk = nk; sa.nl = nl; sa.nq = nk * nl; sa.njb = njb;
   sa.ntask = ntask; sa.cells_per_split = cps; sa.nbx = (int)bx; sa.nsplit = (int)nsplit; sa.sstride = sstride;
   sa.regulate = e->p.regulate_deltaf; sa.outflow = e->p.outflow; sa.dim = dim; sa.op = 1;
-  const size_t shmem = sizeof(double) * (2 * (size_t)kTile * NREC + 2 * (size_t)(kTile + 2) * njb * kJmax + (size_t)(nk + 2 * nl) +
+  const size_t shmem = sizeof(double) * (2 * (size_t)kTile * NREC + 2 * (size_t)(kTile + 2) * njb * kJmax +
+                                         (size_t)kTile * njb * kJmax + (size_t)(nk + 2 * nl) +
                                          (size_t)kTile * sa.nq * NYT);
   if (shmem > 160 * 1024) return e->fail(IS3D_ERR_ARG, "momentum grid too large for the LDS tile");
   const dim3 grid((unsigned)(bx * npT * nsplit));
@@ -1302,7 +1317,7 @@ extern "C" int is3d_calculate_dN_dX(is3d_engine* e, double* dN_taudtaudy, double
     da.yv = e->d_y; da.etav = e->d_eta; da.etaw = e->d_etaw;
     da.npart = np; da.npT = npT; da.nphi = nphi; da.nk = nk; da.nl = nl; da.nq = nk * nl; da.njb = njb; da.dim = dim;
     const size_t nphp = (size_t)njb * kJmax;
-    const size_t shmem = sizeof(double) * ((size_t)kTile * NREC + 2 * nphp + 2 * nphp + nphp + 2 * (size_t)kTile * nphp +
+    const size_t shmem = sizeof(double) * ((size_t)kTile * NREC + 2 * nphp + 2 * nphp + nphp + 3 * (size_t)kTile * nphp +
                                            (size_t)kTile * kBlock + (size_t)(nk + 2 * nl) + (size_t)kTile * da.nq * NYT);
     if (shmem > 160 * 1024) return e->fail(IS3D_ERR_ARG, "momentum grid too large for the LDS tile");
     const long nwg = (long)da.nbx * da.nchunk;

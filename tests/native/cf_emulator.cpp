@@ -110,6 +110,7 @@ extern "C" int emu_spectra(const orc_params* p, const orc_setup* su, const orc_s
   const int nq = nk * nl;
   std::vector<double> Yall((size_t)nq * NYT);
   std::vector<dbl2> CS(nphi), BP(nphi);
+  std::vector<double> QV(nphi + 1);
   std::vector<double> acc((size_t)np * nk * nphi);
   for (int i = 0; i < npT; i++) {
     const double pT = su->pT[i];
@@ -121,6 +122,7 @@ extern "C" int emu_spectra(const orc_params* p, const orc_setup* su, const orc_s
       for (int j = 0; j < nphi; j++) {
         CS[j].x = pT * cph[j]; CS[j].y = pT * sph[j];
         BP[j] = phiterms(mode, R, pT, cph[j], sph[j]);
+        QV[j] = (mode >= PTM && kind == 2.0) ? modqv(R, CS[j]) : 0.0;
       }
       for (int q = 0; q < nq; q++) {
         const int kk = q / nl, l = q % nl;
@@ -167,10 +169,11 @@ extern "C" int emu_spectra(const orc_params* p, const orc_setup* su, const orc_s
               int j = 0;
               for (; j + 1 < nphi; j += 2) {
                 double v0, v1;
-                mod_pair(M, CS[j], CS[j + 1], p->outflow, v0, v1);
+                dbl2 q; q.x = QV[j]; q.y = QV[j + 1];
+                mod_pair(M, CS[j], CS[j + 1], q, p->outflow, v0, v1);
                 a[j] += v0; a[j + 1] += v1;
               }
-              for (; j < nphi; j++) a[j] += mod_point(M, CS[j], p->outflow);
+              for (; j < nphi; j++) a[j] += mod_point(M, CS[j], QV[j], p->outflow);
             }
           }
         }
