@@ -48,7 +48,7 @@ IS3D_HD double kconst(double v) {
   return v;
 }
 
-struct ExpCoef { double l2e, shift, ln2hi, ln2lo, c[10]; };   // c: g(r) coefficients, r^9 first
+struct ExpCoef { double l2e, shift, ln2hi, ln2lo, ln2, c[10]; };   // c: g(r) coefficients, r^9 first
 
 IS3D_HD ExpCoef exp_coef() {
   ExpCoef e;
@@ -56,6 +56,7 @@ IS3D_HD ExpCoef exp_coef() {
   e.shift = kconst(6755399441055744.0);                  // 1.5 * 2^52
   e.ln2hi = kconst(6.93147180369123816490e-01);    // low 32 bits zero
   e.ln2lo = kconst(1.90821492927058770002e-10);
+  e.ln2 = kconst(6.93147180559945286227e-01);
   const double f[10] = {2.510038549551032e-08, 2.7620088445409746e-07, 2.7557268459997064e-06,
                         2.4801521295954376e-05, 0.00019841269863053618, 0.0013888888917213717,
                         0.008333333333330062, 0.04166666666662413, 0.16666666666666669, 0.5000000000000001};
@@ -69,6 +70,21 @@ IS3D_HD double exp_poly(const ExpCoef& E, double x) {
   const double k = t - E.shift;
   double r = fma(-k, E.ln2hi, x);
   r = fma(-k, E.ln2lo, r);
+  double p = E.c[0];
+  for (int i = 1; i < 10; i++) p = fma(p, r, E.c[i]);
+  p = fma(p, r, 1.0);
+  p = fma(p, r, 1.0);
+  return ldexp(p, (int)(unsigned)__builtin_bit_cast(unsigned long long, t));
+}
+
+// As exp_poly with a one-FMA reduction r = x - k ln2 (k ln2 exact inside the FMA; the error
+// |k| |ln2 - ln2_double| <= |k| 2.3e-17 is a third of the rounding error |x| 2^-53 >= |k| 7.7e-17
+// that any double argument x already carries, so the result's accuracy relative to the exact
+// exp of the exact argument is unchanged).  Used per point on the modified-momentum path.
+IS3D_HD double exp_poly1(const ExpCoef& E, double x) {
+  const double t = fma(x, E.l2e, E.shift);
+  const double k = t - E.shift;
+  const double r = fma(-k, E.ln2, x);
   double p = E.c[0];
   for (int i = 1; i < 10; i++) p = fma(p, r, E.c[i]);
   p = fma(p, r, 1.0);
@@ -769,11 +785,13 @@ IS3D_HD void sep_setup(int flavor, const double* R, const double* Y, double mT, 
   L.ssc = sign * esc;
   if (!L.fast) { L.Zc = R[R_UX] * R[R_INVT]; L.Zs = R[R_UY] * R[R_INVT]; } else { L.Zc = L.Zs = 0.0; }
   L.D0 = esc * (mT * Y[Y_D]); L.Dc = esc * Y[Y_WDX]; L.Ds = esc * Y[Y_WDY];
-  L.S0 = fma(mT2, Y[Y_S2], fma(mTb, Y[Y_S1], m2 * R[R_S0M2]));
-  L.Sc = fma(mT, Y[Y_SC1], baryon * R[R_SCB]);
-  L.Ss = fma(mT, Y[Y_SS1], baryon * R[R_SSB]);
+  // fast lanes carry the delta-f coefficients pre-multiplied by a (see sep_fast_tail)
+  const double sa = L.fast ? L.a : 1.0;
+  L.S0 = sa * fma(mT2, Y[Y_S2], fma(mTb, Y[Y_S1], m2 * R[R_S0M2]));
+  L.Sc = sa * fma(mT, Y[Y_SC1], baryon * R[R_SCB]);
+  L.Ss = sa * fma(mT, Y[Y_SS1], baryon * R[R_SSB]);
   L.E0 = mT * Y[Y_A]; L.Ec = -R[R_UX]; L.Es = -R[R_UY];
-  L.L0 = fma(mT, Y[Y_L1], baryon * R[R_L0B]); L.Lc = R[R_LC]; L.Ls = R[R_LS];
+  L.L0 = sa * fma(mT, Y[Y_L1], baryon * R[R_L0B]); L.Lc = sa * R[R_LC]; L.Ls = sa * R[R_LS];
   L.c0 = (flavor == SEP_PTB) ? R[R_DZ] - 3.0 * R[R_DLAM] : 0.0;
 }
 
@@ -790,15 +808,15 @@ IS3D_HD double rcp1(double d) {
 
 IS3D_HD double lin(double c0, double cc, double cs, dbl2 p) { return fma(cc, p.x, fma(cs, p.y, c0)); }
 
-// Everything after f_eq for one separable point: returns w * p.dsigma * f_eq (1 + delta-f)
-// (0 when outflow-cut).  feq is e^S f_eq on the fast path (the e^-S sits in pds).
-template <int FL, bool REG, bool OUT, bool FAST>
+// Slow-path tail (per-point exp, unscaled coefficients): returns w * p.dsigma * f_eq (1 + delta-f)
+// (0 when outflow-cut), with 1 - sign f_eq and 1/E formed as in the reference.
+template <int FL, bool REG, bool OUT>
 IS3D_HD double sep_tail(const SepLane& L, dbl2 cs, dbl2 bp, double pds, double feq, double iE) {
   const bool needE = (FL == SEP_CE || FL == SEP_PTB);
   double g = feq * pds;
   if (OUT) g = (pds <= 0.0) ? 0.0 : g;
   if (FL == SEP_FEQ) return g;
-  const double fbar = fma(FAST ? -L.ssc : -L.sign, feq, 1.0);
+  const double fbar = fma(-L.sign, feq, 1.0);
   double S = fma(L.Sc, cs.x, fma(L.Ss, cs.y, L.S0 + bp.y));
   if (needE) S = fma(S, iE, lin(L.L0, L.Lc, L.Ls, cs));
   double t;
@@ -812,30 +830,51 @@ IS3D_HD double sep_tail(const SepLane& L, dbl2 cs, dbl2 bp, double pds, double f
   return g * t;
 }
 
+// Fast-path tail.  With den = a + ssc b' and rq = 1/(den E) (CE/PTB; 1/den for Grad/f_eq):
+//   e^S f_eq = b' E rq,   1 - sign f_eq = 1 - ssc e^S f_eq = a / den = a E rq   (exactly),
+// so f_eq (1 + delta-f) = b' E rq (1 + rq (S' + E L'))   [CE/PTB: delta-f = (1 - sign f_eq)(S/E + L)]
+//                         b' rq (1 + rq S')              [Grad:   delta-f = (1 - sign f_eq) S]
+// with S' = a S, L' = a L (sep_setup folds a into the lane coefficients, a Phi is one FMA here).
+// 1 - sign f_eq becomes a / den instead of 1 - sign f_eq: the same number without the
+// reference's cancellation for bosons near f_eq = 1 (differences at the 1e-16 absolute level).
+template <int FL, bool REG, bool OUT>
+IS3D_HD double sep_fast_tail(const SepLane& L, dbl2 cs, dbl2 bp, double pds, double E, double rq) {
+  const bool needE = (FL == SEP_CE || FL == SEP_PTB);
+  const double pb = pds * bp.x;
+  const double w = needE ? pb * (E * rq) : pb * rq;     // w_eta p.dsigma f_eq
+  double g;
+  if (FL == SEP_FEQ) {
+    g = w;
+  } else {
+    double in = fma(L.a, bp.y, lin(L.S0, L.Sc, L.Ss, cs));
+    if (needE) in = fma(E, lin(L.L0, L.Lc, L.Ls, cs), in);
+    double t;
+    if (REG) {
+      double dfv = rq * in;
+      if (FL == SEP_PTB) dfv += L.c0;
+      t = 1.0 + fmax(-1.0, fmin(dfv, 1.0));
+    } else {
+      t = fma(rq, in, (FL == SEP_PTB) ? 1.0 + L.c0 : 1.0);
+    }
+    g = w * t;
+  }
+  return (OUT && pds <= 0.0) ? 0.0 : g;
+}
+
 // One separable integrand point; returns w * p.dsigma * f (0 when outflow-cut).
 // FL: separable flavour; REG: regulate_deltaf; OUT: outflow; FAST: exp factorised (see sep_setup).
 template <int FL, bool REG, bool OUT, bool FAST>
 IS3D_HD double sep_point_t(const SepLane& L, dbl2 cs, dbl2 bp) {
   const double pds = lin(L.D0, L.Dc, L.Ds, cs);
-  // feq = 1/(exp(u.p/T - chem) + sign) = b'/(a + sign b'); CE/PTB also need 1/E: one reciprocal
-  double feq, iE = 0.0;
   const bool needE = (FL == SEP_CE || FL == SEP_PTB);
-  const double E = needE ? lin(L.E0, L.Ec, L.Es, cs) : 0.0;
-  // FAST: feq holds e^S feq = b'/(a + ssc b'); the e^-S sits in pds, and 1 - sign feq = 1 - ssc (e^S feq)
+  const double E = needE ? lin(L.E0, L.Ec, L.Es, cs) : 1.0;
   if (FAST) {
     const double den = fma(L.ssc, bp.x, L.a);
-    if (needE) {
-      const double r = rcp1(den * E);
-      feq = bp.x * (E * r);
-      iE = den * r;
-    } else {
-      feq = bp.x * rcp1(den);
-    }
-  } else {
-    feq = 1.0 / (exp(L.x - lin(0.0, L.Zc, L.Zs, cs)) + L.sign);
-    if (needE) iE = 1.0 / E;
+    return sep_fast_tail<FL, REG, OUT>(L, cs, bp, pds, E, rcp1(needE ? den * E : den));
   }
-  return sep_tail<FL, REG, OUT, FAST>(L, cs, bp, pds, feq, iE);
+  // feq = 1/(exp(u.p/T - chem) + sign)
+  const double feq = 1.0 / (exp(L.x - lin(0.0, L.Zc, L.Zs, cs)) + L.sign);
+  return sep_tail<FL, REG, OUT>(L, cs, bp, pds, feq, needE ? 1.0 / E : 0.0);
 }
 
 // Two fast-path points of one lane with one reciprocal: 1/q0 = q1/(q0 q1), 1/q1 = q0/(q0 q1),
@@ -849,16 +888,8 @@ IS3D_HD void sep_pair_t(const SepLane& L, dbl2 c0, dbl2 b0, dbl2 c1, dbl2 b1, do
   const double E0 = needE ? lin(L.E0, L.Ec, L.Es, c0) : 1.0, E1 = needE ? lin(L.E0, L.Ec, L.Es, c1) : 1.0;
   const double q0 = needE ? den0 * E0 : den0, q1 = needE ? den1 * E1 : den1;
   const double r = rcp1(q0 * q1);
-  const double r0 = r * q1, r1 = r * q0;
-  double feq0, feq1, iE0 = 0.0, iE1 = 0.0;
-  if (needE) {
-    feq0 = b0.x * (E0 * r0); iE0 = den0 * r0;
-    feq1 = b1.x * (E1 * r1); iE1 = den1 * r1;
-  } else {
-    feq0 = b0.x * r0; feq1 = b1.x * r1;
-  }
-  v0 = sep_tail<FL, REG, OUT, true>(L, c0, b0, pds0, feq0, iE0);
-  v1 = sep_tail<FL, REG, OUT, true>(L, c1, b1, pds1, feq1, iE1);
+  v0 = sep_fast_tail<FL, REG, OUT>(L, c0, b0, pds0, E0, r * q1);
+  v1 = sep_fast_tail<FL, REG, OUT>(L, c1, b1, pds1, E1, r * q0);
 }
 
 IS3D_HD void sep_pair(int flavor, const SepLane& L, dbl2 c0, dbl2 b0, dbl2 c1, dbl2 b1, int regulate, int outflow,
@@ -968,7 +999,7 @@ template <bool CLAMP>
 IS3D_HD double mod_en(const ModLane& L, dbl2 cs, double qv) {
   const double Emod = sqrt_nr(fma(L.Ec, cs.x, fma(L.Es, cs.y, L.E0 + qv)));
   const double x = fma(-Emod, L.invTm, L.chemm);
-  return CLAMP ? exp_clamped(L.ec, x) : exp_poly(L.ec, x);
+  return CLAMP ? exp_clamped(L.ec, x) : exp_poly1(L.ec, x);
 }
 
 template <bool OUT, bool CLAMP>
