@@ -48,6 +48,11 @@ constexpr int kTile = IS3D_KTILE;   // cells per LDS tile
 #define IS3D_SPECTRA_WAVES_MOD 2
 #endif
 
+// LDS row stride of the y-terms (doubles): NYT + 1 is odd, so the 8-byte stores of one y-term field
+// by consecutive lanes (rows 136 B apart) spread over the 64 banks instead of hitting two of them
+// (a 128-B stride put every lane of a wave on the same bank pair: a 32-way conflict)
+constexpr int kYRow = NYT + 1;
+
 struct DevTables {            // device copy of the delta-f tables (pointers into one blob)
   DfTables tb;
 };
@@ -286,7 +291,7 @@ __global__ __launch_bounds__(kBlock, MODE >= PTM ? IS3D_SPECTRA_WAVES_MOD : IS3D
   dbl2* s_bp = s_cs + nphp;                               // [kTile][nphp] {b', Phi}
   double* s_qv = (double*)(s_bp + kTile * nphp);         // [kTile][nphp]  Qv (modified path)
   double* s_grid = s_qv + kTile * nphp;                   // y[nk] | eta[nl] | eta_w[nl]
-  double* s_y = s_grid + A.nk + 2 * A.nl;                 // [kTile][nq][NYT]
+  double* s_y = s_grid + A.nk + 2 * A.nl;                 // [kTile][nq][kYRow]
 
   const int tid = threadIdx.x;
   // XCD-aware block order (cdna_hip_programming.md T1): blocks that share an XCD (same
@@ -365,7 +370,7 @@ __global__ __launch_bounds__(kBlock, MODE >= PTM ? IS3D_SPECTRA_WAVES_MOD : IS3D
         const double y = s_grid[kk];
         const double eta = (A.dim == 3) ? R[R_ETA] : s_grid[A.nk + l];
         const double w = s_grid[A.nk + A.nl + l];
-        yterms(MODE, A.op, R, y, eta, w, s_y + ((long)t * A.nq + q) * NYT);
+        yterms(MODE, A.op, R, y, eta, w, s_y + ((long)t * A.nq + q) * kYRow);
       }
     }
     lds_barrier();
@@ -383,7 +388,7 @@ __global__ __launch_bounds__(kBlock, MODE >= PTM ? IS3D_SPECTRA_WAVES_MOD : IS3D
         const dbl2* BP = s_bp + t * nphp + j0;
         for (int l = 0; l < A.nl; l++) {
           const int q = k * A.nl + l;
-          const double* Y = s_y + ((long)t * A.nq + q) * NYT;
+          const double* Y = s_y + ((long)t * A.nq + q) * kYRow;
           const bool sep = (MODE <= CE) || kind == 1.0 || Y[Y_NARROW] != 0.0;
           if (sep) {
             SepLane L;
@@ -522,7 +527,7 @@ __global__ __launch_bounds__(kBlock, MODE >= PTM ? IS3D_SPECTRA_WAVES_MOD : IS3D
   double* s_qv = (double*)(s_bp + kTile * nphp);         // [kTile][nphp] Qv of the current pT (modified path)
   double* s_red = s_qv + kTile * nphp;                    // [kTile][kBlock] per-lane cell sums
   double* s_grid = s_red + kTile * kBlock;                // y[nk] | eta[nl] | eta_w[nl]
-  double* s_y = s_grid + A.nk + 2 * A.nl;                 // [kTile][nq][NYT]
+  double* s_y = s_grid + A.nk + 2 * A.nl;                 // [kTile][nq][kYRow]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const long nwg = (long)A.nbx * A.nchunk;
@@ -565,7 +570,7 @@ __global__ __launch_bounds__(kBlock, MODE >= PTM ? IS3D_SPECTRA_WAVES_MOD : IS3D
         const double y = s_grid[ky];
         const double eta = (A.dim == 3) ? R[R_ETA] : s_grid[A.nk + l];
         const double w = s_grid[A.nk + A.nl + l];
-        yterms(MODE, 0, R, y, eta, w, s_y + ((long)t * A.nq + q) * NYT);
+        yterms(MODE, 0, R, y, eta, w, s_y + ((long)t * A.nq + q) * kYRow);
       }
     }
     for (int ipt = 0; ipt < A.npT; ipt++) {
@@ -609,7 +614,7 @@ __global__ __launch_bounds__(kBlock, MODE >= PTM ? IS3D_SPECTRA_WAVES_MOD : IS3D
         for (int task = slot; task < A.ntask; task += nslot) {
           const int kk = task / A.nl, l = task % A.nl;
           const int k = kk % A.nk, jb = kk / A.nk, j0 = jb * kJmax;
-          const double* Y = s_y + ((long)t * A.nq + k * A.nl + l) * NYT;
+          const double* Y = s_y + ((long)t * A.nq + k * A.nl + l) * kYRow;
           const dbl2* BP = s_bp + t * nphp + j0;
           const dbl2* W = (const dbl2*)(s_w + j0);
           const bool sep = (MODE <= CE) || kind == 1.0 || Y[Y_NARROW] != 0.0;
@@ -1170,7 +1175,7 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   sa.regulate = e->p.regulate_deltaf; sa.outflow = e->p.outflow; sa.dim = dim; sa.op = 1;
   const size_t shmem = sizeof(double) * (2 * (size_t)kTile * NREC + 2 * (size_t)(kTile + 2) * njb * kJmax +
                                          (size_t)kTile * njb * kJmax + (size_t)(nk + 2 * nl) +
-                                         (size_t)kTile * sa.nq * NYT);
+                                         (size_t)kTile * sa.nq * kYRow);
   if (shmem > 160 * 1024) return e->fail(IS3D_ERR_ARG, "momentum grid too large for the LDS tile");
   const dim3 grid((unsigned)(bx * npT * nsplit));
   const int kflags = (e->p.regulate_deltaf ? F_REG : 0) | (e->p.outflow ? F_OUT : 0);
@@ -1318,7 +1323,7 @@ extern "C" int is3d_calculate_dN_dX(is3d_engine* e, double* dN_taudtaudy, double
     da.npart = np; da.npT = npT; da.nphi = nphi; da.nk = nk; da.nl = nl; da.nq = nk * nl; da.njb = njb; da.dim = dim;
     const size_t nphp = (size_t)njb * kJmax;
     const size_t shmem = sizeof(double) * ((size_t)kTile * NREC + 2 * nphp + 2 * nphp + nphp + 3 * (size_t)kTile * nphp +
-                                           (size_t)kTile * kBlock + (size_t)(nk + 2 * nl) + (size_t)kTile * da.nq * NYT);
+                                           (size_t)kTile * kBlock + (size_t)(nk + 2 * nl) + (size_t)kTile * da.nq * kYRow);
     if (shmem > 160 * 1024) return e->fail(IS3D_ERR_ARG, "momentum grid too large for the LDS tile");
     const long nwg = (long)da.nbx * da.nchunk;
     if (nwg > 0x7fffffffL) return e->fail(IS3D_ERR_ARG, "surface too large for one dN/dX launch");

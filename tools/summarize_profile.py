@@ -47,7 +47,7 @@ def main():
     os.makedirs(prof, exist_ok=True)
     shutil.copy(os.path.join(d, "trace", "run_kernel_stats.csv"), os.path.join(prof, "%s_kernel_stats.csv" % tag))
     out = {}
-    for sub in ("pmcA", "pmcB", "pmcC"):
+    for sub in ("pmcA", "pmcB", "pmcC", "pmcD"):
         p = os.path.join(d, sub, "run_counter_collection.csv")
         if not os.path.exists(p):
             continue
