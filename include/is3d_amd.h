@@ -22,6 +22,8 @@
  *   is3d_get_cell_yields              dN_dy_cell of each freeze-out cell       (SpacetimeDistribution.cpp:374)
  *   is3d_evaluate_df_coefficients     Deltaf_Data::evaluate_df_coefficients    (DeltafData.cpp:501-519)
  *   is3d_surface_averages             ds_max-weighted averages (Plasma)        (readindata.cpp:316-366, iS3D.cpp:184-219)
+ *   is3d_total_yield                  calculate_total_yield (operation 2       (ParticleSampler.cpp:447-636,
+ *                                     oversampling) + particle densities        DeltafData.cpp:555-690)
  *
  * Conventions: caller-owned host buffers in and out; the engine owns its HBM
  * buffers.  Errors are return codes (never exit()); is3d_last_error() gives the
@@ -36,7 +38,7 @@
 extern "C" {
 #endif
 
-#define IS3D_ABI_VERSION 2
+#define IS3D_ABI_VERSION 3
 
 enum {
   IS3D_OK = 0,
@@ -50,7 +52,7 @@ enum {
 typedef struct is3d_engine is3d_engine;
 
 typedef struct {
-  int operation;                  /* 1 continuous spectra, 0 spacetime distributions (2, the sampler, is rejected);
+  int operation;                  /* 1 continuous spectra, 0 spacetime distributions, 2 the sampler's yield estimate;
                                      informs the host facade -- each compute entry point fixes its own semantics */
   int dimension;                  /* 2 = boost-invariant (eta quadrature), 3 = 3+1d (y grid) */
   int df_mode;                    /* 1 Grad, 2 RTA-CE, 3 PTM, 4 PTB, 5 PTMA */
@@ -160,6 +162,16 @@ int is3d_evaluate_df_coefficients(is3d_engine *e, double T, double muB, double E
 /* out[5] = T, E, P, muB, nB averages (after the setprecision(15) round trip). */
 int is3d_surface_averages(long n_cells, const is3d_surface *s, int include_baryon, double *out5);
 /* Jonah table the engine built: lambda^2, z, bulkPi/P (301 each) and the max. */
+/* operation = 2 oversampling estimate: the reference's Ntotal (ParticleSampler.cpp:447-636
+ * calculate_total_yield, EmissionFunction.cpp:1237-1242), with the per-species densities of
+ * Deltaf_Data::compute_particle_densities (DeltafData.cpp:555-690) evaluated on the device at the
+ * Plasma averages plasma = (T, E, P, muB, nB) (is3d_surface_averages).  Like the reference, the
+ * densities use the alpha = 1, 2, 3 rows of tables/gauss/gla_roots_weights.txt: set that 32-point
+ * table with is3d_set_gauss_laguerre.  2+1D: multiplied by 2 y_cut.  densities (optional, [3][npart]):
+ * equilibrium, bulk and diffusion densities of the chosen species.  Nevents =
+ * min(ceil(min_num_hadrons / Ntotal), max_num_samples) is the caller's (EmissionFunction.cpp:1242). */
+int is3d_total_yield(is3d_engine *e, const double *plasma, double y_cut, double *n_total, double *densities);
+
 int is3d_get_jonah_table(const is3d_engine *e, double *lambda2, double *z, double *bulk_over_P,
                          double *bulk_over_P_max);
 

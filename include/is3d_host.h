@@ -5,6 +5,8 @@
  *   is3d_host_run_particlization   IS3D::run_particlization(1) for operation = 1 or 0 (iS3D.cpp:81-282)
  *                                  reading <workdir>/iS3D_parameters.dat, input/surface.dat, PDG/,
  *                                  deltaf_coefficients/, tables/ and writing results/continuous/
+ *   is3d_host_total_yield          IS3D::run_particlization(1) for operation = 2: the oversampling
+ *                                  estimate Ntotal / Nevents (EmissionFunction.cpp:1235-1249)
  *   is3d_host_read_surface         FO_data_reader::read_freezeout_surface modes 1/5/6/7 (readindata.cpp:149-731)
  *   is3d_host_read_pdg             PDG_Data::read_resonances                            (readindata.cpp:1217-1252)
  *   is3d_host_param                ParameterReader::getVal                              (ParameterReader.cpp:142-155)
@@ -20,6 +22,11 @@ extern "C" {
  * or, per species, [dN_taudtaudy (tau_bins) | dN_2pirdrdy (r_bins) | dN_dphidy (phip_bins)] (operation 0). */
 int is3d_host_run_particlization(const char *workdir, int device, int num_devices, double *dN_out,
                                  long out_capacity, char *err, int errlen);
+/* operation = 2 in <workdir>/iS3D_parameters.dat: n_total = the estimated total yield (0 unless
+ * oversample = 1), n_events = min(ceil(min_num_hadrons / Ntotal), max_num_samples) (1 without
+ * oversampling).  The particle sampler itself is not on this engine's path. */
+int is3d_host_total_yield(const char *workdir, int device, int num_devices, double *n_total, long *n_events,
+                          char *err, int errlen);
 /* Returns the number of cells (or < 0); fields (optional) receives [25][n] in is3d_surface order,
  * avg5 the Plasma averages T, E, P, muB, nB after the 15-digit round trip. */
 long is3d_host_read_surface(const char *workdir, int mode, int dimension, int include_baryon, double *fields,

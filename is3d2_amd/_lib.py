@@ -20,7 +20,7 @@ EXPORTS = ["is3d_abi_version", "is3d_create", "is3d_destroy", "is3d_last_error",
            "is3d_set_df_tables", "is3d_set_surface", "is3d_set_surface_device", "is3d_calculate_spectra",
            "is3d_launch", "is3d_finish", "is3d_get_stats", "is3d_output_size", "is3d_evaluate_df_coefficients",
            "is3d_surface_averages", "is3d_get_jonah_table", "is3d_set_momentum_weights", "is3d_set_spacetime_bins",
-           "is3d_calculate_dN_dX", "is3d_get_cell_yields"]
+           "is3d_calculate_dN_dX", "is3d_get_cell_yields", "is3d_total_yield"]
 
 
 class Params(C.Structure):
@@ -86,5 +86,6 @@ def load():
     lib.is3d_set_spacetime_bins.argtypes = [C.c_void_p, P(SpacetimeBins)]
     lib.is3d_calculate_dN_dX.argtypes = [C.c_void_p, pd, pd, pd]
     lib.is3d_get_cell_yields.argtypes = [C.c_void_p, pd]
+    lib.is3d_total_yield.argtypes = [C.c_void_p, pd, d, pd, pd]
     _lib = lib
     return lib

@@ -529,6 +529,104 @@ IS3D_HD int prep_feqmod(const PrepConsts& k, const DfTables& tb, const double* s
   return DF_OK;
 }
 
+// ---------------------------------------------------------------------------
+// operation = 2 oversampling estimate (ParticleSampler.cpp:447-636 calculate_total_yield)
+// ---------------------------------------------------------------------------
+// The six GaussThermal integrands (GaussThermal.cpp:19-78) that compute_particle_densities
+// (DeltafData.cpp:555-690) needs, at Gauss-Laguerre root p of the matching alpha.
+IS3D_HD double gt_term(int kind, double p, double mbar, double chem, double sign) {
+  const double Eb = sqrt(p * p + mbar * mbar);
+  if (kind == 0) return p * exp(p) / (exp(Eb - chem) + sign);                 // neq   (a = 1)
+  const double q = exp(Eb - chem) + sign, x = exp(p + Eb - chem) / (q * q);
+  switch (kind) {
+    case 1: return p * x;                                                       // J10   (a = 1)
+    case 2: return p * p * p / (Eb * Eb) * x;                                   // J11   (a = 1)
+    case 3: return Eb * x;                                                      // J20   (a = 2)
+    case 4: return Eb * Eb / p * x;                                             // J30   (a = 3)
+    default: return p * x;                                                      // J31   (a = 3)
+  }
+}
+
+// equilibrium / bulk / diffusion densities of one species from its six thermal integrals
+// J[0..5] = (neq, J10, J11, J20, J30, J31) integrals (before the T^n g / 2 pi^2 hbarc^3 factors)
+IS3D_HD void species_densities(int df_mode, const DfCoef& df, double T, double ber, double mass, double degeneracy,
+                               double baryon, const double* J, double two_pi2_hbarC3, double* out3) {
+  const double neq = degeneracy * pow(T, 3) / two_pi2_hbarC3 * J[0];
+  double dn_bulk = 0.0, dn_diff = 0.0;
+  if (df_mode == GRAD) {
+    const double J10 = degeneracy * pow(T, 3) / two_pi2_hbarC3 * J[1];
+    const double J20 = degeneracy * pow(T, 4) / two_pi2_hbarC3 * J[3];
+    const double J30 = degeneracy * pow(T, 5) / two_pi2_hbarC3 * J[4];
+    const double J31 = degeneracy * pow(T, 5) / two_pi2_hbarC3 / 3.0 * J[5];
+    dn_bulk = ((df.c0 - df.c2) * mass * mass * J10 + df.c1 * baryon * J20 + (4.0 * df.c2 - df.c0) * J30);
+    dn_diff = baryon * df.c3 * neq * T + df.c4 * J31;
+  } else if (df_mode != PTB) {   // CE, PTM and PTMA (goto chapman_enskog, :666-669)
+    const double J10 = degeneracy * pow(T, 3) / two_pi2_hbarC3 * J[1];
+    const double J11 = degeneracy * pow(T, 3) / two_pi2_hbarC3 / 3.0 * J[2];
+    const double J20 = degeneracy * pow(T, 4) / two_pi2_hbarC3 * J[3];
+    dn_bulk = (neq + (baryon * J10 * df.G) + (J20 * df.F / pow(T, 2))) / df.betabulk;
+    dn_diff = (neq * T * ber - baryon * J11) / df.betaV;
+  }
+  out3[0] = neq; out3[1] = dn_bulk; out3[2] = dn_diff;
+}
+
+// Sum over chosen species of estimate_mean_particle_number (ParticleSampler.cpp:75-119) for one
+// cell; dsum = species sums of the (equilibrium, bulk, diffusion) densities, which the estimate is
+// linear in.  Returns 0 for cells with u.dsigma <= 0.  ds_space per compute_dsigma_magnitude
+// (the reference reads that member without calling it, :582-583: uninitialised).
+IS3D_HD int yield_cell(const PrepConsts& k, const DfTables& tb, const double* s, const double* dsum, double* out) {
+  *out = 0.0;
+  const double tau = s[S_TAU], tau2 = tau * tau;
+  const double dat = s[S_DAT], dax = s[S_DAX], day = s[S_DAY], dan = s[S_DAN];
+  const double ux = s[S_UX], uy = s[S_UY], un = s[S_UN];
+  const double ut = sqrt(1. + ux * ux + uy * uy + tau2 * un * un);
+  const double uperp = sqrt(ux * ux + uy * uy), utperp = sqrt(1. + ux * ux + uy * uy);
+  const double ux2 = ux * ux, uy2 = uy * uy, ut2 = ut * ut;
+  if (ut * dat + ux * dax + uy * day + un * dan <= 0) return DF_OK;
+  const double T = s[S_T], P = s[S_P], E = s[S_E];
+  double pitt = 0, pitx = 0, pity = 0, pitn = 0, pixx = 0, pixy = 0, pixn = 0, piyy = 0, piyn = 0, pinn = 0;
+  if (k.include_shear && k.df_mode == PTB) {     // pi only enters through the PTB breakdown test
+    pixx = s[S_PIXX]; pixy = s[S_PIXY]; pixn = s[S_PIXN]; piyy = s[S_PIYY]; piyn = s[S_PIYN];
+    pinn = (pixx * (ux2 - ut2) + piyy * (uy2 - ut2) + 2. * (pixy * ux * uy + tau2 * un * (pixn * ux + piyn * uy))) / (tau2 * utperp * utperp);
+    pitn = (pixn * ux + piyn * uy + tau2 * pinn * un) / ut;
+    pity = (pixy * ux + piyy * uy + tau2 * piyn * un) / ut;
+    pitx = (pixx * ux + pixy * uy + tau2 * pixn * un) / ut;
+    pitt = (pitx * ux + pity * uy + tau2 * pitn * un) / ut;
+  }
+  double bulkPi = k.include_bulk ? s[S_BULKPI] : 0.0;
+  double muB = 0, Vt = 0, Vx = 0, Vy = 0, Vn = 0;
+  if (k.include_baryon && k.include_diff) {
+    muB = s[S_MUB]; Vx = s[S_VX]; Vy = s[S_VY]; Vn = s[S_VN];
+    Vt = (Vx * ux + Vy * uy + tau2 * Vn * un) / ut;
+  }
+  const double Vdsigma = Vt * dat + Vx * dax + Vy * day + Vn * dan;
+  if (k.df_mode == PTB) {     // :548-560
+    if (bulkPi <= -P) bulkPi = -(1.0 - 1.e-5) * P;
+    else if (bulkPi / P >= tb.bulk_over_P_max) bulkPi = P * (tb.bulk_over_P_max - 1.e-5);
+  }
+  DfCoef df;
+  const int err = df_eval(tb, T, muB, E, P, bulkPi, df);
+  if (err) return err;
+  const Milne b = milne_basis(ut, ux, uy, un, uperp, utperp, tau);
+  const double ds_time = dat * ut + dax * ux + day * uy + dan * un;          // LocalRestFrame.cpp:81-91
+  const double dsx = -(dat * b.Xt + dax * b.Xx + day * b.Xy + dan * b.Xn);
+  const double dsy = -(dax * b.Yx + day * b.Yy);
+  const double dsz = -(dat * b.Zt + dan * b.Zn);
+  const double ds_space = sqrt(dsx * dsx + dsy * dsy + dsz * dsz);
+  if (k.df_mode == PTB) {
+    const PiLRF pl_ = boost_pi(b, tau2, pitt, pitx, pity, pitn, pixx, pixy, pixn, piyy, piyn, pinn);
+    const double shear_mod = 0.5 / df.betapi, bulk_mod = df.lambda;
+    const double Axx = 1.0 + pl_.xx * shear_mod + bulk_mod, Axy = pl_.xy * shear_mod, Axz = pl_.xz * shear_mod;
+    const double Ayy = 1.0 + pl_.yy * shear_mod + bulk_mod, Ayz = pl_.yz * shear_mod, Azz = 1.0 + pl_.zz * shear_mod + bulk_mod;
+    const double detA = Axx * (Ayy * Azz - Ayz * Ayz) - Axy * (Axy * Azz - Ayz * Axz) + Axz * (Axy * Ayz - Ayy * Axz);
+    const bool breaks = (detA <= k.deta_min || df.z < 0.0);
+    *out = breaks ? ds_time * (1.0 + df.dz) * dsum[0] : ds_time * df.z * dsum[0];
+  } else {
+    *out = ds_time * (dsum[0] + bulkPi * dsum[1]) - ds_space * Vdsigma * dsum[2];
+  }
+  return DF_OK;
+}
+
 // PTM per-(cell, species) renormalisation (MomentumSpectra.cpp:790-832); NaN => species skipped.
 IS3D_HD double ptm_renorm(const PrepConsts& k, const double* aux, double mass, double sign, double degeneracy, double baryon) {
   const double T = aux[0], T_mod = aux[1], alphaB = aux[2], alphaB_mod = aux[3], F = aux[4], G = aux[5];

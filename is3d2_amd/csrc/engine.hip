@@ -695,6 +695,88 @@ __global__ __launch_bounds__(256) void k_stbin(BinArgs A) {
   A.part[(long)A.sorig[s] * A.nent + e] = acc;
 }
 
+// ------------------------------------------------------------------------------------------
+// operation = 2 oversampling estimate (ParticleSampler.cpp:447-636, DeltafData.cpp:555-690)
+// ------------------------------------------------------------------------------------------
+struct DensArgs {
+  DfTables tb;
+  const double *gla;              // [alpha][pts] roots then [alpha][pts] weights
+  int gla_alpha, gla_pts;
+  double T, E, P, muB, nB;        // Plasma averages
+  const double *smass, *ssign, *sdegen, *sbaryon; const int* sorig;
+  int npart, df_mode;
+  double two_pi2_hbarC3;
+  double* dens;                   // [3][npart] original species order
+  int* err;
+};
+
+// one wavefront per (mass-sorted) species: lane k holds Gauss-Laguerre node k of each alpha
+__global__ __launch_bounds__(64) void k_densities(DensArgs A) {
+  const int s = blockIdx.x, lane = threadIdx.x;
+  DfCoef df;
+  const int err = df_eval(A.tb, A.T, A.muB, A.E, A.P, 0.0, df);     // DeltafData.cpp:574
+  if (err) { if (lane == 0) atomicMax(A.err, err); return; }
+  const double mass = A.smass[s], sign = A.ssign[s], baryon = A.sbaryon[s];
+  const double mbar = mass / A.T, chem = baryon * (A.muB / A.T);
+  const double* W = A.gla + (long)A.gla_alpha * A.gla_pts;
+  static constexpr int kAlpha[6] = {1, 1, 1, 2, 3, 3};
+  double J[6];
+  WaveSum ws;
+#pragma unroll
+  for (int q = 0; q < 6; q++) {
+    double v = 0.0;
+    for (int k = lane; k < A.gla_pts; k += 64) {
+      const long o = (long)kAlpha[q] * A.gla_pts + k;
+      v += W[o] * gt_term(q, A.gla[o], mbar, chem, sign);
+    }
+    J[q] = ws(v);
+  }
+  if (lane == 0) {
+    double d3[3];
+    species_densities(A.df_mode, df, A.T, A.nB / (A.E + A.P), mass, A.sdegen[s], baryon, J, A.two_pi2_hbarC3, d3);
+    const int so = A.sorig[s];
+    for (int i = 0; i < 3; i++) A.dens[(long)i * A.npart + so] = d3[i];
+  }
+}
+
+struct YieldArgs {
+  PrepConsts k;
+  DfTables tb;
+  const double* surf; long n;
+  const double* dens; int npart;
+  double* partial;                // [gridDim.x] per-block sums
+  int* err;
+};
+
+// one thread per cell, fixed-order tree sum per block (bit-reproducible); the host adds the blocks in order
+__global__ __launch_bounds__(256) void k_yield(YieldArgs A) {
+  __shared__ double red[256];
+  __shared__ double dsum[3];
+  const int tid = threadIdx.x;
+  if (tid < 3) {                  // species sums in species order
+    double a = 0.0;
+    for (int i = 0; i < A.npart; i++) a += A.dens[(long)tid * A.npart + i];
+    dsum[tid] = a;
+  }
+  __syncthreads();
+  const long c = (long)blockIdx.x * 256 + tid;
+  double v = 0.0;
+  if (c < A.n) {
+    double sv[NSURF];
+#pragma unroll
+    for (int f = 0; f < NSURF; f++) sv[f] = A.surf[(long)f * A.n + c];
+    const int err = yield_cell(A.k, A.tb, sv, dsum, &v);
+    if (err) { atomicMax(A.err, err); v = 0.0; }
+  }
+  red[tid] = v;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) red[tid] += red[tid + o];
+    __syncthreads();
+  }
+  if (tid == 0) A.partial[blockIdx.x] = red[0];
+}
+
 __global__ void k_df_eval(DfTables tb, double T, double muB, double E, double P, double bulkPi, double* out, int* err) {
   DfCoef df;
   *err = df_eval(tb, T, muB, E, P, bulkPi, df);
@@ -809,8 +891,9 @@ extern "C" const char* is3d_last_error(const is3d_engine* e) { return e ? e->err
 
 extern "C" int is3d_set_params(is3d_engine* e, const is3d_params* p) {
   if (!e || !p) return IS3D_ERR_ARG;
-  if (p->operation != 0 && p->operation != 1)
-    return e->fail(IS3D_ERR_UNSUPPORTED, "calculate_spectra: operation = 2 (particle sampler) is not on this path; use 0 or 1");
+  // operation 2 is accepted for its oversampling estimate (is3d_total_yield); the sampler itself is not on this path
+  if (p->operation < 0 || p->operation > 2)
+    return e->fail(IS3D_ERR_ARG, "calculate_spectra error: need to set operation = (0, 1, 2)");
   if (p->dimension != 2 && p->dimension != 3) return e->fail(IS3D_ERR_ARG, "EmissionFunctionArray error: need to set dimension = (2,3)");
   if (p->df_mode < 1 || p->df_mode > 5) return e->fail(IS3D_ERR_ARG, "EmissionFunctionArray error: need to set df_mode = (1,2,3,4,5)");
   if (p->df_mode == PTB && p->include_baryon) return e->fail(IS3D_ERR_UNSUPPORTED, "Bilinear interpolation error: Jonah df doesn't work for nonzero muB. Exiting..");
@@ -1467,6 +1550,54 @@ extern "C" int is3d_evaluate_df_coefficients(is3d_engine* e, double T, double mu
   if (h != hipSuccess) return hip_fail(e, h, "df eval");
   if (derr == DF_SPLINE_RANGE || derr == DF_TABLE_RANGE) return e->fail(IS3D_ERR_DF_RANGE, "df coefficient evaluated out of range");
   if (derr) return e->fail(IS3D_ERR_ARG, "df coefficient error");
+  return IS3D_OK;
+}
+
+extern "C" int is3d_total_yield(is3d_engine* e, const double* plasma, double y_cut, double* n_total,
+                                double* densities) {
+  if (!e || !plasma || !n_total) return IS3D_ERR_ARG;
+  int rc = finalize_tables(e);
+  if (rc) return rc;
+  if (!e->have_gla || e->gla_alpha < 4) return e->fail(IS3D_ERR_STATE, "is3d_set_gauss_laguerre: alpha = 1..3 tables needed");
+  if (e->gla_pts > 64) return e->fail(IS3D_ERR_ARG, "Gauss-Laguerre table longer than 64 points");
+  HIPCHK(e, hipSetDevice(e->device));
+  const int np = (int)e->mass.size();
+  const long n = e->ncell;
+  const long nb = (n + 255) / 256;
+  double* d = dalloc<double>(3 * (size_t)np + (size_t)std::max(nb, 1L) + 1);
+  if (!d) return e->fail(IS3D_ERR_DEVICE, "hipMalloc failed");
+  HIPCHK(e, hipMemset(e->d_err, 0, sizeof(int)));
+  DensArgs da{};
+  da.tb = e->dtb; da.gla = e->d_gla; da.gla_alpha = e->gla_alpha; da.gla_pts = e->gla_pts;
+  da.T = plasma[0]; da.E = plasma[1]; da.P = plasma[2]; da.muB = plasma[3]; da.nB = plasma[4];
+  da.smass = e->d_smass; da.ssign = e->d_ssign; da.sdegen = e->d_sdegen; da.sbaryon = e->d_sbaryon; da.sorig = e->d_sorig;
+  da.npart = np; da.df_mode = e->p.df_mode; da.two_pi2_hbarC3 = 2.0 * std::pow(M_PI, 2) * std::pow(kHbarC, 3);
+  da.dens = d; da.err = e->d_err;
+  hipLaunchKernelGGL(k_densities, dim3((unsigned)np), dim3(64), 0, 0, da);
+  hipError_t h = hipGetLastError();
+  std::vector<double> part((size_t)std::max(nb, 1L), 0.0);
+  if (h == hipSuccess && n > 0) {
+    YieldArgs ya{};
+    ya.k = make_consts(e); ya.tb = e->dtb; ya.surf = e->d_surf; ya.n = n; ya.dens = d; ya.npart = np;
+    ya.partial = d + 3 * (size_t)np; ya.err = e->d_err;
+    hipLaunchKernelGGL(k_yield, dim3((unsigned)nb), dim3(256), 0, 0, ya);
+    h = hipGetLastError();
+  }
+  if (h == hipSuccess) h = hipDeviceSynchronize();
+  int derr = 0;
+  if (h == hipSuccess) h = hipMemcpy(&derr, e->d_err, sizeof(int), hipMemcpyDeviceToHost);
+  if (h == hipSuccess && n > 0) h = hipMemcpy(part.data(), d + 3 * (size_t)np, nb * sizeof(double), hipMemcpyDeviceToHost);
+  if (h == hipSuccess && densities) h = hipMemcpy(densities, d, 3 * (size_t)np * sizeof(double), hipMemcpyDeviceToHost);
+  dfree(d);
+  if (h != hipSuccess) return hip_fail(e, h, "total yield");
+  if (derr == DF_SPLINE_RANGE) return e->fail(IS3D_ERR_DF_RANGE, "gsl: interpolation error (df coefficient spline evaluated out of range)");
+  if (derr == DF_TABLE_RANGE) return e->fail(IS3D_ERR_DF_RANGE, "Error: (T,muB) outside df coefficient table");
+  if (derr == DF_PTB_BARYON) return e->fail(IS3D_ERR_UNSUPPORTED, "Bilinear interpolation error: Jonah df doesn't work for nonzero muB. Exiting..");
+  if (derr) return e->fail(IS3D_ERR_ARG, "df coefficient error");
+  double Ntot = 0.0;
+  for (long b = 0; b < nb; b++) Ntot += part[b];
+  if (e->p.dimension == 2) Ntot *= 2.0 * y_cut;     // :628-631
+  *n_total = Ntot;
   return IS3D_OK;
 }
 

@@ -122,6 +122,11 @@ void EmissionFunctionArray::run_sharded(const RunOptions& opt, int operation) {
       if (operation == 1) {
         parts[k].assign(is3d_output_size(e), 0.0);
         set_or_throw(e, is3d_calculate_spectra(e, parts[k].data()));
+      } else if (operation == 2) {
+        // the estimate is a sum over cells: per-shard partial Ntotal (the Plasma averages stay global)
+        const double plasma[5] = {plasma_.T, plasma_.E, plasma_.P, plasma_.muB, plasma_.nB};
+        parts[k].assign(1, 0.0);
+        set_or_throw(e, is3d_total_yield(e, plasma, p_.get("y_cut", 0.5), parts[k].data(), nullptr));
       } else {
         set_or_throw(e, is3d_set_momentum_weights(e, pTw.data(), phiw.data()));
         set_or_throw(e, is3d_set_spacetime_bins(e, &bins));
@@ -147,6 +152,8 @@ void EmissionFunctionArray::run_sharded(const RunOptions& opt, int operation) {
     for (size_t i = 0; i < sum.size(); i++) sum[i] += parts[k][i];
   if (operation == 1) {
     dN_ = std::move(sum);
+  } else if (operation == 2) {
+    ntotal_ = sum[0];
   } else {
     const long nt = (long)np * bins.tau_bins, nr = (long)np * bins.r_bins;
     bins_ = bins;
@@ -160,6 +167,11 @@ void EmissionFunctionArray::run_sharded(const RunOptions& opt, int operation) {
 void EmissionFunctionArray::calculate_spectra(const RunOptions& opt) { run_sharded(opt, 1); }
 
 void EmissionFunctionArray::calculate_dN_dX(const RunOptions& opt) { run_sharded(opt, 0); }
+
+double EmissionFunctionArray::estimate_total_yield(const RunOptions& opt) {
+  run_sharded(opt, 2);
+  return ntotal_;
+}
 
 void EmissionFunctionArray::write_spacetime_files(const std::string& dir) const {
   SpacetimeView v{dNtau_.data(), dNr_.data(), dNphi_.data(), (int)mass_.size(), bins_.tau_min, bins_.tau_max,
@@ -200,8 +212,7 @@ void IS3D::run_particlization(int fo_from_file, const RunOptions& opt) {
   ParameterReader prm;
   check(prm.read_file(path_in(dir_, "iS3D_parameters.dat")), "ParameterReader::readFromFile error: file iS3D_parameters.dat does not exist.");
   const int operation = (int)prm.get("operation");
-  check(operation == 0 || operation == 1, "operation = " + std::to_string(operation) +
-                            " is not on this engine's path (0 spacetime distributions, 1 continuous spectra)");
+  check(operation == 0 || operation == 1 || operation == 2, "calculate_spectra error: need to set operation = (0, 1, 2)");
   const int mode = (int)prm.get("mode"), dimension = (int)prm.get("dimension"), hrg = (int)prm.get("hrg_eos");
   const int include_baryon = (int)prm.get("include_baryon");
   Surface file_surf;
@@ -235,6 +246,19 @@ void IS3D::run_particlization(int fo_from_file, const RunOptions& opt) {
   err = read_gauss_laguerre(path_in(dir_, "tables/gauss/gla_roots_weights.txt"), galpha, gpts, gr, gw);
   check(err.empty(), err);
   EmissionFunctionArray efa(prm, chosen, pT, phi, y, eta, parts, *surf, df, avg, gr, gw, galpha, gpts);
+  if (operation == 2) {        // EmissionFunction.cpp:1235-1249: the oversampling estimate
+    nevents_ = 1;
+    if ((int)prm.get("oversample", 0.0)) {
+      ntotal_ = efa.estimate_total_yield(opt);
+      if (!opt.quiet) std::printf("\nEstimated total particle yield = %ld particles\n", (long)ntotal_);
+      nevents_ = (long)std::min(std::ceil(prm.get("min_num_hadrons", 1.0e5) / ntotal_), prm.get("max_num_samples", 1.0e3));
+      if (!opt.quiet) std::printf("\nSampling %ld particlization events...\n\n", nevents_);
+    } else if (!opt.quiet) {
+      std::printf("\nSampling 1 particlization event...\n\n");
+    }
+    dN_.clear();
+    return;
+  }
   if (operation == 1) {
     efa.calculate_spectra(opt);
     if (opt.write_files) efa.write_files(dir_);
@@ -281,6 +305,24 @@ extern "C" int is3d_host_run_particlization(const char* workdir, int device, int
       if ((long)dN.size() > out_capacity) { put_err(err, errlen, "output buffer too small"); return IS3D_ERR_ARG; }
       std::copy(dN.begin(), dN.end(), dN_out);
     }
+    return IS3D_OK;
+  } catch (const std::exception& ex) {
+    put_err(err, errlen, ex.what());
+    return IS3D_ERR_ARG;
+  }
+}
+
+extern "C" int is3d_host_total_yield(const char* workdir, int device, int num_devices, double* n_total,
+                                     long* n_events, char* err, int errlen) {
+  try {
+    IS3D run(workdir ? workdir : ".");
+    RunOptions opt;
+    opt.device = device;
+    opt.num_devices = num_devices;
+    opt.quiet = true;
+    run.run_particlization(1, opt);
+    if (n_total) *n_total = run.total_yield();
+    if (n_events) *n_events = run.events();
     return IS3D_OK;
   } catch (const std::exception& ex) {
     put_err(err, errlen, ex.what());

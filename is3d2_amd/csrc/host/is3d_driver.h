@@ -7,8 +7,9 @@
 //
 // Same inputs (iS3D_parameters.dat, input/surface.dat, PDG/, deltaf_coefficients/, tables/
 // relative to a working directory) and the same outputs (results/continuous/*.dat).
-// Differences from the reference: errors are returned / thrown instead of exit(); operation = 2
-// (the sampler) is not on this path; cells may be sharded over several GPUs in one process.
+// Differences from the reference: errors are returned / thrown instead of exit(); of operation = 2
+// only the oversampling estimate (Ntotal, Nevents) is on this path, not the particle sampler itself;
+// cells may be sharded over several GPUs in one process.
 #pragma once
 #include <string>
 #include <vector>
@@ -45,6 +46,8 @@ class EmissionFunctionArray {
   const std::vector<double>& dN_dphidy() const { return dNphi_; }
   is3d_spacetime_bins bins() const { return bins_; }
   const std::vector<long>& mcid() const { return mcid_; }
+  // operation = 2 oversampling estimate (ParticleSampler.cpp:447-636): the reference's Ntotal
+  double estimate_total_yield(const RunOptions& opt);
   double seconds() const { return seconds_; }
 
  private:
@@ -63,7 +66,8 @@ class EmissionFunctionArray {
   std::vector<double> dNtau_, dNr_, dNphi_;
   is3d_spacetime_bins bins_{};
   double seconds_ = 0.0;
-  void run_sharded(const RunOptions& opt, int operation);
+  double ntotal_ = 0.0;
+  void run_sharded(const RunOptions& opt, int operation);   // operation 2: the yield estimate
 };
 
 class IS3D {
@@ -77,13 +81,19 @@ class IS3D {
                                 std::vector<double> uy, std::vector<double> un, std::vector<double> pixx,
                                 std::vector<double> pixy, std::vector<double> pixn, std::vector<double> piyy,
                                 std::vector<double> piyn, std::vector<double> pinn, std::vector<double> Pi);
-  // iS3D.cpp:81-282 for operation = 1 and 0; throws std::runtime_error.  spectra() = the momentum
+  // iS3D.cpp:81-282 for operation = 1, 0 and the estimate of 2; throws std::runtime_error.  spectra() = the momentum
   // spectra (operation 1) or, per species, [dN_taudtaudy | dN_2pirdrdy | dN_dphidy] bins (operation 0)
   void run_particlization(int fo_from_file, const RunOptions& opt = RunOptions());
   const std::vector<double>& spectra() const { return dN_; }
+  // operation = 2: Ntotal and Nevents = min(ceil(min_num_hadrons / Ntotal), max_num_samples) if
+  // oversample, else 1 (EmissionFunction.cpp:1237-1249); the sampling itself is not on this path
+  double total_yield() const { return ntotal_; }
+  long events() const { return nevents_; }
 
  private:
   std::string dir_;
+  double ntotal_ = 0.0;
+  long nevents_ = 0;
   Surface mem_;
   std::vector<double> dN_;
 };

@@ -154,6 +154,15 @@ class Engine:
         self._chk(self.lib.is3d_evaluate_df_coefficients(self._e, T, muB, E, P, bulkPi, _dp(out)))
         return out
 
+    def total_yield(self, plasma, y_cut=0.5):
+        """operation = 2 oversampling estimate (ParticleSampler.cpp:447-636): (Ntotal, densities[3][npart]).
+        plasma = (T, E, P, muB, nB) averages; the engine's Gauss-Laguerre table must be the 32-point one."""
+        pl = _arr(plasma)
+        nt = np.zeros(1)
+        dens = np.zeros(3 * self.npart)
+        self._chk(self.lib.is3d_total_yield(self._e, _dp(pl), float(y_cut), _dp(nt), _dp(dens)))
+        return float(nt[0]), dens.reshape(3, self.npart)
+
     def jonah_table(self):
         l2, z, bp, mx = np.zeros(301), np.zeros(301), np.zeros(301), np.zeros(1)
         self._chk(self.lib.is3d_get_jonah_table(self._e, _dp(l2), _dp(z), _dp(bp), _dp(mx)))

@@ -21,6 +21,7 @@ def load():
         lib.is3d_host_read_surface.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, PD, PD]
         lib.is3d_host_read_pdg.argtypes = [C.c_char_p, C.c_int, C.c_int, PL, PD, PI, PI, PI]
         lib.is3d_host_param.argtypes = [C.c_char_p, C.c_char_p, PD]
+        lib.is3d_host_total_yield.argtypes = [C.c_char_p, C.c_int, C.c_int, PD, PL, C.c_char_p, C.c_int]
         _lib = lib
     return _lib
 
@@ -66,3 +67,14 @@ def run_particlization(workdir, out_size, device=0, num_devices=1):
     if rc:
         raise RuntimeError(err.value.decode())
     return out
+
+
+def total_yield(workdir, device=0, num_devices=1):
+    """operation = 2 in the run directory: (Ntotal, Nevents) of the oversampling estimate."""
+    lib = load()
+    nt, ne = C.c_double(), C.c_long()
+    err = C.create_string_buffer(512)
+    rc = lib.is3d_host_total_yield(workdir.encode(), device, num_devices, C.byref(nt), C.byref(ne), err, 512)
+    if rc:
+        raise RuntimeError(err.value.decode())
+    return nt.value, ne.value

@@ -1568,3 +1568,137 @@ void orc_surface_averages(const orc_surface *S, double *out) {
     out[k] = strtod(buf, NULL);
   }
 }
+
+/* ------------------------------------------------------------------------- */
+/* operation = 2 oversampling estimate                                        */
+/* DeltafData.cpp:555-690 compute_particle_densities (Plasma averages, bulkPi = 0 coefficients)  */
+/* ParticleSampler.cpp:447-636 calculate_total_yield, :75-119 estimate_mean_particle_number      */
+/* ------------------------------------------------------------------------- */
+static void orc_particle_densities(const orc_params *p, const orc_setup *s, const dfcoef *df, const double *plasma,
+                            double *neq_out, double *bulk_out, double *diff_out) {
+  const double T = plasma[0], E = plasma[1], P = plasma[2], muB = plasma[3], nB = plasma[4];
+  const double alphaB = muB / T, ber = nB / (E + P);
+  const int pts = s->gla_points;
+  const double *r1 = s->gla_root + pts, *r2 = s->gla_root + 2 * pts, *r3 = s->gla_root + 3 * pts;
+  const double *w1 = s->gla_weight + pts, *w2 = s->gla_weight + 2 * pts, *w3 = s->gla_weight + 3 * pts;
+  for (int i = 0; i < s->npart; i++) {
+    double mass = s->mass[i], degeneracy = s->degen[i], baryon = s->baryon[i], sign = s->sign[i];
+    double mbar = mass / T;
+    double neq_fact = degeneracy * pow(T, 3) / two_pi2_hbarC3();
+    double neq = neq_fact * orc_gauss_thermal(GT_NEQ, r1, w1, pts, mbar, alphaB, baryon, sign);
+    double dn_bulk = 0.0, dn_diff = 0.0;
+    if (p->df_mode == 1) {                                   /* :614-638 */
+      double J10_fact = degeneracy * pow(T, 3) / two_pi2_hbarC3();
+      double J20_fact = degeneracy * pow(T, 4) / two_pi2_hbarC3();
+      double J30_fact = degeneracy * pow(T, 5) / two_pi2_hbarC3();
+      double J31_fact = degeneracy * pow(T, 5) / two_pi2_hbarC3() / 3.0;
+      double J10 = J10_fact * orc_gauss_thermal(GT_J10, r1, w1, pts, mbar, alphaB, baryon, sign);
+      double J20 = J20_fact * orc_gauss_thermal(GT_J20, r2, w2, pts, mbar, alphaB, baryon, sign);
+      double J30 = J30_fact * orc_gauss_thermal(GT_J30, r3, w3, pts, mbar, alphaB, baryon, sign);
+      double J31 = J31_fact * orc_gauss_thermal(GT_J31, r3, w3, pts, mbar, alphaB, baryon, sign);
+      dn_bulk = ((df->c0 - df->c2) * mass * mass * J10 + df->c1 * baryon * J20 + (4.0 * df->c2 - df->c0) * J30);
+      dn_diff = baryon * df->c3 * neq * T + df->c4 * J31;
+    } else if (p->df_mode == 2 || p->df_mode == 3 || p->df_mode == 5) {   /* :639-661, 666-669 */
+      double J10_fact = degeneracy * pow(T, 3) / two_pi2_hbarC3();
+      double J11_fact = degeneracy * pow(T, 3) / two_pi2_hbarC3() / 3.0;
+      double J20_fact = degeneracy * pow(T, 4) / two_pi2_hbarC3();
+      double J10 = J10_fact * orc_gauss_thermal(GT_J10, r1, w1, pts, mbar, alphaB, baryon, sign);
+      double J11 = J11_fact * orc_gauss_thermal(GT_J11, r1, w1, pts, mbar, alphaB, baryon, sign);
+      double J20 = J20_fact * orc_gauss_thermal(GT_J20, r2, w2, pts, mbar, alphaB, baryon, sign);
+      dn_bulk = (neq + (baryon * J10 * df->G) + (J20 * df->F / pow(T, 2))) / df->betabulk;
+      dn_diff = (neq * T * ber - baryon * J11) / df->betaV;
+    }
+    neq_out[i] = neq; bulk_out[i] = dn_bulk; diff_out[i] = dn_diff;
+  }
+}
+
+/* Surface_Element_Vector::boost_dsigma_to_lrf + compute_dsigma_magnitude (LocalRestFrame.cpp:81-98).
+ * in[9] = ut ux uy un tau dat dax day dan; out[5] = u.dsigma, dsigma_{x,y,z} LRF, dsigma_space */
+void orc_dsigma_lrf(const double *in, double *out) {
+  double ut = in[0], ux = in[1], uy = in[2], un = in[3], tau = in[4];
+  double dat = in[5], dax = in[6], day = in[7], dan = in[8];
+  double uperp = sqrt(ux * ux + uy * uy), utperp = sqrt(1.0 + ux * ux + uy * uy);
+  milne b = milne_basis(ut, ux, uy, un, uperp, utperp, tau);
+  out[0] = dat * ut + dax * ux + day * uy + dan * un;
+  out[1] = -(dat * b.Xt + dax * b.Xx + day * b.Xy + dan * b.Xn);
+  out[2] = -(dax * b.Yx + day * b.Yy);
+  out[3] = -(dat * b.Zt + dan * b.Zn);
+  out[4] = sqrt(out[1] * out[1] + out[2] * out[2] + out[3] * out[3]);
+}
+
+/* Reference loop is serial (its OpenMP pragma is commented out, :456): cells in order, species inner.
+ * ds_space follows Surface_Element_Vector::compute_dsigma_magnitude (LocalRestFrame.cpp:94-98); the
+ * reference reads the member without calling it (:582-583), i.e. an uninitialised value, which only
+ * enters through ds_space * Vdsigma * diffusion_density (baryon diffusion on). */
+int orc_total_yield(const orc_params *p, const orc_setup *s, const orc_surface *S, const double *plasma, double y_cut,
+                    double *n_total, double *densities, char *err, int errlen) {
+  if (p->df_mode < 1 || p->df_mode > 5) { seterr(err, errlen, "Estimate particle yield error: please set df_mode = (1,2,3,4,5)"); return 1; }
+  dfdata d;
+  if (df_setup(&d, p, s, 1)) { seterr(err, errlen, "gsl: x values must be strictly increasing (Jonah table)"); df_free(&d); return 1; }
+  const int npart = s->npart;
+  double *neq = (double *)malloc(sizeof(double) * (3 * npart + 1)), *bulk = neq + npart, *diff = bulk + npart;
+  dfcoef dfa;
+  int rc = df_eval(&d, plasma[0], plasma[3], plasma[1], plasma[2], 0.0, &dfa);   /* DeltafData.cpp:574 */
+  if (rc) { seterr(err, errlen, df_errmsg(rc)); free(neq); df_free(&d); return 1; }
+  orc_particle_densities(p, s, &dfa, plasma, neq, bulk, diff);
+  if (densities) memcpy(densities, neq, sizeof(double) * 3 * npart);
+  const int DF_MODE = p->df_mode;
+  double Ntot = 0.0;
+  for (long ic = 0; ic < S->n; ic++) {
+    double tau = S->tau[ic], tau2 = tau * tau;
+    double dat = S->dat[ic], dax = S->dax[ic], day = S->day[ic], dan = S->dan[ic];
+    double ux = S->ux[ic], uy = S->uy[ic], un = S->un[ic];
+    double ut = sqrt(1. + ux * ux + uy * uy + tau2 * un * un);
+    double uperp = sqrt(ux * ux + uy * uy), utperp = sqrt(1. + ux * ux + uy * uy);
+    double ux2 = ux * ux, uy2 = uy * uy, ut2 = ut * ut;
+    double udsigma = ut * dat + ux * dax + uy * day + un * dan;
+    if (udsigma <= 0) continue;
+    double T = S->T[ic], P = S->P[ic], E = S->E[ic];
+    double pitt = 0, pitx = 0, pity = 0, pitn = 0, pixx = 0, pixy = 0, pixn = 0, piyy = 0, piyn = 0, pinn = 0;
+    if (p->include_shear_deltaf) {
+      pixx = S->pixx[ic]; pixy = S->pixy[ic]; pixn = S->pixn[ic]; piyy = S->piyy[ic]; piyn = S->piyn[ic];
+      pinn = (pixx * (ux2 - ut2) + piyy * (uy2 - ut2) + 2. * (pixy * ux * uy + tau2 * un * (pixn * ux + piyn * uy))) / (tau2 * utperp * utperp);
+      pitn = (pixn * ux + piyn * uy + tau2 * pinn * un) / ut;
+      pity = (pixy * ux + piyy * uy + tau2 * piyn * un) / ut;
+      pitx = (pixx * ux + pixy * uy + tau2 * pixn * un) / ut;
+      pitt = (pitx * ux + pity * uy + tau2 * pitn * un) / ut;
+    }
+    double bulkPi = p->include_bulk_deltaf ? S->bulkPi[ic] : 0.0;
+    double muB = 0, Vt = 0, Vx = 0, Vy = 0, Vn = 0;
+    if (p->include_baryon && p->include_baryondiff_deltaf) {
+      muB = S->muB[ic];
+      Vx = S->Vx[ic]; Vy = S->Vy[ic]; Vn = S->Vn[ic];
+      Vt = (Vx * ux + Vy * uy + tau2 * Vn * un) / ut;
+    }
+    double Vdsigma = Vt * dat + Vx * dax + Vy * day + Vn * dan;
+    if (DF_MODE == 4) {                                        /* :548-560 */
+      if (bulkPi <= -P) bulkPi = -(1.0 - 1.e-5) * P;
+      else if (bulkPi / P >= d.bulkPi_over_Peq_max) bulkPi = P * (d.bulkPi_over_Peq_max - 1.e-5);
+    }
+    dfcoef df;
+    rc = df_eval(&d, T, muB, E, P, bulkPi, &df);
+    if (rc) break;
+    milne b = milne_basis(ut, ux, uy, un, uperp, utperp, tau);
+    double dsin[9] = {ut, ux, uy, un, tau, dat, dax, day, dan}, dso[5];
+    orc_dsigma_lrf(dsin, dso);
+    double ds_time = dso[0], ds_space = dso[4];
+    int breaks = 0;
+    if (DF_MODE == 4) {          /* the only mode whose estimate depends on the breakdown (:91-104) */
+      pilrf pl_ = boost_pimunu(b, tau2, pitt, pitx, pity, pitn, pixx, pixy, pixn, piyy, piyn, pinn);
+      double shear_mod = 0.5 / df.betapi, bulk_mod = df.lambda;
+      double Axx = 1.0 + pl_.xx * shear_mod + bulk_mod, Axy = pl_.xy * shear_mod, Axz = pl_.xz * shear_mod;
+      double Ayy = 1.0 + pl_.yy * shear_mod + bulk_mod, Ayz = pl_.yz * shear_mod, Azz = 1.0 + pl_.zz * shear_mod + bulk_mod;
+      double detA = Axx * (Ayy * Azz - Ayz * Ayz) - Axy * (Axy * Azz - Ayz * Axz) + Axz * (Axy * Ayz - Ayy * Axz);
+      breaks = feqmod_breaks_down(p->mass_pion0, T, df.F, bulkPi, df.betabulk, detA, p->deta_min, df.z, s, 4);
+    }
+    for (int ipart = 0; ipart < npart; ipart++) {
+      if (DF_MODE == 4) Ntot += breaks ? ds_time * (1.0 + df.delta_z) * neq[ipart] : ds_time * df.z * neq[ipart];
+      else Ntot += ds_time * (neq[ipart] + bulkPi * bulk[ipart]) - ds_space * Vdsigma * diff[ipart];
+    }
+  }
+  if (!rc && p->dimension == 2) Ntot *= (2.0 * y_cut);
+  if (rc) seterr(err, errlen, df_errmsg(rc));
+  *n_total = Ntot;
+  free(neq); df_free(&d);
+  return rc ? 1 : 0;
+}

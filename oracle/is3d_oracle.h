@@ -16,6 +16,7 @@
  *   LocalRestFrame.cpp:12-185     Milne basis, pi^{mu nu} / V^mu LRF boosts
  *   AnisoVariables.cpp:15-643     (lambda, aT, aL) Newton solve + famod coefficients
  *   EmissionFunction.cpp:33-109   feqmod breakdown tests
+ *   ParticleSampler.cpp:75-119, 447-636 + DeltafData.cpp:555-690   operation 2 yield estimate
  * The OpenMP cell striding of the reference (thread n takes cells n, n+C, ...,
  * MomentumSpectra.cpp:98-107) is emulated with `threads` = C virtual threads, so
  * the summation order and the PTMA warm-start chains follow the reference run
@@ -113,12 +114,21 @@ int orc_dndx(const orc_params *p, const orc_setup *s, const orc_surface *surf, c
              double *cell_yield, double *tau_out, double *r_out, double *phi_out, long *stats,
              char *err, int errlen);
 
+/* operation = 2 oversampling estimate (ParticleSampler.cpp:447-636 calculate_total_yield with the
+ * DeltafData.cpp:555-690 densities).  plasma = (T, E, P, muB, nB) Plasma averages; the Gauss-Laguerre
+ * table must be tables/gauss/gla_roots_weights.txt (32 points), as compute_particle_densities loads it.
+ * n_total = the reference's Ntotal (x 2 y_cut in 2+1D); densities (optional) = [3][npart] equilibrium,
+ * bulk and diffusion densities of the chosen species. */
+int orc_total_yield(const orc_params *p, const orc_setup *s, const orc_surface *surf, const double *plasma,
+                    double y_cut, double *n_total, double *densities, char *err, int errlen);
+
 /* --- pieces exposed for pinning tests --- */
 double orc_gauss_thermal(int kind, const double *root, const double *weight, int pts,
                          double mbar, double alphaB, double baryon, double sign);
 double orc_gauss1d_mod(int kind, const double *root, const double *weight, int pts,
                        double mbar, double lambda, double sign);
 void orc_milne_lrf(const double *in15, double *out14);
+void orc_dsigma_lrf(const double *in9, double *out5);
 int orc_df_coefficients(const orc_params *p, const orc_setup *s, double T, double muB,
                         double E, double P, double bulkPi, double *out15, char *err, int errlen);
 int orc_jonah_table(const orc_setup *s, double *lambda2, double *z, double *bulk_over_P,

@@ -65,10 +65,13 @@ def load():
         lib.orc_gauss1d_mod.restype = C.c_double
         lib.orc_gauss1d_mod.argtypes = [C.c_int, PD, PD, C.c_int, C.c_double, C.c_double, C.c_double]
         lib.orc_milne_lrf.argtypes = [PD, PD]
+        lib.orc_dsigma_lrf.argtypes = [PD, PD]
         lib.orc_df_coefficients.argtypes = [C.POINTER(OrcParams), C.POINTER(OrcSetup), C.c_double, C.c_double,
                                             C.c_double, C.c_double, C.c_double, PD, C.c_char_p, C.c_int]
         lib.orc_jonah_table.argtypes = [C.POINTER(OrcSetup), PD, PD, PD, PD]
         lib.orc_surface_averages.argtypes = [C.POINTER(OrcSurface), PD]
+        lib.orc_total_yield.argtypes = [C.POINTER(OrcParams), C.POINTER(OrcSetup), C.POINTER(OrcSurface), PD,
+                                        C.c_double, PD, PD, C.c_char_p, C.c_int]
         lib.orc_aniso_solve.argtypes = [C.POINTER(OrcSetup), C.c_double, C.c_double, C.c_double, C.c_double,
                                         C.c_double, C.c_double, PD]
         _lib = lib
@@ -187,3 +190,23 @@ def dndx(spec, surf, T_avg=None, threads=1, omp_threads=0, carry=None, return_ce
     if return_cells:
         return out + (cy[:npart * n].reshape(npart, n),)
     return out
+
+
+def total_yield(spec, surf, plasma=None, y_cut=0.5):
+    """operation = 2 oversampling estimate (ParticleSampler.cpp:447-636): (Ntotal, densities[3][npart]).
+    plasma = (T, E, P, muB, nB) averages (default: this surface's)."""
+    lib = load()
+    p = spec["params"]
+    if plasma is None:
+        plasma = averages(surf, p["include_baryon"])
+    inp = _Inputs(spec, surf, plasma[0], 1)
+    pl = _a(plasma)
+    npart = len(spec["species"]["mass"])
+    dens = np.zeros(3 * npart)
+    nt = np.zeros(1)
+    err = C.create_string_buffer(256)
+    rc = lib.orc_total_yield(C.byref(inp.params), C.byref(inp.setup), C.byref(inp.surf), _p(pl), float(y_cut),
+                             _p(nt), _p(dens), err, 256)
+    if rc:
+        raise RuntimeError("oracle: " + err.value.decode())
+    return float(nt[0]), dens.reshape(3, npart)

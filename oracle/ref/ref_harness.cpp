@@ -14,6 +14,8 @@
 //   ref_harness gauss <file>       -> GaussThermal integrals for stdin lines "kind mbar alphaB baryon sign"
 //   ref_harness gaussmod <file>    -> Gauss1D_mod for stdin lines "kind mbar lambda sign"
 //   ref_harness lrf                -> Milne basis + pi LRF + V LRF for stdin lines of 19 numbers
+//   ref_harness dslrf              -> Surface_Element_Vector LRF boost + magnitude for stdin lines
+//                                     "ut ux uy un tau dat dax day dan"
 //   ref_harness table <file>       -> Table dimensions and contents
 //   ref_harness params <file> k... -> ParameterReader::getVal for each key
 #include <cstdio>
@@ -99,6 +101,23 @@ static void lrf() {
   }
 }
 
+// stdin: ut ux uy un tau dat dax day dan
+static void dslrf() {
+  double v[9];
+  while (true) {
+    for (int i = 0; i < 9; i++) if (scanf("%lf", &v[i]) != 1) return;
+    double ut = v[0], ux = v[1], uy = v[2], un = v[3], tau = v[4];
+    double uperp = sqrt(ux * ux + uy * uy), utperp = sqrt(1.0 + ux * ux + uy * uy);
+    Milne_Basis b(ut, ux, uy, un, uperp, utperp, tau);
+    Surface_Element_Vector ds(v[5], v[6], v[7], v[8]);
+    ds.boost_dsigma_to_lrf(b, ut, ux, uy, un);
+    ds.compute_dsigma_magnitude();
+    double o[] = {ds.dsigmat_LRF, ds.dsigmax_LRF, ds.dsigmay_LRF, ds.dsigmaz_LRF, ds.dsigma_space};
+    for (double x : o) printf("%.17g ", x);
+    printf("\n");
+  }
+}
+
 static void table(const char* file) {
   Table t(file);
   printf("%ld %ld\n", t.getNumberOfCols(), t.getNumberOfRows());
@@ -116,6 +135,7 @@ int main(int argc, char** argv) {
   else if (cmd == "gauss" && argc > 2) gauss(argv[2], false);
   else if (cmd == "gaussmod" && argc > 2) gauss(argv[2], true);
   else if (cmd == "lrf") lrf();
+  else if (cmd == "dslrf") dslrf();
   else if (cmd == "table" && argc > 2) table(argv[2]);
   else if (cmd == "params" && argc > 2) {
     ParameterReader pr;

@@ -16,6 +16,48 @@
 
 using namespace is3d;
 
+// delta-f tables and prepass constants on the host (as finalize_tables / make_consts)
+struct EmuTables {
+  DfTables tb{};
+  PrepConsts k{};
+  std::vector<std::vector<double>> sy, sc;
+  std::vector<double> jl2, jz, jx, jl2c, jzc;
+  EmuTables(const orc_params* p, const orc_setup* su, int op) : sy(NSPL), sc(NSPL) {
+    const int mode = p->df_mode, dim = p->dimension;
+    tb.df_mode = mode; tb.include_baryon = p->include_baryon;
+    tb.nT = su->nT; tb.nmuB = p->include_baryon ? su->nmuB : 1;
+    tb.T = su->Tarr; tb.muB = su->muBarr; tb.tab = su->dftab;
+    tb.T_min = su->Tarr[0]; tb.muB_min = su->muBarr[0];
+    tb.dT = fabs(su->Tarr[1] - su->Tarr[0]);
+    tb.dmuB = su->nmuB > 1 ? fabs(su->muBarr[1] - su->muBarr[0]) : 0.0;
+    const int col[NSPL] = {0, 2, 3, 5, 7, 8, 9};
+    if (!p->include_baryon) {
+      for (int i = 0; i < NSPL; i++) {
+        const double* yv = su->dftab + (size_t)col[i] * su->nmuB * su->nT;
+        sy[i].assign(yv, yv + su->nT);
+        cspline_coeffs(su->Tarr, yv, su->nT, sc[i]);
+        tb.sy[i] = sy[i].data(); tb.sc[i] = sc[i].data();
+      }
+    }
+    double bpmax = -1.0;
+    if (!p->include_baryon && mode == PTB) {
+      jonah_table(su->T_avg, su->npdg, su->pdg_mass, su->pdg_degen, su->pdg_sign, su->gla_root + 2 * su->gla_points,
+                  su->gla_weight + 2 * su->gla_points, su->gla_points, jl2, jz, jx, bpmax);
+      cspline_coeffs(jx.data(), jl2.data(), 301, jl2c);
+      cspline_coeffs(jx.data(), jz.data(), 301, jzc);
+      tb.nj = 301; tb.jx = jx.data(); tb.jl2 = jl2.data(); tb.jl2c = jl2c.data(); tb.jz = jz.data(); tb.jzc = jzc.data();
+    }
+    tb.bulk_over_P_max = bpmax;
+    k.operation = op;
+    k.df_mode = mode; k.dim = dim; k.include_baryon = p->include_baryon; k.include_bulk = p->include_bulk_deltaf;
+    k.include_shear = p->include_shear_deltaf; k.include_diff = p->include_baryondiff_deltaf;
+    k.deta_min = p->deta_min; k.mass_pion0 = p->mass_pion0; k.gla_pts = su->gla_points;
+    k.gla_r1 = su->gla_root + su->gla_points; k.gla_r2 = su->gla_root + 2 * su->gla_points;
+    k.gla_w1 = su->gla_weight + su->gla_points; k.gla_w2 = su->gla_weight + 2 * su->gla_points;
+    k.two_pi2_hbarC3 = 2.0 * pow(M_PI, 2) * pow(kHbarC, 3);
+  }
+};
+
 // op = 1: out = dN/(pT dpT dphi dy)[species][pT][phi][y];  op = 0: out = dN_dy_cell[species][cell]
 // (sum over pT, phi, y of w_pT w_phi (w_eta p.dsigma f) x prefactor g, as k_dndx)
 extern "C" int emu_spectra(const orc_params* p, const orc_setup* su, const orc_surface* S, int chains, int op,
@@ -24,42 +66,9 @@ extern "C" int emu_spectra(const orc_params* p, const orc_setup* su, const orc_s
   const long n = S->n;
   const int np = su->npart, npT = su->npT, nphi = su->nphi;
   const int ny_out = (dim == 3) ? su->ny : 1, nk = ny_out, nl = (dim == 3) ? 1 : su->neta;
-  // --- tables (as finalize_tables)
-  DfTables tb{};
-  tb.df_mode = mode; tb.include_baryon = p->include_baryon;
-  tb.nT = su->nT; tb.nmuB = p->include_baryon ? su->nmuB : 1;
-  tb.T = su->Tarr; tb.muB = su->muBarr; tb.tab = su->dftab;
-  tb.T_min = su->Tarr[0]; tb.muB_min = su->muBarr[0];
-  tb.dT = fabs(su->Tarr[1] - su->Tarr[0]);
-  tb.dmuB = su->nmuB > 1 ? fabs(su->muBarr[1] - su->muBarr[0]) : 0.0;
-  std::vector<std::vector<double>> sy(NSPL), sc(NSPL);
-  const int col[NSPL] = {0, 2, 3, 5, 7, 8, 9};
-  if (!p->include_baryon) {
-    for (int k = 0; k < NSPL; k++) {
-      const double* yv = su->dftab + (size_t)col[k] * su->nmuB * su->nT;
-      sy[k].assign(yv, yv + su->nT);
-      cspline_coeffs(su->Tarr, yv, su->nT, sc[k]);
-      tb.sy[k] = sy[k].data(); tb.sc[k] = sc[k].data();
-    }
-  }
-  std::vector<double> jl2, jz, jx, jl2c, jzc;
-  double bpmax = -1.0;
-  if (!p->include_baryon && mode == PTB) {
-    jonah_table(su->T_avg, su->npdg, su->pdg_mass, su->pdg_degen, su->pdg_sign, su->gla_root + 2 * su->gla_points,
-                su->gla_weight + 2 * su->gla_points, su->gla_points, jl2, jz, jx, bpmax);
-    cspline_coeffs(jx.data(), jl2.data(), 301, jl2c);
-    cspline_coeffs(jx.data(), jz.data(), 301, jzc);
-    tb.nj = 301; tb.jx = jx.data(); tb.jl2 = jl2.data(); tb.jl2c = jl2c.data(); tb.jz = jz.data(); tb.jzc = jzc.data();
-  }
-  tb.bulk_over_P_max = bpmax;
-  PrepConsts k{};
-  k.operation = op;
-  k.df_mode = mode; k.dim = dim; k.include_baryon = p->include_baryon; k.include_bulk = p->include_bulk_deltaf;
-  k.include_shear = p->include_shear_deltaf; k.include_diff = p->include_baryondiff_deltaf;
-  k.deta_min = p->deta_min; k.mass_pion0 = p->mass_pion0; k.gla_pts = su->gla_points;
-  k.gla_r1 = su->gla_root + su->gla_points; k.gla_r2 = su->gla_root + 2 * su->gla_points;
-  k.gla_w1 = su->gla_weight + su->gla_points; k.gla_w2 = su->gla_weight + 2 * su->gla_points;
-  k.two_pi2_hbarC3 = 2.0 * pow(M_PI, 2) * pow(kHbarC, 3);
+  EmuTables et(p, su, op);
+  const DfTables& tb = et.tb;
+  const PrepConsts& k = et.k;
   // --- prepass
   std::vector<double> rec((size_t)n * NREC), aux((size_t)n * 9), sol((size_t)n * 6);
   const double* fields[NSURF] = {S->tau, S->x, S->y, S->eta, S->dat, S->dax, S->day, S->dan, S->ux, S->uy, S->un,
@@ -209,4 +218,48 @@ extern "C" int emu_spectra(const orc_params* p, const orc_setup* su, const orc_s
 extern "C" void emu_exp(const double* x, long n, double* out) {
   const ExpCoef E = exp_coef();
   for (long i = 0; i < n; i++) out[i] = exp_clamped(E, x[i]);
+}
+
+// operation 2 yield estimate with the device math (k_densities + k_yield, sequential sums)
+extern "C" int emu_total_yield(const orc_params* p, const orc_setup* su, const orc_surface* S, const double* plasma,
+                               double y_cut, double* n_total, double* dens) {
+  EmuTables et(p, su, 1);
+  const int np = su->npart, pts = su->gla_points;
+  DfCoef df;
+  int err = df_eval(et.tb, plasma[0], plasma[3], plasma[1], plasma[2], 0.0, df);
+  if (err) return 100 + err;
+  static const int kAlpha[6] = {1, 1, 1, 2, 3, 3};
+  double dsum[3] = {0, 0, 0};
+  for (int s = 0; s < np; s++) {
+    const double T = plasma[0], mbar = su->mass[s] / T, chem = su->baryon[s] * (plasma[3] / T);
+    double J[6];
+    for (int q = 0; q < 6; q++) {
+      double v = 0.0;
+      for (int i = 0; i < pts; i++) {
+        const long o = (long)kAlpha[q] * pts + i;
+        v += su->gla_weight[o] * gt_term(q, su->gla_root[o], mbar, chem, su->sign[s]);
+      }
+      J[q] = v;
+    }
+    double d3[3];
+    species_densities(p->df_mode, df, T, plasma[4] / (plasma[1] + plasma[2]), su->mass[s], su->degen[s], su->baryon[s],
+                      J, et.k.two_pi2_hbarC3, d3);
+    for (int i = 0; i < 3; i++) { dens[(long)i * np + s] = d3[i]; }
+  }
+  for (int i = 0; i < 3; i++) for (int s = 0; s < np; s++) dsum[i] += dens[(long)i * np + s];
+  const double* fields[NSURF] = {S->tau, S->x, S->y, S->eta, S->dat, S->dax, S->day, S->dan, S->ux, S->uy, S->un,
+                                 S->E, S->T, S->P, S->pixx, S->pixy, S->pixn, S->piyy, S->piyn, S->bulkPi,
+                                 S->muB, S->nB, S->Vx, S->Vy, S->Vn};
+  double Ntot = 0.0;
+  for (long c = 0; c < S->n; c++) {
+    double sv[NSURF];
+    for (int f = 0; f < NSURF; f++) sv[f] = fields[f] ? fields[f][c] : 0.0;
+    double v;
+    err = yield_cell(et.k, et.tb, sv, dsum, &v);
+    if (err) return 100 + err;
+    Ntot += v;
+  }
+  if (p->dimension == 2) Ntot *= 2.0 * y_cut;
+  *n_total = Ntot;
+  return 0;
 }

@@ -24,4 +24,4 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version():
     lib = _lib.load()
-    assert lib.is3d_abi_version() == 2
+    assert lib.is3d_abi_version() == 3

@@ -129,3 +129,24 @@ def test_dropin_spacetime_workflow_matches_oracle(tmp_path, dim, mode, threads):
         np.testing.assert_allclose(rows[:, 1], r[k], rtol=1e-6, atol=1e-300)
     host.run_particlization(d, len(ref))            # the reference opens the files in append mode
     assert np.loadtxt(os.path.join(d, "results/continuous/dN_taudtaudy_%d.dat" % mc)).shape == (120, 2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dim,mode,oversample", [(2, 2, 1), (3, 1, 1), (2, 4, 1), (2, 2, 0)])
+def test_dropin_oversampling_estimate_matches_oracle(tmp_path, dim, mode, oversample):
+    # operation = 2: Ntotal (ParticleSampler.cpp:447-636) and Nevents (EmissionFunction.cpp:1237-1249)
+    s = synth.surface(400, seed=43, dimension=dim, full3d=(dim == 3))
+    params = dict(operation=2, dimension=dim, df_mode=mode, include_baryon=0, include_bulk_deltaf=1,
+                  include_shear_deltaf=1, include_baryondiff_deltaf=0, regulate_deltaf=0, outflow=0, deta_min=1e-5,
+                  mass_pion0=0.138, oversample=oversample, min_num_hadrons=1.0e7, max_num_samples=1.0e4, y_cut=0.75)
+    d = rundir.write_run_dir(str(tmp_path), s, params, hrg_eos=2, chosen="smash", surface_format=1)
+    spec = make_spec(hrg_eos=2, chosen="smash", **{k: v for k, v in params.items() if k != "operation"})
+    fields, avg = host.read_surface(d, 1, dim, 0)
+    surf = {k: fields[i] for i, k in enumerate(synth.FIELDS)}
+    ntot, nev = host.total_yield(d)
+    if not oversample:
+        assert (ntot, nev) == (0.0, 1)
+        return
+    ref, _ = O.total_yield(spec, surf, avg, y_cut=0.75)
+    assert abs(ntot - ref) <= 1e-12 * abs(ref)
+    assert nev == int(min(np.ceil(1.0e7 / ref), 1.0e4))
