@@ -93,6 +93,7 @@ def main():
     ap.add_argument("--config", default="config2", choices=sorted(CONFIGS))
     ap.add_argument("--df-mode", type=int, default=0)
     ap.add_argument("--cells", type=int, default=0, help="override cells per GPU (weak) / total (strong)")
+    ap.add_argument("--chosen", default="", help="override the chosen-species list (pikp, smash, urqmd)")
     ap.add_argument("--operation", type=int, default=1, choices=[0, 1],
                     help="1 continuous spectra (default, the BASELINE metric); 0 spacetime distributions dN/dX")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -115,6 +116,8 @@ def main():
     cfg = dict(CONFIGS[args.config])
     if args.cells:
         cfg["cells"] = args.cells
+    if args.chosen:
+        cfg["chosen"] = args.chosen
     mode = args.df_mode or cfg["mode"]
     flags = dict(cfg["flags"])
     if mode == 4:

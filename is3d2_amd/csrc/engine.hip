@@ -34,7 +34,7 @@ using namespace is3d;
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kJmax = 32;     // phi accumulators per lane
+constexpr int kJmax = 32;     // phi accumulators per lane (k_dndx; k_spectra picks KJ per grid, spectra_kj)
 #ifndef IS3D_KTILE
 #define IS3D_KTILE 8
 #endif
@@ -192,10 +192,10 @@ struct SpecArgs {
   const double *smass, *ssign, *sbaryon; const int* sorig;
   const double *pT, *cphi, *sphi, *yv, *etav, *etaw;
   int npart, npT, nphi, ny_out, nk, nl, nq, njb;
-  long ntask;
+  long ntask;                 // npart * nq * njb lanes per pT: (species, q = y x eta node, phi block)
   long cells_per_split;
   int nbx, nsplit;            // lane groups per pT, cell splits (1-D grid of nbx * npT * nsplit)
-  long sstride;               // doubles per slab: npT * nbx * kJmax * kBlock
+  long sstride;               // doubles per slab: npT * nbx * KJ * kBlock
   int regulate, outflow, dim;
   int op;                     // 1 spectra / 0 spacetime (yterms variants)
 };
@@ -209,16 +209,16 @@ constexpr int F_REG = 1, F_OUT = 2;
 
 // 32 phi points of one lane; the next points' LDS pairs are loaded before the current ones are
 // evaluated so the LDS latency overlaps the FP64 chain
-template <int MODE, int FLAGS, bool FAST>
+template <int MODE, int FLAGS, bool FAST, int KJ>
 __device__ __forceinline__ void sep_phi_loop(const SepLane& L, const dbl2* CS, const dbl2* BP, double* acc) {
   constexpr int FL = (MODE == GRAD) ? SEP_GRAD : (MODE == CE || MODE == PTM) ? SEP_CE : (MODE == PTB) ? SEP_PTB : SEP_FEQ;
   constexpr bool REG = (FLAGS & F_REG) != 0, OUT = (FLAGS & F_OUT) != 0;
   if (FAST && IS3D_PAIR_RCP) {
     dbl2 c0 = CS[0], b0 = BP[0], c1 = CS[1], b1 = BP[1];
 #pragma unroll
-    for (int jj = 0; jj < kJmax; jj += 2) {   // phi rows are padded to a multiple of kJmax
+    for (int jj = 0; jj < KJ; jj += 2) {   // phi rows are padded to a multiple of KJ
       dbl2 n0 = c0, m0 = b0, n1 = c1, m1 = b1;
-      if (jj + 2 < kJmax) { n0 = CS[jj + 2]; m0 = BP[jj + 2]; n1 = CS[jj + 3]; m1 = BP[jj + 3]; }
+      if (jj + 2 < KJ) { n0 = CS[jj + 2]; m0 = BP[jj + 2]; n1 = CS[jj + 3]; m1 = BP[jj + 3]; }
       double v0, v1;
       sep_pair_t<FL, REG, OUT>(L, c0, b0, c1, b1, v0, v1);
       acc[jj] += v0; acc[jj + 1] += v1;
@@ -228,22 +228,22 @@ __device__ __forceinline__ void sep_phi_loop(const SepLane& L, const dbl2* CS, c
   }
   dbl2 c = CS[0], b = BP[0];
 #pragma unroll
-  for (int jj = 0; jj < kJmax; jj++) {
+  for (int jj = 0; jj < KJ; jj++) {
     dbl2 cn = c, bn = b;
-    if (jj + 1 < kJmax) { cn = CS[jj + 1]; bn = BP[jj + 1]; }
+    if (jj + 1 < KJ) { cn = CS[jj + 1]; bn = BP[jj + 1]; }
     acc[jj] += sep_point_t<FL, REG, OUT, FAST>(L, c, b);
     c = cn; b = bn;
   }
 }
 
-template <int FLAGS, bool CLAMP>
+template <int FLAGS, bool CLAMP, int KJ>
 __device__ __forceinline__ void mod_phi_loop(const ModLane& M, const dbl2* CS, const dbl2* QV, double* acc) {
   constexpr bool OUT = (FLAGS & F_OUT) != 0;
   dbl2 c0 = CS[0], c1 = CS[1], q = QV[0];
 #pragma unroll
-  for (int jj = 0; jj < kJmax; jj += 2) {
+  for (int jj = 0; jj < KJ; jj += 2) {
     dbl2 n0 = c0, n1 = c1, nq = q;
-    if (jj + 2 < kJmax) { n0 = CS[jj + 2]; n1 = CS[jj + 3]; nq = QV[(jj >> 1) + 1]; }
+    if (jj + 2 < KJ) { n0 = CS[jj + 2]; n1 = CS[jj + 3]; nq = QV[(jj >> 1) + 1]; }
     double v0, v1;
     mod_pair_t<OUT, CLAMP>(M, c0, c1, q, v0, v1);
     acc[jj] += v0; acc[jj + 1] += v1;
@@ -281,10 +281,13 @@ __device__ __forceinline__ void fetch_tile(const double* rec, long cb, long c_en
 
 __device__ __forceinline__ void wait_fetch() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-template <int MODE, int FLAGS>
+// KJ = phi points per lane (an even divisor-friendly block: 32, 24, 8 or 2, spectra_kj); a lane owns one
+// (species, q, phi block) with q = (y, eta node): in 2+1D the eta nodes are spread over lanes and
+// summed by k_reduce, so a few species still fill the wavefronts
+template <int MODE, int FLAGS, int KJ>
 __global__ __launch_bounds__(kBlock, MODE >= PTM ? IS3D_SPECTRA_WAVES_MOD : IS3D_SPECTRA_WAVES_SEP) void k_spectra(SpecArgs A) {
   extern __shared__ double smem[];
-  const int nphp = A.njb * kJmax;                         // phi rows padded to kJmax multiples
+  const int nphp = A.njb * KJ;                            // phi rows padded to KJ multiples
   double* s_recb = smem;                                  // [2][kTile][NREC] double-buffered
   dbl2* s_trig = (dbl2*)(s_recb + 2 * kTile * NREC);      // [nphp]        {cos, sin}
   dbl2* s_cs = s_trig + nphp;                             // [nphp]        {pT cos, pT sin}
@@ -306,14 +309,14 @@ __global__ __launch_bounds__(kBlock, MODE >= PTM ? IS3D_SPECTRA_WAVES_MOD : IS3D
   const double pT = A.pT[ipt];
   const long task = (long)lane_group * kBlock + tid;
   const bool active = task < A.ntask;
-  int s = 0, k = 0, jb = 0;
+  int s = 0, q = 0, jb = 0;
   if (active) {
     s = (int)(task % A.npart);
     const long r = task / A.npart;
-    k = (int)(r % A.nk);
-    jb = (int)(r / A.nk);
+    q = (int)(r % A.nq);
+    jb = (int)(r / A.nq);
   }
-  const int j0 = jb * kJmax;
+  const int j0 = jb * KJ;
   const double mass = A.smass[s], m2 = mass * mass, sign = A.ssign[s], baryon = A.sbaryon[s];
   const double mT = sqrt(m2 + pT * pT), mT2 = mT * mT, mTb = mT * baryon;
 
@@ -333,9 +336,9 @@ __global__ __launch_bounds__(kBlock, MODE >= PTM ? IS3D_SPECTRA_WAVES_MOD : IS3D
     s_grid[A.nk + A.nl + i] = (A.dim == 3) ? 1.0 : A.etaw[i];
   }
 
-  double acc[kJmax];
+  double acc[KJ];
 #pragma unroll
-  for (int jj = 0; jj < kJmax; jj++) acc[jj] = 0.0;
+  for (int jj = 0; jj < KJ; jj++) acc[jj] = 0.0;
 
   const long c_begin = (long)split * A.cells_per_split;
   const long c_end = min(A.n, c_begin + A.cells_per_split);
@@ -386,61 +389,66 @@ __global__ __launch_bounds__(kBlock, MODE >= PTM ? IS3D_SPECTRA_WAVES_MOD : IS3D
           rn_abs = fabs(rn);
         }
         const dbl2* BP = s_bp + t * nphp + j0;
-        for (int l = 0; l < A.nl; l++) {
-          const int q = k * A.nl + l;
-          const double* Y = s_y + ((long)t * A.nq + q) * kYRow;
-          const bool sep = (MODE <= CE) || kind == 1.0 || Y[Y_NARROW] != 0.0;
-          if (sep) {
-            SepLane L;
-            sep_setup(sep_flavor(MODE), R, Y, mT, mT2, m2, mTb, pT, sign, baryon, L);
-            if (L.skip) continue;
-            if (L.fast) sep_phi_loop<MODE, FLAGS, true>(L, s_cs + j0, BP, acc);
-            else sep_phi_loop<MODE, FLAGS, false>(L, s_cs + j0, BP, acc);
-          } else if (MODE >= PTM) {
-            ModLane M;
-            mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, M);
-            if (M.skip) continue;
-            const dbl2* QV = (const dbl2*)(s_qv + t * nphp + j0);
-            if (M.clamp) mod_phi_loop<FLAGS, true>(M, s_cs + j0, QV, acc);
-            else mod_phi_loop<FLAGS, false>(M, s_cs + j0, QV, acc);
-          }
+        const double* Y = s_y + ((long)t * A.nq + q) * kYRow;
+        const bool sep = (MODE <= CE) || kind == 1.0 || Y[Y_NARROW] != 0.0;
+        if (sep) {
+          SepLane L;
+          sep_setup(sep_flavor(MODE), R, Y, mT, mT2, m2, mTb, pT, sign, baryon, L);
+          if (L.skip) continue;
+          if (L.fast) sep_phi_loop<MODE, FLAGS, true, KJ>(L, s_cs + j0, BP, acc);
+          else sep_phi_loop<MODE, FLAGS, false, KJ>(L, s_cs + j0, BP, acc);
+        } else if (MODE >= PTM) {
+          ModLane M;
+          mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, M);
+          if (M.skip) continue;
+          const dbl2* QV = (const dbl2*)(s_qv + t * nphp + j0);
+          if (M.clamp) mod_phi_loop<FLAGS, true, KJ>(M, s_cs + j0, QV, acc);
+          else mod_phi_loop<FLAGS, false, KJ>(M, s_cs + j0, QV, acc);
         }
       }
     }
   }
-  if (active) {
-  }
   // partial sums, slab layout [split][pT][lane group][phi slot][lane]: every store of the wave is
   // one contiguous 512-byte row; non-temporal so the stream does not evict the cell records the
   // XCD's other workgroups are still reading from L2.  k_reduce scatters into the reference layout.
-  double* out = A.slab + (long)split * A.sstride + ((long)ipt * A.nbx + lane_group) * (kJmax * kBlock) + tid;
+  double* out = A.slab + (long)split * A.sstride + ((long)ipt * A.nbx + lane_group) * (KJ * kBlock) + tid;
 #pragma unroll
-  for (int jj = 0; jj < kJmax; jj++) __builtin_nontemporal_store(acc[jj], out + jj * kBlock);
+  for (int jj = 0; jj < KJ; jj++) __builtin_nontemporal_store(acc[jj], out + jj * kBlock);
 }
 
 struct ReduceArgs {
   const double* slab; long sstride; int nsplit;
-  int nbx, npart, npT, nphi, nk, ny_out; long ntask;
+  int nbx, npart, npT, nphi, nk, nl, ny_out, kj; long ntask;
   const int* sorig; const double* degen_orig; double prefactor;
   double* out;
 };
 
-// dN[s][pT][phi][y] = (2 pi hbarc)^-3 g_s * sum over cell splits, in fixed split order
+// dN[s][pT][phi][y] = (2 pi hbarc)^-3 g_s * sum over eta nodes (2+1D) and cell splits, in fixed order.
+// One thread per slab entry of an l = 0 lane; the lanes of the other eta nodes of the same (species, y,
+// phi block) are task + l * npart.
 __global__ __launch_bounds__(256) void k_reduce(ReduceArgs A) {
   const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= A.sstride) return;
+  const int KJ = A.kj;
   const int lane = (int)(e % kBlock);
-  const int jj = (int)((e / kBlock) % kJmax);
-  const long rest = e / ((long)kBlock * kJmax);
+  const int jj = (int)((e / kBlock) % KJ);
+  const long rest = e / ((long)kBlock * KJ);
   const int lane_group = (int)(rest % A.nbx), ipt = (int)(rest / A.nbx);
   const long task = (long)lane_group * kBlock + lane;
   if (task >= A.ntask) return;
   const int s = (int)(task % A.npart);
   const long r = task / A.npart;
-  const int k = (int)(r % A.nk), j = (int)(r / A.nk) * kJmax + jj;
+  const long nq = (long)A.nk * A.nl;
+  const int q = (int)(r % nq);
+  if (q % A.nl != 0) return;
+  const int k = q / A.nl, j = (int)(r / nq) * KJ + jj;
   if (j >= A.nphi) return;
   double acc = 0.0;
-  for (int z = 0; z < A.nsplit; z++) acc += A.slab[(long)z * A.sstride + e];
+  for (int l = 0; l < A.nl; l++) {
+    const long tl = task + (long)l * A.npart;
+    const long el = ((long)ipt * A.nbx + tl / kBlock) * ((long)KJ * kBlock) + (long)jj * kBlock + tl % kBlock;
+    for (int z = 0; z < A.nsplit; z++) acc += A.slab[(long)z * A.sstride + el];
+  }
   const int so = A.sorig[s];
   A.out[(((long)so * A.npT + ipt) * A.nphi + j) * A.ny_out + k] = A.prefactor * A.degen_orig[so] * acc;
 }
@@ -1156,14 +1164,36 @@ static PrepConsts make_consts(const is3d_engine* e) {
   return k;
 }
 
-template <int MODE>
-static void launch_spectra(dim3 grid, size_t shmem, hipStream_t st, const SpecArgs& a, int flags) {
+template <int MODE, int KJ>
+static void launch_spectra_kj(dim3 grid, size_t shmem, hipStream_t st, const SpecArgs& a, int flags) {
   switch (flags) {
-    case 0: hipLaunchKernelGGL((k_spectra<MODE, 0>), grid, dim3(kBlock), shmem, st, a); break;
-    case 1: hipLaunchKernelGGL((k_spectra<MODE, 1>), grid, dim3(kBlock), shmem, st, a); break;
-    case 2: hipLaunchKernelGGL((k_spectra<MODE, 2>), grid, dim3(kBlock), shmem, st, a); break;
-    default: hipLaunchKernelGGL((k_spectra<MODE, 3>), grid, dim3(kBlock), shmem, st, a); break;
+    case 0: hipLaunchKernelGGL((k_spectra<MODE, 0, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+    case 1: hipLaunchKernelGGL((k_spectra<MODE, 1, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+    case 2: hipLaunchKernelGGL((k_spectra<MODE, 2, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+    default: hipLaunchKernelGGL((k_spectra<MODE, 3, KJ>), grid, dim3(kBlock), shmem, st, a); break;
   }
+}
+
+template <int MODE>
+static void launch_spectra(dim3 grid, size_t shmem, hipStream_t st, const SpecArgs& a, int flags, int kj) {
+  switch (kj) {
+    case 32: launch_spectra_kj<MODE, 32>(grid, shmem, st, a, flags); break;
+    case 24: launch_spectra_kj<MODE, 24>(grid, shmem, st, a, flags); break;
+    case 8: launch_spectra_kj<MODE, 8>(grid, shmem, st, a, flags); break;
+    default: launch_spectra_kj<MODE, 2>(grid, shmem, st, a, flags); break;
+  }
+}
+
+// phi points per lane: the block size among 32, 24, 8, 2 with the least padding of the phi grid (ties
+// to the larger block, whose per-lane setup is spread over more points): 1 -> 2, 24 / 48 -> 24, 32 -> 32
+static int spectra_kj(int nphi) {
+  int best = 32;
+  long best_pad = (long)((nphi + 31) / 32) * 32;
+  for (int kj : {24, 8, 2}) {
+    const long pad = (long)((nphi + kj - 1) / kj) * kj;
+    if (pad < best_pad) { best = kj; best_pad = pad; }
+  }
+  return best;
 }
 
 extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
@@ -1231,8 +1261,9 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   }
   HIPCHK(e, hipEventRecord(e->ev[1], st));
   // --- main integral
-  const int njb = (nphi + kJmax - 1) / kJmax;
-  const long ntask = (long)np * nk * njb;
+  const int KJ = spectra_kj(nphi);
+  const int njb = (nphi + KJ - 1) / KJ;
+  const long ntask = (long)np * nk * nl * njb;
   const long bx = (ntask + kBlock - 1) / kBlock;
   const long wgs = bx * npT;
   // cell splits: enough workgroups to fill the chip (>= 8k), and each split's records small enough
@@ -1247,7 +1278,7 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   long cps = (n + nsplit - 1) / nsplit;
   cps = ((cps + kTile - 1) / kTile) * kTile;
   nsplit = (n + cps - 1) / cps;
-  const long sstride = (long)npT * bx * kJmax * kBlock;
+  const long sstride = (long)npT * bx * KJ * kBlock;
   if (!ensure(e->d_slab, e->slab_cap, nsplit * sstride)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(slabs) failed");
   SpecArgs sa{};
   sa.rec = e->d_rec; sa.n = n; sa.renorm = e->d_renorm; sa.slab = e->d_slab; sa.outsize = outsize;
@@ -1256,24 +1287,25 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   sa.npart = np; sa.npT = npT; sa.nphi = nphi; sa.ny_out = ny_out; sa.nk = nk; sa.nl = nl; sa.nq = nk * nl; sa.njb = njb;
   sa.ntask = ntask; sa.cells_per_split = cps; sa.nbx = (int)bx; sa.nsplit = (int)nsplit; sa.sstride = sstride;
   sa.regulate = e->p.regulate_deltaf; sa.outflow = e->p.outflow; sa.dim = dim; sa.op = 1;
-  const size_t shmem = sizeof(double) * (2 * (size_t)kTile * NREC + 2 * (size_t)(kTile + 2) * njb * kJmax +
-                                         (size_t)kTile * njb * kJmax + (size_t)(nk + 2 * nl) +
+  const size_t shmem = sizeof(double) * (2 * (size_t)kTile * NREC + 2 * (size_t)(kTile + 2) * njb * KJ +
+                                         (size_t)kTile * njb * KJ + (size_t)(nk + 2 * nl) +
                                          (size_t)kTile * sa.nq * kYRow);
   if (shmem > 160 * 1024) return e->fail(IS3D_ERR_ARG, "momentum grid too large for the LDS tile");
   const dim3 grid((unsigned)(bx * npT * nsplit));
   const int kflags = (e->p.regulate_deltaf ? F_REG : 0) | (e->p.outflow ? F_OUT : 0);
   switch (mode) {
-    case GRAD: launch_spectra<GRAD>(grid, shmem, st, sa, kflags); break;
-    case CE: launch_spectra<CE>(grid, shmem, st, sa, kflags); break;
-    case PTM: launch_spectra<PTM>(grid, shmem, st, sa, kflags); break;
-    case PTB: launch_spectra<PTB>(grid, shmem, st, sa, kflags); break;
-    default: launch_spectra<PTMA>(grid, shmem, st, sa, kflags); break;
+    case GRAD: launch_spectra<GRAD>(grid, shmem, st, sa, kflags, KJ); break;
+    case CE: launch_spectra<CE>(grid, shmem, st, sa, kflags, KJ); break;
+    case PTM: launch_spectra<PTM>(grid, shmem, st, sa, kflags, KJ); break;
+    case PTB: launch_spectra<PTB>(grid, shmem, st, sa, kflags, KJ); break;
+    default: launch_spectra<PTMA>(grid, shmem, st, sa, kflags, KJ); break;
   }
   HIPCHK(e, hipGetLastError());
   HIPCHK(e, hipEventRecord(e->ev[2], st));
   ReduceArgs ra{};
   ra.slab = e->d_slab; ra.sstride = sstride; ra.nsplit = (int)nsplit;
-  ra.nbx = (int)bx; ra.npart = np; ra.npT = npT; ra.nphi = nphi; ra.nk = nk; ra.ny_out = ny_out; ra.ntask = ntask;
+  ra.nbx = (int)bx; ra.npart = np; ra.npT = npT; ra.nphi = nphi; ra.nk = nk; ra.nl = nl; ra.ny_out = ny_out; ra.kj = KJ;
+  ra.ntask = ntask;
   ra.sorig = e->d_sorig; ra.degen_orig = e->d_degen_orig; ra.prefactor = std::pow(2.0 * M_PI * kHbarC, -3);
   ra.out = dev_out;
   hipLaunchKernelGGL(k_reduce, dim3((unsigned)((sstride + 255) / 256)), dim3(256), 0, st, ra);

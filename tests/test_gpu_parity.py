@@ -159,3 +159,27 @@ def test_full_size_properties(mode):
     m = np.abs(full) > 1e-290          # below that, subnormal products round on an absolute grid
     assert np.array_equal(d[m], 2.0 * full[m])
     assert np.abs(d[~m] - 2.0 * full[~m]).max(initial=0.0) <= 1e-300
+
+
+@pytest.mark.parametrize("phi", ["phi_default", "phi24", "phi32", "phi48"])
+@pytest.mark.parametrize("dim,mode", [(2, 1), (3, 2), (2, 3), (3, 5)])
+def test_phi_grid_blocks(phi, dim, mode):
+    # every phi-block size k_spectra picks (1 -> 2, 24/48 -> 24, 32 -> 32 points per lane) and the
+    # reference's default 51-pt pT table; in 2+1D the eta nodes are spread over lanes
+    s = synth.as_read(synth.surface(120, seed=31, dimension=dim, full3d=(dim == 3)))
+    spec = make_spec(hrg_eos=2, chosen="pikp", df_mode=mode, dimension=dim, pT="pT_default", phi=phi, famod_chains=1)
+    ref = O.spectra(spec, s, threads=1)
+    got, _ = run_gpu(spec, s)
+    rel, zr, zg = parity(got, ref)
+    assert rel < TOL, (rel, zr, zg)
+    assert zr == zg
+
+
+@pytest.mark.parametrize("mode", [1, 4])
+def test_smash_2d_eta_lanes(mode):
+    # 2+1D with many species: the (species, eta node) lanes of one output span several lane groups
+    s = synth.as_read(synth.surface(40, seed=8))
+    spec = make_spec(hrg_eos=2, chosen="smash", df_mode=mode, dimension=2)
+    ref = O.spectra(spec, s, threads=8)
+    got, _ = run_gpu(spec, s)
+    assert parity(got, ref)[0] < TOL
