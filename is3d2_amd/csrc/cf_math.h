@@ -94,6 +94,59 @@ IS3D_HD double exp_poly1(const ExpCoef& E, double x) {
 
 IS3D_HD double exp_dom690(double x) { return exp_poly(exp_coef(), x); }
 
+// Table-driven exp for the per-point exponentials of the modified-momentum path, taking
+// xN = x 64/ln2 (the caller folds 64/ln2 into its coefficients): K = rint(xN) from the low word
+// of xN + 1.5 2^52, rs = xN - K (exact), e^x = 2^(K >> 6) 2^((K & 63)/64) e^(c rs) with c = ln2/64,
+// e^(c rs) - 1 = rs (a1 + rs (a2 + ... a5)) (Taylor; |c rs| <= ln2/128 leaves a 3.4e-17 truncation),
+// and T = 2^((K & 63)/64) correctly rounded from a 64-entry table the kernels keep in LDS:
+// 9 FP64 + 3 INT32 ops instead of exp_poly1's 15 FP64, ~1 ulp.  The error of xN itself
+// (~|x| 2e-16 absolute in x) is the same order as the rounding of the exponent argument that the
+// reference's own exp(E/T - chem) carries.  Valid for |xN| < 2^50; underflow / overflow via ldexp.
+// 2^(j/64), j = 0..63 (tools/gen_exp2_table.py)
+static constexpr double kExp2Tab64[64] = {
+    1.0, 1.0108892860517005, 1.0218971486541166, 1.0330248790212284,
+    1.0442737824274138, 1.0556451783605572, 1.0671404006768237, 1.0787607977571199,
+    1.0905077326652577, 1.102382583307841, 1.1143867425958924, 1.1265216186082418,
+    1.1387886347566916, 1.1511892299529827, 1.1637248587775775, 1.1763969916502812,
+    1.189207115002721, 1.202156731452703, 1.215247359980469, 1.22848053610687,
+    1.241857812073484, 1.255380757024691, 1.2690509571917332, 1.2828700160787783,
+    1.2968395546510096, 1.3109612115247644, 1.3252366431597413, 1.339667524053303,
+    1.3542555469368927, 1.3690024229745905, 1.383909881963832, 1.3989796725383112,
+    1.4142135623730951, 1.42961333839197, 1.4451808069770467, 1.460917794180647,
+    1.4768261459394993, 1.4929077282912648, 1.5091644275934228, 1.5255981507445384,
+    1.5422108254079407, 1.559004400237837, 1.5759808451078865, 1.593142151342267,
+    1.6104903319492543, 1.6280274218573478, 1.645755478153965, 1.6636765803267364,
+    1.681792830507429, 1.7001063537185235, 1.718619298122478, 1.7373338352737062,
+    1.7562521603732995, 1.7753764925265212, 1.7947090750031072, 1.8142521755003989,
+    1.8340080864093424, 1.8539791250833855, 1.8741676341103, 1.8945759815869656,
+    1.9152065613971474, 1.9360617934922943, 1.9571441241754002, 1.978456026387951,
+};
+// a_k = (ln2/64)^k / k!, k = 1..5
+static constexpr double kExpTabA[5] = {0.010830424696249145, 5.86490495505617e-05, 2.1173137155464776e-07, 5.732851688640402e-10, 1.2417843701716925e-12};
+static constexpr double kInvLn2x64 = 92.33248261689366;   // 64 / ln2
+
+struct ExpTabCoef { double shift, a[5]; };
+
+IS3D_HD ExpTabCoef exp_tab_coef() {
+  ExpTabCoef e;
+  e.shift = kconst(6755399441055744.0);                  // 1.5 * 2^52
+  for (int i = 0; i < 5; i++) e.a[i] = kconst(kExpTabA[i]);
+  return e;
+}
+
+IS3D_HD double exp_tab(const ExpTabCoef& E, const double* tab, double xN) {
+  const double t = xN + E.shift;
+  const double K = t - E.shift;
+  const double rs = xN - K;
+  const int ki = (int)(unsigned)__builtin_bit_cast(unsigned long long, t);
+  double q = fma(E.a[4], rs, E.a[3]);
+  q = fma(q, rs, E.a[2]);
+  q = fma(q, rs, E.a[1]);
+  q = fma(q, rs, E.a[0]);
+  const double T = tab[ki & 63];
+  return ldexp(fma(T, rs * q, T), ki >> 6);
+}
+
 // exp(x) for any x: clamped into [-746, 710] first; ldexp saturates to +inf above 709.78 (the
 // reference's exp overflow, after which 1/(inf + sign) = 0) and rounds to subnormal / zero below
 // -708.4
@@ -1057,8 +1110,10 @@ IS3D_HD double sqrt_nr(double v) {
 // where the reference's exp overflows to 1/inf = 0.  |renorm| is folded into p.dsigma.
 struct ModLane {
   double E0, Ec, Es, D0, Dc, Ds, invTm, chemm, sign;
-  ExpCoef ec;    // pinned once per lane setup, reused by every phi point
-  int skip, clamp;   // clamp: some point's exp argument may leave exp_poly's domain
+  double invTmN, chemmN;       // invTm, chemm x 64/ln2 (exp_tab's scaled argument)
+  ExpTabCoef et;               // pinned once per lane setup, reused by every phi point
+  const double* etab;          // 2^(j/64) table (LDS on the device)
+  int skip, clamp;   // clamp: some point's exp argument may leave exp_tab's domain (exp_clamped instead)
 };
 
 // Qv = |pc Vc + ps Vs|^2 for one (cell, phi)
@@ -1070,7 +1125,7 @@ IS3D_HD double modqv(const double* R, dbl2 cs) {
 }
 
 IS3D_HD void mod_setup(const double* R, const double* Y, double mT, double m2, double pT, double sign, double baryon,
-                       double renorm_abs, ModLane& L) {
+                       double renorm_abs, const double* etab, ModLane& L) {
   const double ux = Y[Y_MUX], uy = Y[Y_MUY], uz = Y[Y_MUZ];
   const double u2 = fma(ux, ux, fma(uy, uy, uz * uz));
   L.E0 = fma(mT * mT, u2, m2);
@@ -1080,7 +1135,9 @@ IS3D_HD void mod_setup(const double* R, const double* Y, double mT, double m2, d
   L.D0 = renorm_abs * (mT * Y[Y_MD]); L.Dc = renorm_abs * Y[Y_WDX]; L.Ds = renorm_abs * Y[Y_WDY];
   L.sign = sign;
   L.invTm = R[R_INVTM]; L.chemm = baryon * R[R_CHEMM];
-  L.ec = exp_coef();
+  L.invTmN = L.invTm * kInvLn2x64; L.chemmN = L.chemm * kInvLn2x64;
+  L.et = exp_tab_coef();
+  L.etab = etab;
   // | |mT U| - pT |V|max | <= |p_mod| <= |mT U| + pT |V|max: if even the smallest E_mod overflows
   // exp, every phi point is exactly 0; if the largest could push the exp argument out of
   // exp_poly's domain the lane takes the clamped exp
@@ -1096,8 +1153,8 @@ IS3D_HD void mod_setup(const double* R, const double* Y, double mT, double m2, d
 template <bool CLAMP>
 IS3D_HD double mod_en(const ModLane& L, dbl2 cs, double qv) {
   const double Emod = sqrt_nr(fma(L.Ec, cs.x, fma(L.Es, cs.y, L.E0 + qv)));
-  const double x = fma(-Emod, L.invTm, L.chemm);
-  return CLAMP ? exp_clamped(L.ec, x) : exp_poly1(L.ec, x);
+  if (CLAMP) return exp_clamped(exp_coef(), fma(-Emod, L.invTm, L.chemm));
+  return exp_tab(L.et, L.etab, fma(-Emod, L.invTmN, L.chemmN));
 }
 
 template <bool OUT, bool CLAMP>

@@ -40,13 +40,21 @@ constexpr int kJmax = 32;     // phi accumulators per lane (k_dndx; k_spectra pi
 #endif
 constexpr int kTile = IS3D_KTILE;   // cells per LDS tile
 // waves per SIMD the spectra kernel is register-allocated for (measured on MI355X, config2):
-// the separable modes run best at 3 (168 VGPRs), the modified-momentum modes at 2 (no spills)
+// Grad runs best at 3 (168 VGPRs), RTA-CE and the modified-momentum modes at 2 (no spills)
 #ifndef IS3D_SPECTRA_WAVES_SEP
 #define IS3D_SPECTRA_WAVES_SEP 3
 #endif
 #ifndef IS3D_SPECTRA_WAVES_MOD
 #define IS3D_SPECTRA_WAVES_MOD 2
 #endif
+#ifndef IS3D_SPECTRA_WAVES_CE
+#define IS3D_SPECTRA_WAVES_CE 2      // RTA-CE: 2 (no spills) beat 3 (53 spilled VGPRs) by 7% on MI355X (profiles/round1_r1n_ab_ce.log)
+#endif
+// waves per SIMD of one spectra / dN/dX instantiation
+template <int MODE>
+constexpr int spectra_waves() {
+  return MODE >= PTM ? IS3D_SPECTRA_WAVES_MOD : MODE == CE ? IS3D_SPECTRA_WAVES_CE : IS3D_SPECTRA_WAVES_SEP;
+}
 
 // LDS row stride of the y-terms (doubles): NYT + 1 is odd, so the 8-byte stores of one y-term field
 // by consecutive lanes (rows 136 B apart) spread over the 64 banks instead of hitting two of them
@@ -285,7 +293,7 @@ __device__ __forceinline__ void wait_fetch() { asm volatile("s_waitcnt vmcnt(0)"
 // (species, q, phi block) with q = (y, eta node): in 2+1D the eta nodes are spread over lanes and
 // summed by k_reduce, so a few species still fill the wavefronts
 template <int MODE, int FLAGS, int KJ>
-__global__ __launch_bounds__(kBlock, MODE >= PTM ? IS3D_SPECTRA_WAVES_MOD : IS3D_SPECTRA_WAVES_SEP) void k_spectra(SpecArgs A) {
+__global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_spectra(SpecArgs A) {
   extern __shared__ double smem[];
   const int nphp = A.njb * KJ;                            // phi rows padded to KJ multiples
   double* s_recb = smem;                                  // [2][kTile][NREC] double-buffered
@@ -295,8 +303,10 @@ __global__ __launch_bounds__(kBlock, MODE >= PTM ? IS3D_SPECTRA_WAVES_MOD : IS3D
   double* s_qv = (double*)(s_bp + kTile * nphp);         // [kTile][nphp]  Qv (modified path)
   double* s_grid = s_qv + kTile * nphp;                   // y[nk] | eta[nl] | eta_w[nl]
   double* s_y = s_grid + A.nk + 2 * A.nl;                 // [kTile][nq][kYRow]
+  double* s_etab = s_y + (long)kTile * A.nq * kYRow;      // [64] exp_tab's 2^(j/64)
 
   const int tid = threadIdx.x;
+  if (MODE >= PTM && tid < 64) s_etab[tid] = kExp2Tab64[tid];
   // XCD-aware block order (cdna_hip_programming.md T1): blocks that share an XCD (same
   // blockIdx % 8) take one contiguous range of logical ids, and logical ids run split-major, so
   // each XCD's L2 sees only its own cell splits (sized to fit) instead of every split
@@ -399,7 +409,7 @@ __global__ __launch_bounds__(kBlock, MODE >= PTM ? IS3D_SPECTRA_WAVES_MOD : IS3D
           else sep_phi_loop<MODE, FLAGS, false, KJ>(L, s_cs + j0, BP, acc);
         } else if (MODE >= PTM) {
           ModLane M;
-          mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, M);
+          mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, s_etab, M);
           if (M.skip) continue;
           const dbl2* QV = (const dbl2*)(s_qv + t * nphp + j0);
           if (M.clamp) mod_phi_loop<FLAGS, true, KJ>(M, s_cs + j0, QV, acc);
@@ -524,7 +534,7 @@ struct DndxArgs {
 // in LDS and every lane adds w_pT x sum_phi w_phi (point) into its column of s_red; after the pT loop a
 // species' slot columns are summed in slot order.  No atomics: bit-reproducible.
 template <int MODE, int FLAGS>
-__global__ __launch_bounds__(kBlock, MODE >= PTM ? IS3D_SPECTRA_WAVES_MOD : IS3D_SPECTRA_WAVES_SEP) void k_dndx(DndxArgs A) {
+__global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_dndx(DndxArgs A) {
   extern __shared__ double smem[];
   const int nphp = A.njb * kJmax;
   double* s_rec = smem;                                   // [kTile][NREC]
@@ -536,8 +546,10 @@ __global__ __launch_bounds__(kBlock, MODE >= PTM ? IS3D_SPECTRA_WAVES_MOD : IS3D
   double* s_red = s_qv + kTile * nphp;                    // [kTile][kBlock] per-lane cell sums
   double* s_grid = s_red + kTile * kBlock;                // y[nk] | eta[nl] | eta_w[nl]
   double* s_y = s_grid + A.nk + 2 * A.nl;                 // [kTile][nq][kYRow]
+  double* s_etab = s_y + (long)kTile * A.nq * kYRow;      // [64] exp_tab's 2^(j/64)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (MODE >= PTM && tid < 64) s_etab[tid] = kExp2Tab64[tid];
   const long nwg = (long)A.nbx * A.nchunk;
   const long bid = blockIdx.x, q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
   const long lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
@@ -634,7 +646,7 @@ __global__ __launch_bounds__(kBlock, MODE >= PTM ? IS3D_SPECTRA_WAVES_MOD : IS3D
                            : sep_phi_wsum<MODE, FLAGS, false>(L, s_cs + j0, BP, W);
           } else if (MODE >= PTM) {
             ModLane M;
-            mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, M);
+            mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, s_etab, M);
             if (M.skip) continue;
             const dbl2* QV = (const dbl2*)(s_qv + t * nphp + j0);
             cell += M.clamp ? mod_phi_wsum<FLAGS, true>(M, s_cs + j0, QV, W) : mod_phi_wsum<FLAGS, false>(M, s_cs + j0, QV, W);
@@ -1289,7 +1301,7 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   sa.regulate = e->p.regulate_deltaf; sa.outflow = e->p.outflow; sa.dim = dim; sa.op = 1;
   const size_t shmem = sizeof(double) * (2 * (size_t)kTile * NREC + 2 * (size_t)(kTile + 2) * njb * KJ +
                                          (size_t)kTile * njb * KJ + (size_t)(nk + 2 * nl) +
-                                         (size_t)kTile * sa.nq * kYRow);
+                                         (size_t)kTile * sa.nq * kYRow + 64);
   if (shmem > 160 * 1024) return e->fail(IS3D_ERR_ARG, "momentum grid too large for the LDS tile");
   const dim3 grid((unsigned)(bx * npT * nsplit));
   const int kflags = (e->p.regulate_deltaf ? F_REG : 0) | (e->p.outflow ? F_OUT : 0);
@@ -1438,7 +1450,7 @@ extern "C" int is3d_calculate_dN_dX(is3d_engine* e, double* dN_taudtaudy, double
     da.npart = np; da.npT = npT; da.nphi = nphi; da.nk = nk; da.nl = nl; da.nq = nk * nl; da.njb = njb; da.dim = dim;
     const size_t nphp = (size_t)njb * kJmax;
     const size_t shmem = sizeof(double) * ((size_t)kTile * NREC + 2 * nphp + 2 * nphp + nphp + 3 * (size_t)kTile * nphp +
-                                           (size_t)kTile * kBlock + (size_t)(nk + 2 * nl) + (size_t)kTile * da.nq * kYRow);
+                                           (size_t)kTile * kBlock + (size_t)(nk + 2 * nl) + (size_t)kTile * da.nq * kYRow + 64);
     if (shmem > 160 * 1024) return e->fail(IS3D_ERR_ARG, "momentum grid too large for the LDS tile");
     const long nwg = (long)da.nbx * da.nchunk;
     if (nwg > 0x7fffffffL) return e->fail(IS3D_ERR_ARG, "surface too large for one dN/dX launch");

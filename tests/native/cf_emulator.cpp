@@ -173,7 +173,7 @@ extern "C" int emu_spectra(const orc_params* p, const orc_setup* su, const orc_s
                 a[j] += sep_point(sep_flavor(mode), L, CS[j], BP[j], p->regulate_deltaf, p->outflow);
             } else {
               ModLane M;
-              mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, M);
+              mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, kExp2Tab64, M);
               if (M.skip) continue;
               int j = 0;
               for (; j + 1 < nphi; j += 2) {
@@ -218,6 +218,12 @@ extern "C" int emu_spectra(const orc_params* p, const orc_setup* su, const orc_s
 extern "C" void emu_exp(const double* x, long n, double* out) {
   const ExpCoef E = exp_coef();
   for (long i = 0; i < n; i++) out[i] = exp_clamped(E, x[i]);
+}
+
+// the modified path's table exp (exp_tab) on x: the caller's scaling x 64/ln2 included
+extern "C" void emu_exp_tab(const double* x, long n, double* out) {
+  const ExpTabCoef E = exp_tab_coef();
+  for (long i = 0; i < n; i++) out[i] = exp_tab(E, kExp2Tab64, x[i] * kInvLn2x64);
 }
 
 // operation 2 yield estimate with the device math (k_densities + k_yield, sequential sums)

@@ -67,3 +67,25 @@ def test_kernel_exp_accuracy():
     assert ulp.max() <= 2.0, ulp.max()
     assert np.isinf(out[x >= 709.79]).all()
     assert (out[x <= -746.0] == 0.0).all()
+
+
+def test_kernel_exp_tab_accuracy():
+    """exp_tab (cf_math.h, per-point exp of the modified-momentum path) against libm exp: the table /
+    polynomial part within 2 ulp, plus the rounding of the scaled argument x 64/ln2 (|x| 2.5e-16)."""
+    import ctypes as C
+    from helpers import emulator
+    lib = emulator()
+    rng = np.random.default_rng(4)
+    x = np.concatenate([rng.uniform(-700, 700, 200000), rng.uniform(-2, 2, 100000), rng.uniform(-1e6, -746, 1000),
+                        np.array([0.0, 1e-300, -1e-300, 690.0, -690.0, 700.0, -745.0])])
+    out = np.empty_like(x)
+    P = C.POINTER(C.c_double)
+    lib.emu_exp_tab(x.ctypes.data_as(P), C.c_long(len(x)), out.ctypes.data_as(P))
+    ref = np.exp(x)
+    norm = (ref > 1e-300) & np.isfinite(ref)
+    rel = np.abs(out[norm] - ref[norm]) / ref[norm]
+    bound = 2.0 * 2.0 ** -52 + np.abs(x[norm]) * 2.5e-16
+    assert (rel <= bound).all(), (rel / bound).max()
+    small = np.abs(x) <= 2
+    assert (np.abs(out[small] - ref[small]) <= 2 * np.spacing(ref[small])).all()
+    assert (out[x < -746.0] == 0.0).all()
