@@ -303,6 +303,55 @@ IS3D_HD int df_eval(const DfTables& t, double T, double muB, double E, double P,
 }
 
 // ---------------------------------------------------------------------------
+// PTB "Jonah" table (DeltafData.cpp:220-295 compute_jonah_coefficients): 301 lambda rows in
+// [-1, 2]; per row the HRG kinetic E, P at lambda = 0 and at lambda over the PDG (photon skipped).
+// Built on the device (k_jonah_terms / k_jonah_sum) and by the test emulator from these pieces;
+// no FMA contraction here, so the device table is bit-identical to the host's (and the reference
+// expression order is kept: lmin + i dl rounds the product first).
+// ---------------------------------------------------------------------------
+static constexpr int kJonahN = 301;
+
+IS3D_HD double jonah_lambda(int i) {
+#pragma clang fp contract(off)
+  const double lmin = -1.0, lmax = 2.0, dl = (lmax - lmin) / ((double)kJonahN - 1.0);
+  return lmin + (double)i * dl;
+}
+
+// E_mod_int (kind 0) / P_mod_int (kind 1) Gauss sums (GaussThermal.cpp:108-130)
+IS3D_HD double gauss1d_mod(int kind, const double* r, const double* w, int n, double mbar, double lambda, double sign) {
+#pragma clang fp contract(off)
+  const ExpCoef E = exp_coef();
+  double sum = 0.0;
+  for (int k = 0; k < n; k++) {
+    const double p = r[k], scale2 = (1.0 + lambda) * (1.0 + lambda), Eb = sqrt(p * p + mbar * mbar);
+    const double v = (kind == 0) ? sqrt(p * p * scale2 + mbar * mbar) * exp_clamped(E, p) / (exp_clamped(E, Eb) + sign)
+                                 : p * p * scale2 / sqrt(p * p * scale2 + mbar * mbar) * exp_clamped(E, p) / (exp_clamped(E, Eb) + sign);
+    sum += w[k] * v;
+  }
+  return sum;
+}
+
+// one hadron's terms of a row: g E_mod and g P_mod / 3 (0 for m = 0: the reference skips the photon)
+IS3D_HD void jonah_terms(double T, double mass, double degen, double sign, const double* r2, const double* w2, int pts,
+                         double lambda, double* em, double* pm) {
+#pragma clang fp contract(off)
+  if (mass == 0.0) { *em = 0.0; *pm = 0.0; return; }
+  const double mbar = mass / T;
+  *em = degen * gauss1d_mod(0, r2, w2, pts, mbar, lambda, sign);
+  *pm = (1.0 / 3.0) * degen * gauss1d_mod(1, r2, w2, pts, mbar, lambda, sign);
+}
+
+// row i from the hadron sums (E, P at lambda = 0; Em, Pm at lambda): lambda^2, z, bulkPi/P
+IS3D_HD void jonah_row(int i, double E, double P, double Em, double Pm, double* l2, double* z, double* bp) {
+#pragma clang fp contract(off)
+  const double lambda = jonah_lambda(i);
+  const double zz = E / Em;
+  l2[i] = lambda * lambda;
+  z[i] = zz;
+  bp[i] = (Pm / P) * zz - 1.0;
+}
+
+// ---------------------------------------------------------------------------
 // Gauss-Laguerre thermal integrals (GaussThermal.cpp:7-78)
 // ---------------------------------------------------------------------------
 IS3D_HD double gt_neq(const double* r, const double* w, int n, double mbar, double alphaB, double baryon, double sign) {

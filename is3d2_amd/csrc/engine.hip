@@ -797,6 +797,42 @@ __global__ __launch_bounds__(256) void k_yield(YieldArgs A) {
   if (tid == 0) A.partial[blockIdx.x] = red[0];
 }
 
+// ------------------------------------------------------------------------------------------
+// PTB "Jonah" table (DeltafData.cpp:220-295): thread (row, hadron) evaluates the two Gauss sums, one
+// thread per row then adds the hadrons in PDG order (the reference's order), so the table is
+// bit-reproducible; row kJonahN holds the lambda = 0 terms.
+// ------------------------------------------------------------------------------------------
+struct JonahArgs {
+  double T; int npdg, pts;
+  const double *mass, *degen, *sign, *r2, *w2;
+  double* terms;                  // [kJonahN + 1][2][npdg]
+  double *l2, *z, *bp;            // [kJonahN] each
+};
+
+__global__ __launch_bounds__(256) void k_jonah_terms(JonahArgs A) {
+  const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long)(kJonahN + 1) * A.npdg) return;
+  const int i = (int)(idx / A.npdg), n = (int)(idx % A.npdg);
+  const double lambda = (i < kJonahN) ? jonah_lambda(i) : 0.0;
+  double* t = A.terms + (long)i * 2 * A.npdg;
+  jonah_terms(A.T, A.mass[n], A.degen[n], A.sign[n], A.r2, A.w2, A.pts, lambda, t + n, t + A.npdg + n);
+}
+
+__global__ __launch_bounds__(64) void k_jonah_sum(JonahArgs A) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= kJonahN) return;
+  const double* e0 = A.terms + (long)kJonahN * 2 * A.npdg;
+  const double* p0 = e0 + A.npdg;
+  const double* em = A.terms + (long)i * 2 * A.npdg;
+  const double* pm = em + A.npdg;
+  double E = 0.0, P = 0.0, Em = 0.0, Pm = 0.0;
+  for (int n = 0; n < A.npdg; n++) {
+    if (A.mass[n] == 0.0) continue;
+    E += e0[n]; P += p0[n]; Em += em[n]; Pm += pm[n];
+  }
+  jonah_row(i, E, P, Em, Pm, A.l2, A.z, A.bp);
+}
+
 __global__ void k_df_eval(DfTables tb, double T, double muB, double E, double P, double bulkPi, double* out, int* err) {
   DfCoef df;
   *err = df_eval(tb, T, muB, E, P, bulkPi, df);
@@ -1008,6 +1044,44 @@ extern "C" int is3d_set_df_tables(is3d_engine* e, int nT, int nmuB, const double
 }
 
 // Build the derived tables (splines, Jonah) and upload everything read-only to HBM.
+// PTB Jonah table on the device (k_jonah_terms + k_jonah_sum) into e->jl2 / jz / jx / bp_max; the
+// host keeps only the two 301-point spline solves
+static int device_jonah_table(is3d_engine* e, const double* r2, const double* w2) {
+  const int npdg = (int)e->pdg_mass.size(), pts = e->gla_pts;
+  if (npdg == 0) return e->fail(IS3D_ERR_STATE, "PTB needs the PDG (is3d_set_pdg)");
+  std::vector<double> in;
+  in.insert(in.end(), e->pdg_mass.begin(), e->pdg_mass.end());
+  in.insert(in.end(), e->pdg_degen.begin(), e->pdg_degen.end());
+  in.insert(in.end(), e->pdg_sign.begin(), e->pdg_sign.end());
+  in.insert(in.end(), r2, r2 + pts);
+  in.insert(in.end(), w2, w2 + pts);
+  const size_t nterms = (size_t)(kJonahN + 1) * 2 * npdg, nout = 3 * (size_t)kJonahN;
+  double* d = dalloc<double>(in.size() + nterms + nout);
+  if (!d) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(Jonah table) failed");
+  JonahArgs ja{};
+  ja.T = e->T_avg; ja.npdg = npdg; ja.pts = pts;
+  ja.mass = d; ja.degen = d + npdg; ja.sign = d + 2 * npdg; ja.r2 = d + 3 * npdg; ja.w2 = d + 3 * npdg + pts;
+  ja.terms = d + in.size();
+  ja.l2 = ja.terms + nterms; ja.z = ja.l2 + kJonahN; ja.bp = ja.z + kJonahN;
+  std::vector<double> out(nout);
+  hipError_t er = hipMemcpy(d, in.data(), in.size() * sizeof(double), hipMemcpyHostToDevice);
+  if (er == hipSuccess) {
+    const long nthr = (long)(kJonahN + 1) * npdg;
+    hipLaunchKernelGGL(k_jonah_terms, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, 0, ja);
+    hipLaunchKernelGGL(k_jonah_sum, dim3((kJonahN + 63) / 64), dim3(64), 0, 0, ja);
+    er = hipGetLastError();
+  }
+  if (er == hipSuccess) er = hipMemcpy(out.data(), ja.l2, nout * sizeof(double), hipMemcpyDeviceToHost);
+  dfree(d);
+  if (er != hipSuccess) return e->fail(IS3D_ERR_DEVICE, std::string("Jonah table: ") + hipGetErrorString(er));
+  e->jl2.assign(out.begin(), out.begin() + kJonahN);
+  e->jz.assign(out.begin() + kJonahN, out.begin() + 2 * kJonahN);
+  e->jx.assign(out.begin() + 2 * kJonahN, out.end());
+  e->bp_max = -1.0;
+  for (int i = 0; i < kJonahN; i++) e->bp_max = std::fmax(e->bp_max, e->jx[i]);
+  return IS3D_OK;
+}
+
 static int finalize_tables(is3d_engine* e) {
   if (!e->have_params) return e->fail(IS3D_ERR_STATE, "is3d_set_params not called");
   if (!e->have_species) return e->fail(IS3D_ERR_STATE, "is3d_set_species not called");
@@ -1043,8 +1117,8 @@ static int finalize_tables(is3d_engine* e) {
   if (!e->p.include_baryon && mode == PTB) {
     const double* r2 = e->gla_r.data() + 2 * e->gla_pts;
     const double* w2 = e->gla_w.data() + 2 * e->gla_pts;
-    jonah_table(e->T_avg, (int)e->pdg_mass.size(), e->pdg_mass.data(), e->pdg_degen.data(), e->pdg_sign.data(), r2, w2,
-                e->gla_pts, e->jl2, e->jz, e->jx, e->bp_max);
+    const int rc = device_jonah_table(e, r2, w2);
+    if (rc) return rc;
     if (!cspline_coeffs(e->jx.data(), e->jl2.data(), 301, e->jl2c) || !cspline_coeffs(e->jx.data(), e->jz.data(), 301, e->jzc))
       return e->fail(IS3D_ERR_DF_RANGE, "gsl: x values must be strictly increasing (Jonah bulkPi/P table)");
     nj = 301;

@@ -1,9 +1,11 @@
 // spline_host.h -- host-side construction of the natural cubic splines the
 // engine evaluates on the GPU (gsl_interp_cspline semantics, DeltafData.cpp:298-321
-// and :290-294), plus the PTB "Jonah" table (DeltafData.cpp:220-295).
+// and :290-294), plus a serial PTB "Jonah" table for the test emulator (DeltafData.cpp:220-295).
 #pragma once
 #include <cmath>
 #include <vector>
+
+#include "cf_math.h"
 
 namespace is3d {
 
@@ -39,49 +41,25 @@ inline bool cspline_coeffs(const double* x, const double* y, int n, std::vector<
   return true;
 }
 
-// E_mod_int / P_mod_int Gauss sums (GaussThermal.cpp:108-130)
-inline double gauss1d_mod(int kind, const double* r, const double* w, int n, double mbar, double lambda, double sign) {
-  double sum = 0.0;
-  for (int k = 0; k < n; k++) {
-    const double p = r[k], scale2 = (1.0 + lambda) * (1.0 + lambda), Eb = sqrt(p * p + mbar * mbar);
-    const double v = (kind == 0) ? sqrt(p * p * scale2 + mbar * mbar) * exp(p) / (exp(Eb) + sign)
-                                 : p * p * scale2 / sqrt(p * p * scale2 + mbar * mbar) * exp(p) / (exp(Eb) + sign);
-    sum += w[k] * v;
-  }
-  return sum;
-}
-
-// compute_jonah_coefficients: 301 lambda points in [-1, 2]; photon (m = 0) skipped.
+// compute_jonah_coefficients serially on the host (test emulator only; the engine builds the table
+// on the device from the same cf_math.h pieces, summing every row over the PDG in the same order)
 inline void jonah_table(double T, int npdg, const double* mass, const double* degen, const double* sign, const double* r2,
                         const double* w2, int pts, std::vector<double>& l2, std::vector<double>& z,
                         std::vector<double>& bp, double& bpmax) {
-  const int N = 301;
-  const double lmin = -1.0, lmax = 2.0, dl = (lmax - lmin) / ((double)N - 1.0);
-  l2.assign(N, 0.0); z.assign(N, 0.0); bp.assign(N, 0.0);
+  l2.assign(kJonahN, 0.0); z.assign(kJonahN, 0.0); bp.assign(kJonahN, 0.0);
   bpmax = -1.0;
-  // lambda-independent sums (the reference recomputes them identically for every lambda)
-  std::vector<double> e0(npdg, 0.0), p0(npdg, 0.0);
-  for (int n = 0; n < npdg; n++) {
-    if (mass[n] == 0.0) continue;
-    const double mbar = mass[n] / T;
-    e0[n] = degen[n] * gauss1d_mod(0, r2, w2, pts, mbar, 0.0, sign[n]);
-    p0[n] = (1.0 / 3.0) * degen[n] * gauss1d_mod(1, r2, w2, pts, mbar, 0.0, sign[n]);
-  }
-  for (int i = 0; i < N; i++) {
-    const double lambda = lmin + (double)i * dl;
+  std::vector<double> e0(npdg), p0(npdg);
+  for (int n = 0; n < npdg; n++) jonah_terms(T, mass[n], degen[n], sign[n], r2, w2, pts, 0.0, &e0[n], &p0[n]);
+  for (int i = 0; i < kJonahN; i++) {
     double E = 0.0, P = 0.0, Em = 0.0, Pm = 0.0;
     for (int n = 0; n < npdg; n++) {
-      const double g = degen[n], m = mass[n], sg = sign[n];
-      if (m == 0.0) continue;
-      const double mbar = m / T;
-      E += e0[n];
-      P += p0[n];
-      Em += g * gauss1d_mod(0, r2, w2, pts, mbar, lambda, sg);
-      Pm += (1.0 / 3.0) * g * gauss1d_mod(1, r2, w2, pts, mbar, lambda, sg);
+      if (mass[n] == 0.0) continue;
+      double em, pm;
+      jonah_terms(T, mass[n], degen[n], sign[n], r2, w2, pts, jonah_lambda(i), &em, &pm);
+      E += e0[n]; P += p0[n]; Em += em; Pm += pm;
     }
-    const double zz = E / Em, b = (Pm / P) * zz - 1.0;
-    l2[i] = lambda * lambda; z[i] = zz; bp[i] = b;
-    bpmax = std::fmax(bpmax, b);
+    jonah_row(i, E, P, Em, Pm, l2.data(), z.data(), bp.data());
+    bpmax = std::fmax(bpmax, bp[i]);
   }
 }
 

@@ -220,6 +220,14 @@ extern "C" void emu_exp(const double* x, long n, double* out) {
   for (long i = 0; i < n; i++) out[i] = exp_clamped(E, x[i]);
 }
 
+// PTB Jonah table from the cf_math.h pieces, serially (the device builds it in parallel, same order)
+extern "C" void emu_jonah_table(const orc_setup* su, double* l2, double* z, double* bp, double* bpmax) {
+  std::vector<double> a, b, c;
+  jonah_table(su->T_avg, su->npdg, su->pdg_mass, su->pdg_degen, su->pdg_sign, su->gla_root + 2 * su->gla_points,
+              su->gla_weight + 2 * su->gla_points, su->gla_points, a, b, c, *bpmax);
+  for (int i = 0; i < kJonahN; i++) { l2[i] = a[i]; z[i] = b[i]; bp[i] = c[i]; }
+}
+
 // the modified path's table exp (exp_tab) on x: the caller's scaling x 64/ln2 included
 extern "C" void emu_exp_tab(const double* x, long n, double* out) {
   const ExpTabCoef E = exp_tab_coef();

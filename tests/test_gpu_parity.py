@@ -110,10 +110,32 @@ def test_jonah_table_matches_oracle():
     e.calculate_spectra()
     l2, z, bp, mx = e.jonah_table()
     rc, l2r, zr, bpr, mxr = O.jonah_table(spec, surface_averages(s)[0])
+    # built on the device with the kernel exp (<= 2 ulp of glibc's)
     np.testing.assert_allclose(l2, l2r, rtol=0, atol=0)
-    np.testing.assert_allclose(z, zr, rtol=1e-15)
+    np.testing.assert_allclose(z, zr, rtol=1e-14)
     np.testing.assert_allclose(bp, bpr, rtol=1e-13, atol=1e-15)
     assert abs(mx - mxr) < 1e-14
+
+
+def test_jonah_table_device_matches_host_pieces():
+    # k_jonah_terms / k_jonah_sum against the same cf_math.h functions run serially on the host (same
+    # summation order, contraction off): bit for bit
+    import ctypes as C
+    from helpers import emulator
+    s = synth.as_read(synth.surface(200, seed=7))
+    spec = make_spec(hrg_eos=2, chosen="smash", df_mode=4)
+    T_avg = surface_averages(s)[0]
+    e = build_engine(spec, s, T_avg=T_avg)
+    e.calculate_spectra()
+    l2, z, bp, mx = e.jonah_table()
+    e.close()
+    inp = O._Inputs(spec, s, T_avg, 1)
+    h = [np.zeros(301) for _ in range(3)] + [np.zeros(1)]
+    emulator().emu_jonah_table(C.byref(inp.setup), *[O._p(a) for a in h])
+    np.testing.assert_array_equal(l2, h[0])
+    np.testing.assert_array_equal(z, h[1])
+    np.testing.assert_array_equal(bp, h[2])
+    assert mx == h[3][0]
 
 
 def _config2(mode=1, n=100000):
