@@ -106,8 +106,11 @@ def main():
 
     import torch
     import torch.distributed as dist
+    # rehearsal knobs for a 1-GPU box (never set by the driver): every rank on one device, gloo
+    backend = os.environ.get("IS3D_BENCH_BACKEND", "nccl")
+    local_rank = int(os.environ.get("IS3D_BENCH_DEVICE", local_rank))
     if world > 1:
-        dist.init_process_group("nccl", init_method="env://")
+        dist.init_process_group(backend, init_method="env://")
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
 
