@@ -134,7 +134,8 @@ IS3D_HD ExpTabCoef exp_tab_coef() {
   return e;
 }
 
-IS3D_HD double exp_tab(const ExpTabCoef& E, const double* tab, double xN) {
+// e^x 2^-kshift (exact shift, no intermediate overflow)
+IS3D_HD double exp_tab(const ExpTabCoef& E, const double* tab, double xN, int kshift = 0) {
   const double t = xN + E.shift;
   const double K = t - E.shift;
   const double rs = xN - K;
@@ -144,7 +145,29 @@ IS3D_HD double exp_tab(const ExpTabCoef& E, const double* tab, double xN) {
   q = fma(q, rs, E.a[1]);
   q = fma(q, rs, E.a[0]);
   const double T = tab[ki & 63];
-  return ldexp(fma(T, rs * q, T), ki >> 6);
+  return ldexp(fma(T, rs * q, T), (ki >> 6) - kshift);
+}
+
+// sinh and cosh of d for the y-terms: |d| < 0.5 by their Taylor series through d^17 / d^16 (truncation
+// < 5e-20 relative), otherwise from e = e^d and 1/e (e -/+ 1/e loses at most a factor coth(0.5) = 2.2 in
+// relative accuracy): ~25 VALU ops instead of the library's double-double sinh / cosh (~100 each)
+IS3D_HD void sinh_cosh(double d, double* sh, double* ch) {
+  if (fabs(d) < 0.5) {
+    const double d2 = d * d;
+    double ps = 1.0 / 355687428096000.0, pc = 1.0 / 20922789888000.0;   // 1/17!, 1/16!
+    const double fs[8] = {1.0 / 1307674368000.0, 1.0 / 6227020800.0, 1.0 / 39916800.0, 1.0 / 362880.0,
+                          1.0 / 5040.0, 1.0 / 120.0, 1.0 / 6.0, 1.0};
+    const double fc[8] = {1.0 / 87178291200.0, 1.0 / 479001600.0, 1.0 / 3628800.0, 1.0 / 40320.0,
+                          1.0 / 720.0, 1.0 / 24.0, 0.5, 1.0};
+    for (int i = 0; i < 8; i++) { ps = fma(ps, d2, fs[i]); pc = fma(pc, d2, fc[i]); }
+    *sh = d * ps;
+    *ch = pc;
+    return;
+  }
+  const double e = exp_dom690(d);
+  const double r = 1.0 / e;
+  *sh = 0.5 * (e - r);
+  *ch = 0.5 * (e + r);
 }
 
 // exp(x) for any x: clamped into [-746, 710] first; ldexp saturates to +inf above 709.78 (the
@@ -873,8 +896,9 @@ IS3D_HD void yterms(int mode, int op, const double* R, double y, double eta, dou
   const int quirk = quirk_pds(mode, op);
   // separable part: p^tau = mT cosh(y-eta) (spectra Grad/CE: sqrt(1+sinh^2), MomentumSpectra.cpp:307-308;
   // the spacetime path uses cosh, SpacetimeDistribution.cpp:313)
-  const double sh = sinh(y - eta);
-  const double ch = (mode <= CE && op != 0) ? sqrt(1.0 + sh * sh) : cosh(y - eta);
+  double sh, chx;
+  sinh_cosh(y - eta, &sh, &chx);
+  const double ch = (mode <= CE && op != 0) ? sqrt(1.0 + sh * sh) : chx;
   const double A = ch * R[R_UT] - sh * R[R_TAUUN];
   Y[Y_A] = A;
   Y[Y_AT] = A * R[R_INVT];
@@ -903,7 +927,8 @@ IS3D_HD void yterms(int mode, int op, const double* R, double y, double eta, dou
   Y[Y_S2] = S2; Y[Y_S1] = S1; Y[Y_SC1] = SC1; Y[Y_SS1] = SS1; Y[Y_L1] = L1;
   if (mode >= PTM) {
     const double es = R[R_ETASCALE];
-    const double shm = sinh(y - es * eta), chm = cosh(y - es * eta);
+    double shm, chm;
+    sinh_cosh(y - es * eta, &shm, &chm);
     Y[Y_MUX] = chm * R[R_UCX] + shm * R[R_USX];
     Y[Y_MUY] = chm * R[R_UCY] + shm * R[R_USY];
     Y[Y_MUZ] = chm * R[R_UCZ] + shm * R[R_USZ];
@@ -925,11 +950,12 @@ IS3D_HD void yterms(int mode, int op, const double* R, double y, double eta, dou
 //                                         Phi = the part of delta-f quadratic in (pc, ps)
 // Grad: Phi = shear p_i pi^{ij} p_j + bulk2 (pT B)^2 + c4 (pT B)(V.p)   (E^2 and E (V.p) cross terms)
 // CE / PTM / PTB (separable): Phi = shear p_i pi^{ij} p_j
-IS3D_HD dbl2 phiterms(int mode, const double* R, double pT, double c, double s) {
+IS3D_HD dbl2 phiterms(int mode, const double* R, double pT, double c, double s, const double* etab) {
   const double PTB = pT * (c * R[R_UX] + s * R[R_UY]);
   const double Q3 = R[R_SHEAR] * (pT * pT * (R[R_PIXX] * c * c + R[R_PIYY] * s * s + 2.0 * R[R_PIXY] * c * s));
   dbl2 o;
-  o.x = exp(PTB / R[R_T] - pT * R[R_ZB]);      // b' e^-zb <= 1, zb = pT |u_perp| / T >= pT B / T
+  // b' e^-zb <= 1, zb = pT |u_perp| / T >= pT B / T (table exp; underflows to 0 below e^-745)
+  o.x = exp_tab(exp_tab_coef(), etab, fma(PTB, R[R_INVT], -pT * R[R_ZB]) * kInvLn2x64);
   if (mode == GRAD) {
     const double WP = pT * (R[R_VX] * c + R[R_VY] * s);
     o.y = Q3 + PTB * (R[R_BULK2] * PTB + R[R_DIFF1] * WP);
@@ -941,7 +967,6 @@ IS3D_HD dbl2 phiterms(int mode, const double* R, double pT, double c, double s) 
 
 // exp(x) overflows above this; 1/(inf + sign) == 0 exactly as in the reference
 static constexpr double kExpMax = 709.782712893384;
-static constexpr double kFastMax = 690.0;
 
 // ---------------------------------------------------------------------------
 // Lane state for one (cell, species, pT, q) and the per-phi integrand.
@@ -968,20 +993,21 @@ struct SepLane {
 //   PTB   as CE, delta-f = (1 - sign feq) S + dz - 3 dlambda
 // mT2 = mT * mT and mTb = mT * b are per-lane constants hoisted by the caller.
 IS3D_HD void sep_setup(int flavor, const double* R, const double* Y, double mT, double mT2, double m2, double mTb,
-                       double pT, double sign, double baryon, SepLane& L) {
+                       double pT, double sign, double baryon, const double* etab, SepLane& L) {
   L.sign = sign;
   L.x = fma(mT, Y[Y_AT], -baryon * R[R_CHEM]);
   const double zb = pT * R[R_ZB];                 // >= max_j |pT B_j / T|
   L.skip = (L.x - zb > kExpMax) ? 1 : 0;
-  // b' carries e^-zb, so a = e^(x - zb - S).  u.p > 0 makes x - zb >= -chem, so without the shift
-  // S the lane's a spans [e^-chem, e^710]; S = rint(x - zb) - 300 (an integer: the subtraction is
-  // exact) for x - zb > 300 keeps every denominator a + ssc b' in ~[1e-2, e^300], so the
-  // product of two of them (paired reciprocals) stays finite and normal
+  // b' carries e^-zb, so a = e^(x - zb) 2^-k.  u.p > 0 makes x - zb >= -chem, so without the
+  // shift the lane's a spans [e^-chem, e^710]; for x - zb > 300 the exact scale esc = 2^-k with
+  // k = floor((x - zb - 300) / ln2) keeps every denominator a + ssc b' in ~[1e-2, e^301], so the
+  // product of two of them (paired reciprocals) stays finite and normal.  The scale is exact, so
+  // a = e^(x - zb) 2^-k is as accurate as e^(x - zb) itself (table exp, ~1 ulp)
   const double xs = L.x - zb;
-  const double S = (xs > 300.0) ? rint(xs) - 300.0 : 0.0;
-  L.fast = (xs >= -300.0 && S <= kFastMax) ? 1 : 0;
-  L.a = L.fast ? exp_dom690(xs - S) : 0.0;
-  const double esc = (L.fast && S > 0.0) ? exp_dom690(-S) : 1.0;
+  L.fast = (xs >= -300.0) ? 1 : 0;
+  const int k = (L.fast && xs > 300.0) ? (int)((xs - 300.0) * 1.4426950408889634) : 0;
+  L.a = L.fast ? exp_tab(exp_tab_coef(), etab, xs * kInvLn2x64, k) : 0.0;
+  const double esc = ldexp(1.0, -k);
   L.ssc = sign * esc;
   if (!L.fast) { L.Zc = R[R_UX] * R[R_INVT]; L.Zs = R[R_UY] * R[R_INVT]; } else { L.Zc = L.Zs = 0.0; }
   L.D0 = esc * (mT * Y[Y_D]); L.Dc = esc * Y[Y_WDX]; L.Ds = esc * Y[Y_WDY];

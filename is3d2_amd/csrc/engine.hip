@@ -306,7 +306,7 @@ __global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_spectra(SpecA
   double* s_etab = s_y + (long)kTile * A.nq * kYRow;      // [64] exp_tab's 2^(j/64)
 
   const int tid = threadIdx.x;
-  if (MODE >= PTM && tid < 64) s_etab[tid] = kExp2Tab64[tid];
+  if (tid < 64) s_etab[tid] = kExp2Tab64[tid];
   // XCD-aware block order (cdna_hip_programming.md T1): blocks that share an XCD (same
   // blockIdx % 8) take one contiguous range of logical ids, and logical ids run split-major, so
   // each XCD's L2 sees only its own cell splits (sized to fit) instead of every split
@@ -369,7 +369,7 @@ __global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_spectra(SpecA
       double qv = 0.0;
       if (j < A.nphi && R[R_KIND] != 0.0) {
         const dbl2 tr = s_trig[j];
-        v = phiterms(MODE, R, pT, tr.x, tr.y);
+        v = phiterms(MODE, R, pT, tr.x, tr.y, s_etab);
         if (MODE >= PTM && R[R_KIND] == 2.0) qv = modqv(R, s_cs[j]);
       }
       s_bp[t * nphp + j] = v;
@@ -403,7 +403,7 @@ __global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_spectra(SpecA
         const bool sep = (MODE <= CE) || kind == 1.0 || Y[Y_NARROW] != 0.0;
         if (sep) {
           SepLane L;
-          sep_setup(sep_flavor(MODE), R, Y, mT, mT2, m2, mTb, pT, sign, baryon, L);
+          sep_setup(sep_flavor(MODE), R, Y, mT, mT2, m2, mTb, pT, sign, baryon, s_etab, L);
           if (L.skip) continue;
           if (L.fast) sep_phi_loop<MODE, FLAGS, true, KJ>(L, s_cs + j0, BP, acc);
           else sep_phi_loop<MODE, FLAGS, false, KJ>(L, s_cs + j0, BP, acc);
@@ -549,7 +549,7 @@ __global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_dndx(DndxArgs
   double* s_etab = s_y + (long)kTile * A.nq * kYRow;      // [64] exp_tab's 2^(j/64)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (MODE >= PTM && tid < 64) s_etab[tid] = kExp2Tab64[tid];
+  if (tid < 64) s_etab[tid] = kExp2Tab64[tid];
   const long nwg = (long)A.nbx * A.nchunk;
   const long bid = blockIdx.x, q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
   const long lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
@@ -609,7 +609,7 @@ __global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_dndx(DndxArgs
         double qv = 0.0;
         if (j < A.nphi && R[R_KIND] != 0.0) {
           const dbl2 tr = s_trig[j];
-          v = phiterms(MODE, R, pT, tr.x, tr.y);
+          v = phiterms(MODE, R, pT, tr.x, tr.y, s_etab);
           if (MODE >= PTM && R[R_KIND] == 2.0) {
             dbl2 c; c.x = pT * tr.x; c.y = pT * tr.y;
             qv = modqv(R, c);
@@ -640,7 +640,7 @@ __global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_dndx(DndxArgs
           const bool sep = (MODE <= CE) || kind == 1.0 || Y[Y_NARROW] != 0.0;
           if (sep) {
             SepLane L;
-            sep_setup(sep_flavor(MODE), R, Y, mT, mT2, m2, mTb, pT, sign, baryon, L);
+            sep_setup(sep_flavor(MODE), R, Y, mT, mT2, m2, mTb, pT, sign, baryon, s_etab, L);
             if (L.skip) continue;
             cell += L.fast ? sep_phi_wsum<MODE, FLAGS, true>(L, s_cs + j0, BP, W)
                            : sep_phi_wsum<MODE, FLAGS, false>(L, s_cs + j0, BP, W);

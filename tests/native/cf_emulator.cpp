@@ -130,7 +130,7 @@ extern "C" int emu_spectra(const orc_params* p, const orc_setup* su, const orc_s
       if (kind == 0.0) continue;
       for (int j = 0; j < nphi; j++) {
         CS[j].x = pT * cph[j]; CS[j].y = pT * sph[j];
-        BP[j] = phiterms(mode, R, pT, cph[j], sph[j]);
+        BP[j] = phiterms(mode, R, pT, cph[j], sph[j], kExp2Tab64);
         QV[j] = (mode >= PTM && kind == 2.0) ? modqv(R, CS[j]) : 0.0;
       }
       for (int q = 0; q < nq; q++) {
@@ -157,7 +157,7 @@ extern "C" int emu_spectra(const orc_params* p, const orc_setup* su, const orc_s
             const bool sep = (mode <= CE) || kind == 1.0 || Y[Y_NARROW] != 0.0;
             if (sep) {
               SepLane L;
-              sep_setup(sep_flavor(mode), R, Y, mT, mT * mT, m2, mT * baryon, pT, sign, baryon, L);
+              sep_setup(sep_flavor(mode), R, Y, mT, mT * mT, m2, mT * baryon, pT, sign, baryon, kExp2Tab64, L);
               if (L.skip) continue;
               // same arithmetic as k_spectra: fast lanes evaluate phi points in pairs sharing one
               // reciprocal (an odd tail point alone)
@@ -218,6 +218,11 @@ extern "C" int emu_spectra(const orc_params* p, const orc_setup* su, const orc_s
 extern "C" void emu_exp(const double* x, long n, double* out) {
   const ExpCoef E = exp_coef();
   for (long i = 0; i < n; i++) out[i] = exp_clamped(E, x[i]);
+}
+
+// the y-terms' sinh / cosh (sinh_cosh)
+extern "C" void emu_sinh_cosh(const double* x, long n, double* sh, double* ch) {
+  for (long i = 0; i < n; i++) sinh_cosh(x[i], sh + i, ch + i);
 }
 
 // PTB Jonah table from the cf_math.h pieces, serially (the device builds it in parallel, same order)

@@ -89,3 +89,19 @@ def test_kernel_exp_tab_accuracy():
     small = np.abs(x) <= 2
     assert (np.abs(out[small] - ref[small]) <= 2 * np.spacing(ref[small])).all()
     assert (out[x < -746.0] == 0.0).all()
+
+
+def test_kernel_sinh_cosh_accuracy():
+    """sinh_cosh (cf_math.h, y-terms) against libm over |y - eta| <= 12: <= 4 ulp, odd / even symmetry."""
+    import ctypes as C
+    from helpers import emulator
+    rng = np.random.default_rng(6)
+    x = np.concatenate([rng.uniform(-12, 12, 100000), rng.uniform(-0.6, 0.6, 100000),
+                        np.array([0.0, 1e-300, -1e-300, 0.5, -0.5, np.nextafter(0.5, 0), 12.0])])
+    sh, ch = np.empty_like(x), np.empty_like(x)
+    P = C.POINTER(C.c_double)
+    emulator().emu_sinh_cosh(x.ctypes.data_as(P), C.c_long(len(x)), sh.ctypes.data_as(P), ch.ctypes.data_as(P))
+    nz = x != 0
+    assert (np.abs(sh[nz] - np.sinh(x[nz])) <= 4 * np.spacing(np.abs(np.sinh(x[nz])))).all()
+    assert (np.abs(ch - np.cosh(x)) <= 4 * np.spacing(np.cosh(x))).all()
+    assert sh[x == 0].tolist() == [0.0] and ch[x == 0].tolist() == [1.0]
