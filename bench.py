@@ -183,14 +183,17 @@ def main():
     ms_total = float(np.mean([s["ms_total"] for s in kstats]))
     flops = FLOPS_PER_NODE[mode] * neta * units_local
     achieved = flops / (ms_spectra * 1e-3) / 1e12
-    traffic = None
+    traffic, executed = None, None
+    key = "%s_mode%d" % (args.config, mode) if args.operation == 1 else "%s_op0_mode%d" % (args.config, mode)
     pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(pmc):
-        try:
-            key = "%s_mode%d" % (args.config, mode) if args.operation == 1 else "%s_op0_mode%d" % (args.config, mode)
-            traffic = json.load(open(pmc)).get(key)
-        except Exception:
-            traffic = None
+        traffic = json.load(open(pmc)).get(key)
+    pv = os.path.join(ROOT, "profiles", "pmc_valu.json")
+    if os.path.exists(pv):
+        executed = json.load(open(pv)).get(key)
+    if executed is not None:
+        executed = dict(executed, note="PMC pass (tag) of this workload: share of SIMD cycles issuing VALU; "
+                                       "achieved/frac above use the reference's frozen flop counts")
 
     if rank == 0:
         res = {
@@ -221,7 +224,7 @@ def main():
                 "kernel": "k_spectra" if args.operation == 1 else "k_dndx", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
                 "algorithmic_flops_per_launch": flops, "flops_per_point": FLOPS_PER_NODE[mode] * neta,
-                "kernel_ms": ms_spectra, "pass_ms": ms_total,
+                "kernel_ms": ms_spectra, "pass_ms": ms_total, "executed": executed,
             },
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -26,6 +26,9 @@ __global__ __launch_bounds__(256) void kbench(double* out, double seed) {
                      e = fma(-v[c], r, 1.0); v[c] = fma(r, e, r); }
       if (OP == 6) v[c] = __builtin_amdgcn_rsq(v[c]);                       // v_rsq_f64
       if (OP == 7) v[c] = (float)(1.0f / (float)v[c]);                      // f32 rcp + cvts
+      if (OP == 8) v[c] = ldexp(v[c], (int)(threadIdx.x & 1) - (int)(c & 1)); // v_ldexp_f64
+      if (OP == 9) v[c] = v[c] * 0.999999;                                  // v_mul_f64
+      if (OP == 10) v[c] = __builtin_bit_cast(double, __builtin_bit_cast(unsigned long long, v[c]) ^ 1ull); // 2x v_xor_b32
     }
   }
   double s = 0;
@@ -64,13 +67,15 @@ int main() {
   int blocks = 256 * 8;   // 8 blocks of 4 waves per CU
   double* out;
   hipMalloc(&out, sizeof(double) * blocks * 256);
-  const char* names[] = {"v_fma_f64", "v_rcp_f64", "1.0/x (IEEE)", "exp(x) ocml", "sqrt (IEEE)", "rcp+2NR", "v_rsq_f64", "f32 rcp+cvt"};
-  float ms[8];
+  const char* names[] = {"v_fma_f64", "v_rcp_f64", "1.0/x (IEEE)", "exp(x) ocml", "sqrt (IEEE)", "rcp+2NR", "v_rsq_f64",
+                         "f32 rcp+cvt", "v_ldexp_f64", "v_mul_f64", "2x v_xor_b32"};
+  float ms[11];
   ms[0] = run<0>(out, blocks); ms[1] = run<1>(out, blocks); ms[2] = run<2>(out, blocks); ms[3] = run<3>(out, blocks);
   ms[4] = run<4>(out, blocks); ms[5] = run<5>(out, blocks); ms[6] = run<6>(out, blocks); ms[7] = run<7>(out, blocks);
+  ms[8] = run<8>(out, blocks); ms[9] = run<9>(out, blocks); ms[10] = run<10>(out, blocks);
   const double ops = (double)blocks * 4 /*waves*/ * ITERS * CH;   // wave-level operations
   const double simds = 256 * 4;
-  for (int k = 0; k < 8; k++) {
+  for (int k = 0; k < 11; k++) {
     const double ns_per_op_per_simd = ms[k] * 1e6 / (ops / simds);
     printf("%-14s %8.3f ms  %6.3f ns/wave-op/SIMD  (= %.1f cycles @2.4GHz, %.2fx fma)\n", names[k], ms[k],
            ns_per_op_per_simd, ns_per_op_per_simd * 2.4, ms[k] / ms[0]);

@@ -5,6 +5,8 @@
   profiles/<tag>_pmc.json           per-kernel averages of the PMC passes
   profiles/pmc_traffic.json         HBM bytes per k_spectra launch, keyed "<config>_mode<m>",
                                     read by bench.py for roofline.traffic
+  profiles/pmc_valu.json            k_spectra VALU instructions, issue fraction and clock, same keys,
+                                    read by bench.py for roofline.executed
 
 HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (KiB -> B): on gfx950 FETCH_SIZE counts
 half the bytes of wide coalesced reads (MI355X_MICROARCH.md, HBM section); WRITE_SIZE is exact
@@ -62,12 +64,29 @@ def main():
         if "FETCH_SIZE" in e and "WRITE_SIZE" in e:
             e["hbm_bytes_per_launch"] = (2.0 * e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024.0
     json.dump(out, open(os.path.join(prof, "%s_pmc.json" % tag), "w"), indent=1, sort_keys=True)
+    for k, e in out.items():
+        # executed-work view: the effective clock is GRBM_GUI_ACTIVE / 8 XCDs over the dispatch, and
+        # SQ_ACTIVE_INST_VALU counts quad-cycles in which a wave issued VALU, summed over waves, so
+        # valu_issue_frac = 4 x SQ_ACTIVE_INST_VALU / (1024 SIMDs x cycles): the share of SIMD cycles
+        # the VALU pipes were issuing (MI355X_MICROARCH.md, PMC and DVFS sections)
+        if "GRBM_GUI_ACTIVE" in e and "SQ_ACTIVE_INST_VALU" in e:
+            cyc = e["GRBM_GUI_ACTIVE"] / 8.0
+            e["clock_ghz"] = cyc / e["avg_ns_pmc_pass"]
+            e["valu_issue_frac"] = 4.0 * e["SQ_ACTIVE_INST_VALU"] / (1024.0 * cyc)
     spec = [k for k in out if k.startswith("k_spectra")]
+    key = "%s_mode%d" % (config, mode)
     if spec and "hbm_bytes_per_launch" in out[spec[0]]:
         tp = os.path.join(prof, "pmc_traffic.json")
         t = json.load(open(tp)) if os.path.exists(tp) else {}
-        t["%s_mode%d" % (config, mode)] = out[spec[0]]["hbm_bytes_per_launch"]
+        t[key] = out[spec[0]]["hbm_bytes_per_launch"]
         json.dump(t, open(tp, "w"), indent=1, sort_keys=True)
+    if spec and "valu_issue_frac" in out[spec[0]]:
+        vp = os.path.join(prof, "pmc_valu.json")
+        v = json.load(open(vp)) if os.path.exists(vp) else {}
+        e = out[spec[0]]
+        v[key] = {"tag": tag, "valu_insts_per_launch": e["SQ_INSTS_VALU"], "valu_issue_frac": e["valu_issue_frac"],
+                  "clock_ghz": e["clock_ghz"]}
+        json.dump(v, open(vp, "w"), indent=1, sort_keys=True)
     for k, e in sorted(out.items()):
         print(k, {c: round(v, 3) for c, v in e.items()})
 
