@@ -27,6 +27,7 @@ sys.path.insert(0, ROOT)
 
 FLOPS_PER_NODE = {1: 65, 2: 67, 3: 140, 4: 140, 5: 140}   # SURVEY.md 8(d), frozen algorithmic counts
 FP64_PEAK_TFLOPS = 78.6                                     # MI355X FP64 vector (= FP64 matrix) dense peak
+HBM_PEAK_BPS = 8.0e12                                       # MI355X HBM3E
 MODE_NAMES = {1: "grad14", 2: "rta-ce", 3: "ptm", 4: "ptb", 5: "ptma"}
 
 CONFIGS = {
@@ -225,6 +226,9 @@ def main():
                 "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
                 "algorithmic_flops_per_launch": flops, "flops_per_point": FLOPS_PER_NODE[mode] * neta,
                 "kernel_ms": ms_spectra, "pass_ms": ms_total, "executed": executed,
+                # HBM view (north_star): PMC bytes per launch over the live kernel time, vs 8 TB/s
+                "hbm_gbs": None if traffic is None else traffic / (ms_spectra * 1e-3) / 1e9,
+                "hbm_frac": None if traffic is None else traffic / (ms_spectra * 1e-3) / HBM_PEAK_BPS,
             },
         }
         if world == 1 and not args.no_cpu_baseline:
