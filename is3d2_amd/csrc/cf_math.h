@@ -999,13 +999,14 @@ IS3D_HD void sep_setup(int flavor, const double* R, const double* Y, double mT, 
   const double zb = pT * R[R_ZB];                 // >= max_j |pT B_j / T|
   L.skip = (L.x - zb > kExpMax) ? 1 : 0;
   // b' carries e^-zb, so a = e^(x - zb) 2^-k.  u.p > 0 makes x - zb >= -chem, so without the
-  // shift the lane's a spans [e^-chem, e^710]; for x - zb > 300 the exact scale esc = 2^-k with
-  // k = floor((x - zb - 300) / ln2) keeps every denominator a + ssc b' in ~[1e-2, e^301], so the
-  // product of two of them (paired reciprocals) stays finite and normal.  The scale is exact, so
+  // shift the lane's a spans [e^-chem, e^710]; for x - zb > 150 the exact scale esc = 2^-k with
+  // k = floor((x - zb - 150) / ln2) keeps every denominator a + ssc b' in ~[1e-2, e^151] (times
+  // E = u.p < e^10 for CE/PTB), so the product of four of them (one reciprocal per four points,
+  // sep_quad_t) stays finite and normal.  The scale is exact, so
   // a = e^(x - zb) 2^-k is as accurate as e^(x - zb) itself (table exp, ~1 ulp)
   const double xs = L.x - zb;
   L.fast = (xs >= -300.0) ? 1 : 0;
-  const int k = (L.fast && xs > 300.0) ? (int)((xs - 300.0) * 1.4426950408889634) : 0;
+  const int k = (L.fast && xs > 150.0) ? (int)((xs - 150.0) * 1.4426950408889634) : 0;
   L.a = L.fast ? exp_tab(exp_tab_coef(), etab, xs * kInvLn2x64, k) : 0.0;
   const double esc = ldexp(1.0, -k);
   L.ssc = sign * esc;
@@ -1087,6 +1088,24 @@ IS3D_HD double sep_fast_tail(const SepLane& L, dbl2 cs, dbl2 bp, double pds, dou
   return (OUT && pds <= 0.0) ? 0.0 : g;
 }
 
+// phi points per lane: the block size among 32, 24, 8, 2 with the least padding of the phi grid (ties
+// to the larger block, whose per-lane setup is spread over more points): 1 -> 2, 24 / 48 -> 24, 32 -> 32
+IS3D_HD int spectra_kj(int nphi) {
+  int best = 32;
+  long best_pad = (long)((nphi + 31) / 32) * 32;
+  const int cand[3] = {24, 8, 2};
+  for (int kj : cand) {
+    const long pad = (long)((nphi + kj - 1) / kj) * kj;
+    if (pad < best_pad) { best = kj; best_pad = pad; }
+  }
+  return best;
+}
+
+// Fast separable lanes take their phi points four per reciprocal (sep_quad_t) except Grad, whose
+// 3-waves/SIMD register budget the extra in-flight points overflow (MI355X A/B, profiles/round1_r1q_ab_quad.log:
+// RTA-CE +5.5% with fours, Grad -6% from spills); pairs otherwise
+IS3D_HD bool sep_quads(int mode, int kj) { return mode != GRAD && kj % 4 == 0; }
+
 // One separable integrand point; returns w * p.dsigma * f (0 when outflow-cut).
 // FL: separable flavour; REG: regulate_deltaf; OUT: outflow; FAST: exp factorised (see sep_setup).
 template <int FL, bool REG, bool OUT, bool FAST>
@@ -1118,6 +1137,27 @@ IS3D_HD void sep_pair_t(const SepLane& L, dbl2 c0, dbl2 b0, dbl2 c1, dbl2 b1, do
   v1 = sep_fast_tail<FL, REG, OUT>(L, c1, b1, pds1, E1, r * q0);
 }
 
+// Four fast-path points with one reciprocal: r = 1/(q0 q1 q2 q3), 1/(q0 q1) = r q2 q3, then as the pair
+template <int FL, bool REG, bool OUT>
+IS3D_HD void sep_quad_t(const SepLane& L, const dbl2* c, const dbl2* b, double* v) {
+  const bool needE = (FL == SEP_CE || FL == SEP_PTB);
+  double pds[4], E[4], q[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    pds[i] = lin(L.D0, L.Dc, L.Ds, c[i]);
+    const double den = fma(L.ssc, b[i].x, L.a);
+    E[i] = needE ? lin(L.E0, L.Ec, L.Es, c[i]) : 1.0;
+    q[i] = needE ? den * E[i] : den;
+  }
+  const double q01 = q[0] * q[1], q23 = q[2] * q[3];
+  const double r = rcp1(q01 * q23);
+  const double r01 = r * q23, r23 = r * q01;
+  v[0] = sep_fast_tail<FL, REG, OUT>(L, c[0], b[0], pds[0], E[0], r01 * q[1]);
+  v[1] = sep_fast_tail<FL, REG, OUT>(L, c[1], b[1], pds[1], E[1], r01 * q[0]);
+  v[2] = sep_fast_tail<FL, REG, OUT>(L, c[2], b[2], pds[2], E[2], r23 * q[3]);
+  v[3] = sep_fast_tail<FL, REG, OUT>(L, c[3], b[3], pds[3], E[3], r23 * q[2]);
+}
+
 IS3D_HD void sep_pair(int flavor, const SepLane& L, dbl2 c0, dbl2 b0, dbl2 c1, dbl2 b1, int regulate, int outflow,
                       double& v0, double& v1) {
 #define IS3D_PAIR_CASE(FLV)                                                                       \
@@ -1136,6 +1176,25 @@ IS3D_HD void sep_pair(int flavor, const SepLane& L, dbl2 c0, dbl2 b0, dbl2 c1, d
   IS3D_PAIR_CASE(SEP_PTB)
   IS3D_PAIR_CASE(SEP_FEQ)
 #undef IS3D_PAIR_CASE
+}
+
+IS3D_HD void sep_quad(int flavor, const SepLane& L, const dbl2* c, const dbl2* b, int regulate, int outflow, double* v) {
+#define IS3D_QUAD_CASE(FLV)                                                                       \
+  if (flavor == FLV) {                                                                            \
+    if (regulate) {                                                                               \
+      if (outflow) sep_quad_t<FLV, true, true>(L, c, b, v);                                       \
+      else sep_quad_t<FLV, true, false>(L, c, b, v);                                              \
+    } else {                                                                                      \
+      if (outflow) sep_quad_t<FLV, false, true>(L, c, b, v);                                      \
+      else sep_quad_t<FLV, false, false>(L, c, b, v);                                             \
+    }                                                                                             \
+    return;                                                                                       \
+  }
+  IS3D_QUAD_CASE(SEP_GRAD)
+  IS3D_QUAD_CASE(SEP_CE)
+  IS3D_QUAD_CASE(SEP_PTB)
+  IS3D_QUAD_CASE(SEP_FEQ)
+#undef IS3D_QUAD_CASE
 }
 
 IS3D_HD double sep_point(int flavor, const SepLane& L, dbl2 cs, dbl2 bp, int regulate, int outflow) {
@@ -1249,6 +1308,36 @@ IS3D_HD void mod_pair_t(const ModLane& L, dbl2 c0, dbl2 c1, dbl2 qv, double& v0,
   const double g0 = pds0 * (en0 * (r * q1)), g1 = pds1 * (en1 * (r * q0));
   v0 = (OUT && pds0 <= 0.0) ? 0.0 : g0;
   v1 = (OUT && pds1 <= 0.0) ? 0.0 : g1;
+}
+
+// four points, one reciprocal (1 + sign en lies in ~[1e-3, 2], so the product of four is normal)
+template <bool OUT, bool CLAMP>
+IS3D_HD void mod_quad_t(const ModLane& L, const dbl2* c, dbl2 qa, dbl2 qb, double* v) {
+  const double en[4] = {mod_en<CLAMP>(L, c[0], qa.x), mod_en<CLAMP>(L, c[1], qa.y), mod_en<CLAMP>(L, c[2], qb.x),
+                        mod_en<CLAMP>(L, c[3], qb.y)};
+  double q[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) q[i] = fma(L.sign, en[i], 1.0);
+  const double q01 = q[0] * q[1], q23 = q[2] * q[3];
+  const double r = rcp1(q01 * q23);
+  const double r01 = r * q23, r23 = r * q01;
+  const double rq[4] = {r01 * q[1], r01 * q[0], r23 * q[3], r23 * q[2]};
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const double pds = lin(L.D0, L.Dc, L.Ds, c[i]);
+    const double g = pds * (en[i] * rq[i]);
+    v[i] = (OUT && pds <= 0.0) ? 0.0 : g;
+  }
+}
+
+IS3D_HD void mod_quad(const ModLane& L, const dbl2* c, dbl2 qa, dbl2 qb, int outflow, double* v) {
+  if (L.clamp) {
+    if (outflow) mod_quad_t<true, true>(L, c, qa, qb, v);
+    else mod_quad_t<false, true>(L, c, qa, qb, v);
+  } else {
+    if (outflow) mod_quad_t<true, false>(L, c, qa, qb, v);
+    else mod_quad_t<false, false>(L, c, qa, qb, v);
+  }
 }
 
 IS3D_HD double mod_point(const ModLane& L, dbl2 cs, double qv, int outflow) {

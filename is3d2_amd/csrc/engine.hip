@@ -211,6 +211,12 @@ struct SpecArgs {
 // flag bits of the spectra kernel instantiation
 constexpr int F_REG = 1, F_OUT = 2;
 
+#ifndef IS3D_QUAD_RCP
+#define IS3D_QUAD_RCP 1       // fast path: four phi points per reciprocal where sep_quads() says so
+#endif
+#ifndef IS3D_MOD_QUAD
+#define IS3D_MOD_QUAD 1       // modified path: four phi points per reciprocal when KJ % 4 == 0
+#endif
 #ifndef IS3D_PAIR_RCP
 #define IS3D_PAIR_RCP 1       // fast path: two phi points per reciprocal (sep_pair_t)
 #endif
@@ -221,6 +227,25 @@ template <int MODE, int FLAGS, bool FAST, int KJ>
 __device__ __forceinline__ void sep_phi_loop(const SepLane& L, const dbl2* CS, const dbl2* BP, double* acc) {
   constexpr int FL = (MODE == GRAD) ? SEP_GRAD : (MODE == CE || MODE == PTM) ? SEP_CE : (MODE == PTB) ? SEP_PTB : SEP_FEQ;
   constexpr bool REG = (FLAGS & F_REG) != 0, OUT = (FLAGS & F_OUT) != 0;
+  if (FAST && IS3D_QUAD_RCP && sep_quads(MODE, KJ)) {
+    dbl2 c[4], b[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) { c[i] = CS[i]; b[i] = BP[i]; }
+#pragma unroll
+    for (int jj = 0; jj < KJ; jj += 4) {
+      dbl2 nc[4], nb[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        nc[i] = c[i]; nb[i] = b[i];
+        if (jj + 4 < KJ) { nc[i] = CS[jj + 4 + i]; nb[i] = BP[jj + 4 + i]; }
+      }
+      double v[4];
+      sep_quad_t<FL, REG, OUT>(L, c, b, v);
+#pragma unroll
+      for (int i = 0; i < 4; i++) { acc[jj + i] += v[i]; c[i] = nc[i]; b[i] = nb[i]; }
+    }
+    return;
+  }
   if (FAST && IS3D_PAIR_RCP) {
     dbl2 c0 = CS[0], b0 = BP[0], c1 = CS[1], b1 = BP[1];
 #pragma unroll
@@ -247,6 +272,27 @@ __device__ __forceinline__ void sep_phi_loop(const SepLane& L, const dbl2* CS, c
 template <int FLAGS, bool CLAMP, int KJ>
 __device__ __forceinline__ void mod_phi_loop(const ModLane& M, const dbl2* CS, const dbl2* QV, double* acc) {
   constexpr bool OUT = (FLAGS & F_OUT) != 0;
+  if (IS3D_MOD_QUAD && KJ % 4 == 0) {
+    dbl2 c[4], qa = QV[0], qb = QV[1];
+#pragma unroll
+    for (int i = 0; i < 4; i++) c[i] = CS[i];
+#pragma unroll
+    for (int jj = 0; jj < KJ; jj += 4) {
+      dbl2 nc[4], na = qa, nb = qb;
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        nc[i] = c[i];
+        if (jj + 4 < KJ) nc[i] = CS[jj + 4 + i];
+      }
+      if (jj + 4 < KJ) { na = QV[(jj >> 1) + 2]; nb = QV[(jj >> 1) + 3]; }
+      double v[4];
+      mod_quad_t<OUT, CLAMP>(M, c, qa, qb, v);
+#pragma unroll
+      for (int i = 0; i < 4; i++) { acc[jj + i] += v[i]; c[i] = nc[i]; }
+      qa = na; qb = nb;
+    }
+    return;
+  }
   dbl2 c0 = CS[0], c1 = CS[1], q = QV[0];
 #pragma unroll
   for (int jj = 0; jj < KJ; jj += 2) {
@@ -1270,17 +1316,6 @@ static void launch_spectra(dim3 grid, size_t shmem, hipStream_t st, const SpecAr
   }
 }
 
-// phi points per lane: the block size among 32, 24, 8, 2 with the least padding of the phi grid (ties
-// to the larger block, whose per-lane setup is spread over more points): 1 -> 2, 24 / 48 -> 24, 32 -> 32
-static int spectra_kj(int nphi) {
-  int best = 32;
-  long best_pad = (long)((nphi + 31) / 32) * 32;
-  for (int kj : {24, 8, 2}) {
-    const long pad = (long)((nphi + kj - 1) / kj) * kj;
-    if (pad < best_pad) { best = kj; best_pad = pad; }
-  }
-  return best;
-}
 
 extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   if (!e) return IS3D_ERR_ARG;

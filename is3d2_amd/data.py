@@ -8,7 +8,13 @@ DF_HRG = {1: "urqmd", 2: "smash", 3: "smash_box"}   # DeltafData.cpp:30-45
 
 
 def grid(name):
-    """(values, weights) of a 2-column quadrature table, e.g. 'pT48', 'phi32', 'y21', 'eta24'."""
+    """(values, weights) of a 2-column quadrature table, e.g. 'pT48', 'phi32', 'y21', 'eta24', or an
+    explicit table given as rows [[value, weight], ...] / a (values, weights) pair."""
+    if not isinstance(name, str):
+        g = np.asarray(name, dtype=np.float64)
+        if g.ndim == 2 and g.shape[0] == 2 and g.shape[1] != 2:
+            g = g.T
+        return np.ascontiguousarray(g[:, 0]), np.ascontiguousarray(g[:, 1])
     g = np.load(os.path.join(_DATA, "grids.npz"))[name]
     return g[:, 0].copy(), g[:, 1].copy()
 

@@ -159,10 +159,16 @@ extern "C" int emu_spectra(const orc_params* p, const orc_setup* su, const orc_s
               SepLane L;
               sep_setup(sep_flavor(mode), R, Y, mT, mT * mT, m2, mT * baryon, pT, sign, baryon, kExp2Tab64, L);
               if (L.skip) continue;
-              // same arithmetic as k_spectra: fast lanes evaluate phi points in pairs sharing one
-              // reciprocal (an odd tail point alone)
+              // same arithmetic as k_spectra: fast lanes evaluate phi points in fours (phi blocks that
+              // are multiples of 4) or pairs sharing one reciprocal (an odd tail point alone)
               int j = 0;
               if (L.fast) {
+                if (op != 0 && sep_quads(mode, spectra_kj(nphi)))   // k_spectra; k_dndx pairs
+                  for (; j + 3 < nphi; j += 4) {
+                    double v[4];
+                    sep_quad(sep_flavor(mode), L, &CS[j], &BP[j], p->regulate_deltaf, p->outflow, v);
+                    for (int i = 0; i < 4; i++) a[j + i] += v[i];
+                  }
                 for (; j + 1 < nphi; j += 2) {
                   double v0, v1;
                   sep_pair(sep_flavor(mode), L, CS[j], BP[j], CS[j + 1], BP[j + 1], p->regulate_deltaf, p->outflow, v0, v1);
@@ -176,6 +182,13 @@ extern "C" int emu_spectra(const orc_params* p, const orc_setup* su, const orc_s
               mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, kExp2Tab64, M);
               if (M.skip) continue;
               int j = 0;
+              if (op != 0 && spectra_kj(nphi) % 4 == 0)       // k_spectra's fours; k_dndx pairs
+                for (; j + 3 < nphi; j += 4) {
+                  double v[4];
+                  dbl2 qa, qb; qa.x = QV[j]; qa.y = QV[j + 1]; qb.x = QV[j + 2]; qb.y = QV[j + 3];
+                  mod_quad(M, &CS[j], qa, qb, p->outflow, v);
+                  for (int i = 0; i < 4; i++) a[j + i] += v[i];
+                }
               for (; j + 1 < nphi; j += 2) {
                 double v0, v1;
                 dbl2 q; q.x = QV[j]; q.y = QV[j + 1];
