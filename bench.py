@@ -98,7 +98,7 @@ def main():
     ap.add_argument("--operation", type=int, default=1, choices=[0, 1],
                     help="1 continuous spectra (default, the BASELINE metric); 0 spacetime distributions dN/dX")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=25.0)
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))

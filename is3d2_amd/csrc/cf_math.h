@@ -1101,10 +1101,10 @@ IS3D_HD int spectra_kj(int nphi) {
   return best;
 }
 
-// Fast separable lanes take their phi points four per reciprocal (sep_quad_t) except Grad, whose
-// 3-waves/SIMD register budget the extra in-flight points overflow (MI355X A/B, profiles/round1_r1q_ab_quad.log:
-// RTA-CE +5.5% with fours, Grad -6% from spills); pairs otherwise
-IS3D_HD bool sep_quads(int mode, int kj) { return mode != GRAD && kj % 4 == 0; }
+// Fast separable lanes take their phi points four per reciprocal (sep_quad_t) when the phi block is a
+// multiple of 4, pairs otherwise (MI355X A/B: RTA-CE +5.5%, profiles/round1_r1q_ab_quad.log; Grad +1.2%
+// when its fours skip the prefetch that overflows its 3-waves/SIMD registers, round1_r1t_ab_gq.log)
+IS3D_HD bool sep_quads(int mode, int kj) { return kj % 4 == 0; }
 
 // One separable integrand point; returns w * p.dsigma * f (0 when outflow-cut).
 // FL: separable flavour; REG: regulate_deltaf; OUT: outflow; FAST: exp factorised (see sep_setup).

@@ -227,6 +227,20 @@ template <int MODE, int FLAGS, bool FAST, int KJ>
 __device__ __forceinline__ void sep_phi_loop(const SepLane& L, const dbl2* CS, const dbl2* BP, double* acc) {
   constexpr int FL = (MODE == GRAD) ? SEP_GRAD : (MODE == CE || MODE == PTM) ? SEP_CE : (MODE == PTB) ? SEP_PTB : SEP_FEQ;
   constexpr bool REG = (FLAGS & F_REG) != 0, OUT = (FLAGS & F_OUT) != 0;
+  if (FAST && IS3D_QUAD_RCP && MODE == GRAD && sep_quads(MODE, KJ)) {
+    // Grad: fours without the one-quad-ahead prefetch, whose registers the 3-waves/SIMD budget lacks
+#pragma unroll
+    for (int jj = 0; jj < KJ; jj += 4) {
+      dbl2 c[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) { c[i] = CS[jj + i]; b[i] = BP[jj + i]; }
+      double v[4];
+      sep_quad_t<FL, REG, OUT>(L, c, b, v);
+#pragma unroll
+      for (int i = 0; i < 4; i++) acc[jj + i] += v[i];
+    }
+    return;
+  }
   if (FAST && IS3D_QUAD_RCP && sep_quads(MODE, KJ)) {
     dbl2 c[4], b[4];
 #pragma unroll
