@@ -211,6 +211,9 @@ struct SpecArgs {
 // flag bits of the spectra kernel instantiation
 constexpr int F_REG = 1, F_OUT = 2;
 
+#ifndef IS3D_SPLIT_BYTES
+#define IS3D_SPLIT_BYTES (2L << 20)   // record bytes per cell split (k_spectra grid sizing)
+#endif
 #ifndef IS3D_QUAD_RCP
 #define IS3D_QUAD_RCP 1       // fast path: four phi points per reciprocal where sep_quads() says so
 #endif
@@ -1406,7 +1409,7 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   // so every XCD owns whole splits; at most 64 slabs
   const long max_split = (n + kTile - 1) / kTile;
   const long by_fill = (8192 + wgs - 1) / wgs;
-  const long by_l2 = ((long)NREC * 8 * n + (2L << 20) - 1) / (2L << 20);
+  const long by_l2 = ((long)NREC * 8 * n + IS3D_SPLIT_BYTES - 1) / IS3D_SPLIT_BYTES;
   long nsplit = std::max(by_fill, std::min(by_l2, 64L));
   if (nsplit >= 8) nsplit = (nsplit + 7) / 8 * 8;
   nsplit = std::max(1L, std::min(nsplit, max_split));
