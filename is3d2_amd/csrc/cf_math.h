@@ -154,12 +154,13 @@ IS3D_HD double exp_tab(const ExpTabCoef& E, const double* tab, double xN, int ks
 IS3D_HD void sinh_cosh(double d, double* sh, double* ch) {
   if (fabs(d) < 0.5) {
     const double d2 = d * d;
-    double ps = 1.0 / 355687428096000.0, pc = 1.0 / 20922789888000.0;   // 1/17!, 1/16!
+    double ps = kconst(1.0 / 355687428096000.0), pc = kconst(1.0 / 20922789888000.0);   // 1/17!, 1/16!
     const double fs[8] = {1.0 / 1307674368000.0, 1.0 / 6227020800.0, 1.0 / 39916800.0, 1.0 / 362880.0,
                           1.0 / 5040.0, 1.0 / 120.0, 1.0 / 6.0, 1.0};
     const double fc[8] = {1.0 / 87178291200.0, 1.0 / 479001600.0, 1.0 / 3628800.0, 1.0 / 40320.0,
                           1.0 / 720.0, 1.0 / 24.0, 0.5, 1.0};
-    for (int i = 0; i < 8; i++) { ps = fma(ps, d2, fs[i]); pc = fma(pc, d2, fc[i]); }
+    // coefficients pinned to SGPRs at the point of use (kconst): hoisted into VGPRs they were spilled
+    for (int i = 0; i < 8; i++) { ps = fma(ps, d2, kconst(fs[i])); pc = fma(pc, d2, kconst(fc[i])); }
     *sh = d * ps;
     *ch = pc;
     return;
@@ -1103,7 +1104,7 @@ IS3D_HD int spectra_kj(int nphi) {
 
 // Fast separable lanes take their phi points four per reciprocal (sep_quad_t) when the phi block is a
 // multiple of 4, pairs otherwise (MI355X A/B: RTA-CE +5.5%, profiles/round1_r1q_ab_quad.log; Grad +1.2%
-// when its fours skip the prefetch that overflows its 3-waves/SIMD registers, round1_r1t_ab_gq.log)
+// without prefetch while it spilled, round1_r1t_ab_gq.log, +1.2% more with it once spill-free, round1_r1w_ab_gpf.log)
 IS3D_HD bool sep_quads(int mode, int kj) { return kj % 4 == 0; }
 
 // One separable integrand point; returns w * p.dsigma * f (0 when outflow-cut).

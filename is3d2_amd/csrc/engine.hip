@@ -214,6 +214,9 @@ constexpr int F_REG = 1, F_OUT = 2;
 #ifndef IS3D_SPLIT_BYTES
 #define IS3D_SPLIT_BYTES (2L << 20)   // record bytes per cell split (k_spectra grid sizing)
 #endif
+#ifndef IS3D_GRAD_NOPF
+#define IS3D_GRAD_NOPF 0      // 1: Grad fours without the one-quad-ahead prefetch (needed while Grad spilled)
+#endif
 #ifndef IS3D_QUAD_RCP
 #define IS3D_QUAD_RCP 1       // fast path: four phi points per reciprocal where sep_quads() says so
 #endif
@@ -230,8 +233,8 @@ template <int MODE, int FLAGS, bool FAST, int KJ>
 __device__ __forceinline__ void sep_phi_loop(const SepLane& L, const dbl2* CS, const dbl2* BP, double* acc) {
   constexpr int FL = (MODE == GRAD) ? SEP_GRAD : (MODE == CE || MODE == PTM) ? SEP_CE : (MODE == PTB) ? SEP_PTB : SEP_FEQ;
   constexpr bool REG = (FLAGS & F_REG) != 0, OUT = (FLAGS & F_OUT) != 0;
-  if (FAST && IS3D_QUAD_RCP && MODE == GRAD && sep_quads(MODE, KJ)) {
-    // Grad: fours without the one-quad-ahead prefetch, whose registers the 3-waves/SIMD budget lacks
+  if (FAST && IS3D_QUAD_RCP && IS3D_GRAD_NOPF && MODE == GRAD && sep_quads(MODE, KJ)) {
+    // Grad fours without the one-quad-ahead prefetch (for register-starved builds)
 #pragma unroll
     for (int jj = 0; jj < KJ; jj += 4) {
       dbl2 c[4], b[4];

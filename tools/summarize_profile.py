@@ -63,7 +63,6 @@ def main():
     for k, e in out.items():
         if "FETCH_SIZE" in e and "WRITE_SIZE" in e:
             e["hbm_bytes_per_launch"] = (2.0 * e["FETCH_SIZE"] + e["WRITE_SIZE"]) * 1024.0
-    json.dump(out, open(os.path.join(prof, "%s_pmc.json" % tag), "w"), indent=1, sort_keys=True)
     for k, e in out.items():
         # executed-work view: the effective clock is GRBM_GUI_ACTIVE / 8 XCDs over the dispatch, and
         # SQ_ACTIVE_INST_VALU counts quad-cycles in which a wave issued VALU, summed over waves, so
@@ -73,6 +72,7 @@ def main():
             cyc = e["GRBM_GUI_ACTIVE"] / 8.0
             e["clock_ghz"] = cyc / e["avg_ns_pmc_pass"]
             e["valu_issue_frac"] = 4.0 * e["SQ_ACTIVE_INST_VALU"] / (1024.0 * cyc)
+    json.dump(out, open(os.path.join(prof, "%s_pmc.json" % tag), "w"), indent=1, sort_keys=True)
     spec = [k for k in out if k.startswith("k_spectra")]
     key = "%s_mode%d" % (config, mode)
     if spec and "hbm_bytes_per_launch" in out[spec[0]]:
