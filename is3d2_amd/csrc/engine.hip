@@ -34,7 +34,6 @@ using namespace is3d;
 namespace {
 
 constexpr int kBlock = 256;
-constexpr int kJmax = 32;     // phi accumulators per lane (k_dndx; k_spectra picks KJ per grid, spectra_kj)
 #ifndef IS3D_KTILE
 #define IS3D_KTILE 8
 #endif
@@ -534,7 +533,7 @@ __global__ __launch_bounds__(256) void k_reduce(ReduceArgs A) {
 // ------------------------------------------------------------------------------------------
 // Weighted phi sums: sum_j w_phi[j] x (w_eta p.dsigma f)(phi_j) for one lane and cell, with the
 // same per-point arithmetic as k_spectra (W = phi weights as {w_j, w_j+1} pairs, 0 in the padding).
-template <int MODE, int FLAGS, bool FAST>
+template <int MODE, int FLAGS, bool FAST, int KJ>
 __device__ __forceinline__ double sep_phi_wsum(const SepLane& L, const dbl2* CS, const dbl2* BP, const dbl2* W) {
   constexpr int FL = (MODE == GRAD) ? SEP_GRAD : (MODE == CE || MODE == PTM) ? SEP_CE : (MODE == PTB) ? SEP_PTB : SEP_FEQ;
   constexpr bool REG = (FLAGS & F_REG) != 0, OUT = (FLAGS & F_OUT) != 0;
@@ -542,9 +541,9 @@ __device__ __forceinline__ double sep_phi_wsum(const SepLane& L, const dbl2* CS,
   if (FAST && IS3D_PAIR_RCP) {
     dbl2 c0 = CS[0], b0 = BP[0], c1 = CS[1], b1 = BP[1];
 #pragma unroll
-    for (int jj = 0; jj < kJmax; jj += 2) {
+    for (int jj = 0; jj < KJ; jj += 2) {
       dbl2 n0 = c0, m0 = b0, n1 = c1, m1 = b1;
-      if (jj + 2 < kJmax) { n0 = CS[jj + 2]; m0 = BP[jj + 2]; n1 = CS[jj + 3]; m1 = BP[jj + 3]; }
+      if (jj + 2 < KJ) { n0 = CS[jj + 2]; m0 = BP[jj + 2]; n1 = CS[jj + 3]; m1 = BP[jj + 3]; }
       const dbl2 w = W[jj >> 1];
       double v0, v1;
       sep_pair_t<FL, REG, OUT>(L, c0, b0, c1, b1, v0, v1);
@@ -554,7 +553,7 @@ __device__ __forceinline__ double sep_phi_wsum(const SepLane& L, const dbl2* CS,
     return a0 + a1;
   }
 #pragma unroll
-  for (int jj = 0; jj < kJmax; jj += 2) {
+  for (int jj = 0; jj < KJ; jj += 2) {
     const dbl2 w = W[jj >> 1];
     a0 = fma(w.x, sep_point_t<FL, REG, OUT, FAST>(L, CS[jj], BP[jj]), a0);
     a1 = fma(w.y, sep_point_t<FL, REG, OUT, FAST>(L, CS[jj + 1], BP[jj + 1]), a1);
@@ -562,15 +561,15 @@ __device__ __forceinline__ double sep_phi_wsum(const SepLane& L, const dbl2* CS,
   return a0 + a1;
 }
 
-template <int FLAGS, bool CLAMP>
+template <int FLAGS, bool CLAMP, int KJ>
 __device__ __forceinline__ double mod_phi_wsum(const ModLane& M, const dbl2* CS, const dbl2* QV, const dbl2* W) {
   constexpr bool OUT = (FLAGS & F_OUT) != 0;
   double a0 = 0.0, a1 = 0.0;
   dbl2 c0 = CS[0], c1 = CS[1], q = QV[0];
 #pragma unroll
-  for (int jj = 0; jj < kJmax; jj += 2) {
+  for (int jj = 0; jj < KJ; jj += 2) {
     dbl2 n0 = c0, n1 = c1, nq = q;
-    if (jj + 2 < kJmax) { n0 = CS[jj + 2]; n1 = CS[jj + 3]; nq = QV[(jj >> 1) + 1]; }
+    if (jj + 2 < KJ) { n0 = CS[jj + 2]; n1 = CS[jj + 3]; nq = QV[(jj >> 1) + 1]; }
     const dbl2 w = W[jj >> 1];
     double v0, v1;
     mod_pair_t<OUT, CLAMP>(M, c0, c1, q, v0, v1);
@@ -599,10 +598,10 @@ struct DndxArgs {
 // k_spectra.  The momentum loop (pT) is inside: per (cell tile, pT) the {b', Phi} phi-terms are rebuilt
 // in LDS and every lane adds w_pT x sum_phi w_phi (point) into its column of s_red; after the pT loop a
 // species' slot columns are summed in slot order.  No atomics: bit-reproducible.
-template <int MODE, int FLAGS>
+template <int MODE, int FLAGS, int KJ>
 __global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_dndx(DndxArgs A) {
   extern __shared__ double smem[];
-  const int nphp = A.njb * kJmax;
+  const int nphp = A.njb * KJ;
   double* s_rec = smem;                                   // [kTile][NREC]
   dbl2* s_trig = (dbl2*)(s_rec + kTile * NREC);           // [nphp] {cos, sin}
   dbl2* s_cs = s_trig + nphp;                             // [nphp] {pT cos, pT sin} of the current pT
@@ -699,7 +698,7 @@ __global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_dndx(DndxArgs
         double cell = 0.0;
         for (int task = slot; task < A.ntask; task += nslot) {
           const int kk = task / A.nl, l = task % A.nl;
-          const int k = kk % A.nk, jb = kk / A.nk, j0 = jb * kJmax;
+          const int k = kk % A.nk, jb = kk / A.nk, j0 = jb * KJ;
           const double* Y = s_y + ((long)t * A.nq + k * A.nl + l) * kYRow;
           const dbl2* BP = s_bp + t * nphp + j0;
           const dbl2* W = (const dbl2*)(s_w + j0);
@@ -708,14 +707,15 @@ __global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_dndx(DndxArgs
             SepLane L;
             sep_setup(sep_flavor(MODE), R, Y, mT, mT2, m2, mTb, pT, sign, baryon, s_etab, L);
             if (L.skip) continue;
-            cell += L.fast ? sep_phi_wsum<MODE, FLAGS, true>(L, s_cs + j0, BP, W)
-                           : sep_phi_wsum<MODE, FLAGS, false>(L, s_cs + j0, BP, W);
+            cell += L.fast ? sep_phi_wsum<MODE, FLAGS, true, KJ>(L, s_cs + j0, BP, W)
+                           : sep_phi_wsum<MODE, FLAGS, false, KJ>(L, s_cs + j0, BP, W);
           } else if (MODE >= PTM) {
             ModLane M;
             mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, s_etab, M);
             if (M.skip) continue;
             const dbl2* QV = (const dbl2*)(s_qv + t * nphp + j0);
-            cell += M.clamp ? mod_phi_wsum<FLAGS, true>(M, s_cs + j0, QV, W) : mod_phi_wsum<FLAGS, false>(M, s_cs + j0, QV, W);
+            cell += M.clamp ? mod_phi_wsum<FLAGS, true, KJ>(M, s_cs + j0, QV, W)
+                            : mod_phi_wsum<FLAGS, false, KJ>(M, s_cs + j0, QV, W);
           }
         }
         s_red[t * kBlock + tid] = fma(wpT, cell, s_red[t * kBlock + tid]);
@@ -1494,13 +1494,23 @@ extern "C" int is3d_calculate_spectra(is3d_engine* e, double* dN_out) {
   return IS3D_OK;
 }
 
-template <int MODE>
-static void launch_dndx(dim3 grid, size_t shmem, hipStream_t st, const DndxArgs& a, int flags) {
+template <int MODE, int KJ>
+static void launch_dndx_kj(dim3 grid, size_t shmem, hipStream_t st, const DndxArgs& a, int flags) {
   switch (flags) {
-    case 0: hipLaunchKernelGGL((k_dndx<MODE, 0>), grid, dim3(kBlock), shmem, st, a); break;
-    case 1: hipLaunchKernelGGL((k_dndx<MODE, 1>), grid, dim3(kBlock), shmem, st, a); break;
-    case 2: hipLaunchKernelGGL((k_dndx<MODE, 2>), grid, dim3(kBlock), shmem, st, a); break;
-    default: hipLaunchKernelGGL((k_dndx<MODE, 3>), grid, dim3(kBlock), shmem, st, a); break;
+    case 0: hipLaunchKernelGGL((k_dndx<MODE, 0, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+    case 1: hipLaunchKernelGGL((k_dndx<MODE, 1, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+    case 2: hipLaunchKernelGGL((k_dndx<MODE, 2, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+    default: hipLaunchKernelGGL((k_dndx<MODE, 3, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+  }
+}
+
+template <int MODE>
+static void launch_dndx(dim3 grid, size_t shmem, hipStream_t st, const DndxArgs& a, int flags, int kj) {
+  switch (kj) {
+    case 32: launch_dndx_kj<MODE, 32>(grid, shmem, st, a, flags); break;
+    case 24: launch_dndx_kj<MODE, 24>(grid, shmem, st, a, flags); break;
+    case 8: launch_dndx_kj<MODE, 8>(grid, shmem, st, a, flags); break;
+    default: launch_dndx_kj<MODE, 2>(grid, shmem, st, a, flags); break;
   }
 }
 
@@ -1561,7 +1571,8 @@ extern "C" int is3d_calculate_dN_dX(is3d_engine* e, double* dN_taudtaudy, double
   HIPCHK(e, hipEventRecord(e->ev[1], st));
   if (n > 0) {
     // --- per-(species, cell) yields
-    const int njb = (nphi + kJmax - 1) / kJmax;
+    const int KJ = spectra_kj(nphi);
+    const int njb = (nphi + KJ - 1) / KJ;
     DndxArgs da{};
     da.ntask = nk * njb * nl;
     da.Sl = std::min(np, 64);
@@ -1577,7 +1588,7 @@ extern "C" int is3d_calculate_dN_dX(is3d_engine* e, double* dN_taudtaudy, double
     da.pT = e->d_pT; da.pTw = e->d_pTw; da.cphi = e->d_cphi; da.sphi = e->d_sphi; da.phiw = e->d_phiw;
     da.yv = e->d_y; da.etav = e->d_eta; da.etaw = e->d_etaw;
     da.npart = np; da.npT = npT; da.nphi = nphi; da.nk = nk; da.nl = nl; da.nq = nk * nl; da.njb = njb; da.dim = dim;
-    const size_t nphp = (size_t)njb * kJmax;
+    const size_t nphp = (size_t)njb * KJ;
     const size_t shmem = sizeof(double) * ((size_t)kTile * NREC + 2 * nphp + 2 * nphp + nphp + 3 * (size_t)kTile * nphp +
                                            (size_t)kTile * kBlock + (size_t)(nk + 2 * nl) + (size_t)kTile * da.nq * kYRow + 64);
     if (shmem > 160 * 1024) return e->fail(IS3D_ERR_ARG, "momentum grid too large for the LDS tile");
@@ -1585,10 +1596,10 @@ extern "C" int is3d_calculate_dN_dX(is3d_engine* e, double* dN_taudtaudy, double
     if (nwg > 0x7fffffffL) return e->fail(IS3D_ERR_ARG, "surface too large for one dN/dX launch");
     const int kflags = (e->p.regulate_deltaf ? F_REG : 0) | (e->p.outflow ? F_OUT : 0);
     switch (mode) {
-      case GRAD: launch_dndx<GRAD>(dim3((unsigned)nwg), shmem, st, da, kflags); break;
-      case CE: launch_dndx<CE>(dim3((unsigned)nwg), shmem, st, da, kflags); break;
-      case PTM: launch_dndx<PTM>(dim3((unsigned)nwg), shmem, st, da, kflags); break;
-      default: launch_dndx<PTB>(dim3((unsigned)nwg), shmem, st, da, kflags); break;
+      case GRAD: launch_dndx<GRAD>(dim3((unsigned)nwg), shmem, st, da, kflags, KJ); break;
+      case CE: launch_dndx<CE>(dim3((unsigned)nwg), shmem, st, da, kflags, KJ); break;
+      case PTM: launch_dndx<PTM>(dim3((unsigned)nwg), shmem, st, da, kflags, KJ); break;
+      default: launch_dndx<PTB>(dim3((unsigned)nwg), shmem, st, da, kflags, KJ); break;
     }
     HIPCHK(e, hipGetLastError());
     e->ycell_n = n;
