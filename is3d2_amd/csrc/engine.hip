@@ -39,7 +39,7 @@ constexpr int kBlock = 256;
 #endif
 constexpr int kTile = IS3D_KTILE;   // cells per LDS tile
 // waves per SIMD the spectra kernel is register-allocated for (measured on MI355X, config2):
-// Grad runs best at 3 (168 VGPRs), RTA-CE and the modified-momentum modes at 2 (no spills)
+// Grad and RTA-CE run best at 3 (168 VGPRs), the modified-momentum modes at 2
 #ifndef IS3D_SPECTRA_WAVES_SEP
 #define IS3D_SPECTRA_WAVES_SEP 3
 #endif
@@ -47,13 +47,17 @@ constexpr int kTile = IS3D_KTILE;   // cells per LDS tile
 #define IS3D_SPECTRA_WAVES_MOD 2
 #endif
 #ifndef IS3D_SPECTRA_WAVES_CE
-#define IS3D_SPECTRA_WAVES_CE 2      // RTA-CE: 2 (no spills) beat 3 (53 spilled VGPRs) by 7% on MI355X (profiles/round1_r1n_ab_ce.log)
+#define IS3D_SPECTRA_WAVES_CE 3      // RTA-CE: 3 (16 spilled VGPRs, 3 scratch accesses per 32 points) beat 2 by 4.3% once
+                                     // the lane setup shrank (profiles/round1_r1z_ab_ce3.log; 2 won before, r1n)
 #endif
 // waves per SIMD of one spectra / dN/dX instantiation
 template <int MODE>
 constexpr int spectra_waves() {
   return MODE >= PTM ? IS3D_SPECTRA_WAVES_MOD : MODE == CE ? IS3D_SPECTRA_WAVES_CE : IS3D_SPECTRA_WAVES_SEP;
 }
+// k_dndx keeps RTA-CE at 2 (its pT loop holds more live state: 215 VGPRs)
+template <int MODE>
+constexpr int dndx_waves() { return MODE == CE ? 2 : spectra_waves<MODE>(); }
 
 // LDS row stride of the y-terms (doubles): NYT + 1 is odd, so the 8-byte stores of one y-term field
 // by consecutive lanes (rows 136 B apart) spread over the 64 banks instead of hitting two of them
@@ -213,8 +217,8 @@ constexpr int F_REG = 1, F_OUT = 2;
 #ifndef IS3D_SPLIT_BYTES
 #define IS3D_SPLIT_BYTES (2L << 20)   // record bytes per cell split (k_spectra grid sizing)
 #endif
-#ifndef IS3D_GRAD_NOPF
-#define IS3D_GRAD_NOPF 0      // 1: Grad fours without the one-quad-ahead prefetch (needed while Grad spilled)
+#ifndef IS3D_NOPF_MODES
+#define IS3D_NOPF_MODES 0     // bit m: mode m's fours skip the one-quad-ahead prefetch (register-starved builds)
 #endif
 #ifndef IS3D_QUAD_RCP
 #define IS3D_QUAD_RCP 1       // fast path: four phi points per reciprocal where sep_quads() says so
@@ -232,8 +236,8 @@ template <int MODE, int FLAGS, bool FAST, int KJ>
 __device__ __forceinline__ void sep_phi_loop(const SepLane& L, const dbl2* CS, const dbl2* BP, double* acc) {
   constexpr int FL = (MODE == GRAD) ? SEP_GRAD : (MODE == CE || MODE == PTM) ? SEP_CE : (MODE == PTB) ? SEP_PTB : SEP_FEQ;
   constexpr bool REG = (FLAGS & F_REG) != 0, OUT = (FLAGS & F_OUT) != 0;
-  if (FAST && IS3D_QUAD_RCP && IS3D_GRAD_NOPF && MODE == GRAD && sep_quads(MODE, KJ)) {
-    // Grad fours without the one-quad-ahead prefetch (for register-starved builds)
+  if (FAST && IS3D_QUAD_RCP && ((IS3D_NOPF_MODES >> MODE) & 1) && sep_quads(MODE, KJ)) {
+    // fours without the one-quad-ahead prefetch (for register-starved builds)
 #pragma unroll
     for (int jj = 0; jj < KJ; jj += 4) {
       dbl2 c[4], b[4];
@@ -599,7 +603,7 @@ struct DndxArgs {
 // in LDS and every lane adds w_pT x sum_phi w_phi (point) into its column of s_red; after the pT loop a
 // species' slot columns are summed in slot order.  No atomics: bit-reproducible.
 template <int MODE, int FLAGS, int KJ>
-__global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_dndx(DndxArgs A) {
+__global__ __launch_bounds__(kBlock, dndx_waves<MODE>()) void k_dndx(DndxArgs A) {
   extern __shared__ double smem[];
   const int nphp = A.njb * KJ;
   double* s_rec = smem;                                   // [kTile][NREC]
