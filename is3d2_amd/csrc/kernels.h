@@ -1,0 +1,612 @@
+// kernels.h -- the momentum-integral kernels (k_spectra: operation 1, k_dndx: operation 0), their
+// argument blocks and launchers.  The kernels and launchers are compiled one delta-f mode per
+// translation unit (spectra_tu.hip, built five times in parallel: 5 modes x 4 flag sets x 4 phi-block
+// sizes of each kernel no longer serialise the build); engine.hip (host side) sees declarations.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "cf_math.h"
+
+namespace is3d {
+namespace kern {
+
+constexpr int kBlock = 256;
+#ifndef IS3D_KTILE
+#define IS3D_KTILE 8
+#endif
+constexpr int kTile = IS3D_KTILE;   // cells per LDS tile
+// waves per SIMD the spectra kernel is register-allocated for (measured on MI355X, config2):
+// Grad and RTA-CE run best at 3 (168 VGPRs), the modified-momentum modes at 2
+#ifndef IS3D_SPECTRA_WAVES_SEP
+#define IS3D_SPECTRA_WAVES_SEP 3
+#endif
+#ifndef IS3D_SPECTRA_WAVES_MOD
+#define IS3D_SPECTRA_WAVES_MOD 2
+#endif
+#ifndef IS3D_SPECTRA_WAVES_CE
+#define IS3D_SPECTRA_WAVES_CE 3      // RTA-CE: 3 (16 spilled VGPRs, 3 scratch accesses per 32 points) beat 2 by 4.3% once
+                                     // the lane setup shrank (profiles/round1_r1z_ab_ce3.log; 2 won before, r1n)
+#endif
+// waves per SIMD of one spectra / dN/dX instantiation
+template <int MODE>
+constexpr int spectra_waves() {
+  return MODE >= PTM ? IS3D_SPECTRA_WAVES_MOD : MODE == CE ? IS3D_SPECTRA_WAVES_CE : IS3D_SPECTRA_WAVES_SEP;
+}
+// k_dndx keeps RTA-CE at 2 (its pT loop holds more live state: 215 VGPRs)
+template <int MODE>
+constexpr int dndx_waves() { return MODE == CE ? 2 : spectra_waves<MODE>(); }
+
+// LDS row stride of the y-terms (doubles): NYT + 1 is odd, so the 8-byte stores of one y-term field
+// by consecutive lanes (rows 136 B apart) spread over the 64 banks instead of hitting two of them
+// (a 128-B stride put every lane of a wave on the same bank pair: a 32-way conflict)
+constexpr int kYRow = NYT + 1;
+
+// ------------------------------------------------------------------------------------------
+// spectra kernel
+// ------------------------------------------------------------------------------------------
+struct SpecArgs {
+  const double* rec; long n;
+  const double* renorm;       // PTM: [c][s_sorted]
+  double* slab; long outsize;
+  const double *smass, *ssign, *sbaryon; const int* sorig;
+  const double *pT, *cphi, *sphi, *yv, *etav, *etaw;
+  int npart, npT, nphi, ny_out, nk, nl, nq, njb;
+  long ntask;                 // npart * nq * njb lanes per pT: (species, q = y x eta node, phi block)
+  long cells_per_split;
+  int nbx, nsplit;            // lane groups per pT, cell splits (1-D grid of nbx * npT * nsplit)
+  long sstride;               // doubles per slab: npT * nbx * KJ * kBlock
+  int regulate, outflow, dim;
+  int op;                     // 1 spectra / 0 spacetime (yterms variants)
+};
+
+// flag bits of the spectra kernel instantiation
+constexpr int F_REG = 1, F_OUT = 2;
+
+#ifndef IS3D_SPLIT_BYTES
+#define IS3D_SPLIT_BYTES (2L << 20)   // record bytes per cell split (k_spectra grid sizing)
+#endif
+#ifndef IS3D_NOPF_MODES
+#define IS3D_NOPF_MODES 0     // bit m: mode m's fours skip the one-quad-ahead prefetch (register-starved builds)
+#endif
+#ifndef IS3D_QUAD_RCP
+#define IS3D_QUAD_RCP 1       // fast path: four phi points per reciprocal where sep_quads() says so
+#endif
+#ifndef IS3D_MOD_QUAD
+#define IS3D_MOD_QUAD 1       // modified path: four phi points per reciprocal when KJ % 4 == 0
+#endif
+#ifndef IS3D_PAIR_RCP
+#define IS3D_PAIR_RCP 1       // fast path: two phi points per reciprocal (sep_pair_t)
+#endif
+
+
+struct DndxArgs {
+  const double* rec; long n;
+  const double* renorm;       // PTM: [c][s_sorted]
+  double* ycell;              // [npart (sorted)][n]: sum over (pT, phi, y, eta) of w_pT w_phi w_eta p.dsigma f
+  const double *smass, *ssign, *sbaryon;
+  const double *pT, *pTw, *cphi, *sphi, *phiw, *yv, *etav, *etaw;
+  int npart, npT, nphi, nk, nl, nq, njb;
+  int Sl, Yl, ntask, nbx;     // species per wavefront, task slots per wavefront, tasks per species
+                              // (y x phi block x eta node), species groups
+  long cells_per_wg, nchunk;
+  int dim;
+};
+
+template <int MODE>
+void launch_spectra(dim3 grid, size_t shmem, hipStream_t st, const SpecArgs& a, int flags, int kj);
+template <int MODE>
+void launch_dndx(dim3 grid, size_t shmem, hipStream_t st, const DndxArgs& a, int flags, int kj);
+
+#ifdef IS3D_KERNEL_DEFS
+// The kernels and their helpers have internal linkage (unnamed namespace): with external linkage the
+// AMDGPU backend must keep them callable from elsewhere and allocated Grad's k_spectra 35 spilled
+// VGPRs + 60 spilled SGPRs (11% slower on MI355X) where the internal-linkage build spills nothing.
+namespace {
+// 32 phi points of one lane; the next points' LDS pairs are loaded before the current ones are
+// evaluated so the LDS latency overlaps the FP64 chain
+template <int MODE, int FLAGS, bool FAST, int KJ>
+__device__ __forceinline__ void sep_phi_loop(const SepLane& L, const dbl2* CS, const dbl2* BP, double* acc) {
+  constexpr int FL = (MODE == GRAD) ? SEP_GRAD : (MODE == CE || MODE == PTM) ? SEP_CE : (MODE == PTB) ? SEP_PTB : SEP_FEQ;
+  constexpr bool REG = (FLAGS & F_REG) != 0, OUT = (FLAGS & F_OUT) != 0;
+  if (FAST && IS3D_QUAD_RCP && ((IS3D_NOPF_MODES >> MODE) & 1) && sep_quads(MODE, KJ)) {
+    // fours without the one-quad-ahead prefetch (for register-starved builds)
+#pragma unroll
+    for (int jj = 0; jj < KJ; jj += 4) {
+      dbl2 c[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) { c[i] = CS[jj + i]; b[i] = BP[jj + i]; }
+      double v[4];
+      sep_quad_t<FL, REG, OUT>(L, c, b, v);
+#pragma unroll
+      for (int i = 0; i < 4; i++) acc[jj + i] += v[i];
+    }
+    return;
+  }
+  if (FAST && IS3D_QUAD_RCP && sep_quads(MODE, KJ)) {
+    dbl2 c[4], b[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) { c[i] = CS[i]; b[i] = BP[i]; }
+#pragma unroll
+    for (int jj = 0; jj < KJ; jj += 4) {
+      dbl2 nc[4], nb[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        nc[i] = c[i]; nb[i] = b[i];
+        if (jj + 4 < KJ) { nc[i] = CS[jj + 4 + i]; nb[i] = BP[jj + 4 + i]; }
+      }
+      double v[4];
+      sep_quad_t<FL, REG, OUT>(L, c, b, v);
+#pragma unroll
+      for (int i = 0; i < 4; i++) { acc[jj + i] += v[i]; c[i] = nc[i]; b[i] = nb[i]; }
+    }
+    return;
+  }
+  if (FAST && IS3D_PAIR_RCP) {
+    dbl2 c0 = CS[0], b0 = BP[0], c1 = CS[1], b1 = BP[1];
+#pragma unroll
+    for (int jj = 0; jj < KJ; jj += 2) {   // phi rows are padded to a multiple of KJ
+      dbl2 n0 = c0, m0 = b0, n1 = c1, m1 = b1;
+      if (jj + 2 < KJ) { n0 = CS[jj + 2]; m0 = BP[jj + 2]; n1 = CS[jj + 3]; m1 = BP[jj + 3]; }
+      double v0, v1;
+      sep_pair_t<FL, REG, OUT>(L, c0, b0, c1, b1, v0, v1);
+      acc[jj] += v0; acc[jj + 1] += v1;
+      c0 = n0; b0 = m0; c1 = n1; b1 = m1;
+    }
+    return;
+  }
+  dbl2 c = CS[0], b = BP[0];
+#pragma unroll
+  for (int jj = 0; jj < KJ; jj++) {
+    dbl2 cn = c, bn = b;
+    if (jj + 1 < KJ) { cn = CS[jj + 1]; bn = BP[jj + 1]; }
+    acc[jj] += sep_point_t<FL, REG, OUT, FAST>(L, c, b);
+    c = cn; b = bn;
+  }
+}
+
+template <int FLAGS, bool CLAMP, int KJ>
+__device__ __forceinline__ void mod_phi_loop(const ModLane& M, const dbl2* CS, const dbl2* QV, double* acc) {
+  constexpr bool OUT = (FLAGS & F_OUT) != 0;
+  if (IS3D_MOD_QUAD && KJ % 4 == 0) {
+    dbl2 c[4], qa = QV[0], qb = QV[1];
+#pragma unroll
+    for (int i = 0; i < 4; i++) c[i] = CS[i];
+#pragma unroll
+    for (int jj = 0; jj < KJ; jj += 4) {
+      dbl2 nc[4], na = qa, nb = qb;
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        nc[i] = c[i];
+        if (jj + 4 < KJ) nc[i] = CS[jj + 4 + i];
+      }
+      if (jj + 4 < KJ) { na = QV[(jj >> 1) + 2]; nb = QV[(jj >> 1) + 3]; }
+      double v[4];
+      mod_quad_t<OUT, CLAMP>(M, c, qa, qb, v);
+#pragma unroll
+      for (int i = 0; i < 4; i++) { acc[jj + i] += v[i]; c[i] = nc[i]; }
+      qa = na; qb = nb;
+    }
+    return;
+  }
+  dbl2 c0 = CS[0], c1 = CS[1], q = QV[0];
+#pragma unroll
+  for (int jj = 0; jj < KJ; jj += 2) {
+    dbl2 n0 = c0, n1 = c1, nq = q;
+    if (jj + 2 < KJ) { n0 = CS[jj + 2]; n1 = CS[jj + 3]; nq = QV[(jj >> 1) + 1]; }
+    double v0, v1;
+    mod_pair_t<OUT, CLAMP>(M, c0, c1, q, v0, v1);
+    acc[jj] += v0; acc[jj + 1] += v1;
+    c0 = n0; c1 = n1; q = nq;
+  }
+}
+
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations (lgkmcnt) but
+// not for its outstanding global loads -- a __syncthreads() (or a workgroup release fence) would
+// also wait for vmcnt(0) and drain the next tile's record copy.  The empty asm statements with a
+// memory clobber keep the compiler from moving LDS accesses across the barrier.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// dbl2 pairs of one record tile (kTile consecutive records of NREC doubles)
+constexpr int kTilePairs = kTile * NREC / 2;
+
+// Async copy of the record tile starting at cell cb into LDS (global_load_lds_dwordx4: no VGPR
+// staging; the LDS destination of a wave-instruction is base + 16 * lane, so the tile lands
+// in the same linear order as the records in HBM).  Completion is tracked by vmcnt.
+__device__ __forceinline__ void fetch_tile(const double* rec, long cb, long c_end, double* dst) {
+  const int tid = threadIdx.x;
+  const long lim = (min(c_end, cb + kTile) - cb) * (NREC / 2);
+  for (int base = 0; base < kTilePairs; base += kBlock) {
+    const int e = base + tid;
+    const int wave0 = base + (tid & ~63);
+    if (e < lim)
+      __builtin_amdgcn_global_load_lds((const void*)(rec + (cb * (NREC / 2) + e) * 2),
+                                       (__attribute__((address_space(3))) void*)(dst + 2 * wave0), 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ void wait_fetch() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// KJ = phi points per lane (an even divisor-friendly block: 32, 24, 8 or 2, spectra_kj); a lane owns one
+// (species, q, phi block) with q = (y, eta node): in 2+1D the eta nodes are spread over lanes and
+// summed by k_reduce, so a few species still fill the wavefronts
+template <int MODE, int FLAGS, int KJ>
+__global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_spectra(SpecArgs A) {
+  extern __shared__ double smem[];
+  const int nphp = A.njb * KJ;                            // phi rows padded to KJ multiples
+  double* s_recb = smem;                                  // [2][kTile][NREC] double-buffered
+  dbl2* s_trig = (dbl2*)(s_recb + 2 * kTile * NREC);      // [nphp]        {cos, sin}
+  dbl2* s_cs = s_trig + nphp;                             // [nphp]        {pT cos, pT sin}
+  dbl2* s_bp = s_cs + nphp;                               // [kTile][nphp] {b', Phi}
+  double* s_qv = (double*)(s_bp + kTile * nphp);         // [kTile][nphp]  Qv (modified path)
+  double* s_grid = s_qv + kTile * nphp;                   // y[nk] | eta[nl] | eta_w[nl]
+  double* s_y = s_grid + A.nk + 2 * A.nl;                 // [kTile][nq][kYRow]
+  double* s_etab = s_y + (long)kTile * A.nq * kYRow;      // [64] exp_tab's 2^(j/64)
+
+  const int tid = threadIdx.x;
+  if (tid < 64) s_etab[tid] = kExp2Tab64[tid];
+  // XCD-aware block order (cdna_hip_programming.md T1): blocks that share an XCD (same
+  // blockIdx % 8) take one contiguous range of logical ids, and logical ids run split-major, so
+  // each XCD's L2 sees only its own cell splits (sized to fit) instead of every split
+  const long nwg = (long)A.nbx * A.npT * A.nsplit;
+  const long bid = blockIdx.x, q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
+  const long lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int lane_group = (int)(lid % A.nbx);
+  const int ipt = (int)((lid / A.nbx) % A.npT);
+  const int split = (int)(lid / ((long)A.nbx * A.npT));
+  const double pT = A.pT[ipt];
+  const long task = (long)lane_group * kBlock + tid;
+  const bool active = task < A.ntask;
+  int s = 0, q = 0, jb = 0;
+  if (active) {
+    s = (int)(task % A.npart);
+    const long r = task / A.npart;
+    q = (int)(r % A.nq);
+    jb = (int)(r / A.nq);
+  }
+  const int j0 = jb * KJ;
+  const double mass = A.smass[s], m2 = mass * mass, sign = A.ssign[s], baryon = A.sbaryon[s];
+  const double mT = sqrt(m2 + pT * pT), mT2 = mT * mT, mTb = mT * baryon;
+
+  // per-workgroup constants into LDS: inside the cell loop the only global loads are the
+  // record prefetch (and PTM's renormalisation factor)
+  for (int j = tid; j < nphp; j += kBlock) {
+    const bool in = j < A.nphi;
+    const double c = in ? A.cphi[j] : 0.0, sn = in ? A.sphi[j] : 0.0;
+    dbl2 v; v.x = c; v.y = sn;
+    s_trig[j] = v;
+    v.x = pT * c; v.y = pT * sn;
+    s_cs[j] = v;
+  }
+  for (int i = tid; i < A.nk; i += kBlock) s_grid[i] = (A.dim == 3) ? A.yv[i] : 0.0;
+  for (int i = tid; i < A.nl; i += kBlock) {
+    s_grid[A.nk + i] = (A.dim == 3) ? 0.0 : A.etav[i];
+    s_grid[A.nk + A.nl + i] = (A.dim == 3) ? 1.0 : A.etaw[i];
+  }
+
+  double acc[KJ];
+#pragma unroll
+  for (int jj = 0; jj < KJ; jj++) acc[jj] = 0.0;
+
+  const long c_begin = (long)split * A.cells_per_split;
+  const long c_end = min(A.n, c_begin + A.cells_per_split);
+
+  // record tiles: tile i lives in buffer i & 1; tile i + 1 is copied in while tile i is integrated
+  if (c_begin < c_end) fetch_tile(A.rec, c_begin, c_end, s_recb);
+  int buf = 0;
+  for (long cb = c_begin; cb < c_end; cb += kTile, buf ^= 1) {
+    const int nt = (int)min((long)kTile, c_end - cb);
+    double* s_rec = s_recb + buf * (kTile * NREC);
+    wait_fetch();
+    lds_barrier();     // tile cb visible to all waves; everyone is done with the previous tile
+    if (cb + kTile < c_end) fetch_tile(A.rec, cb + kTile, c_end, s_recb + (buf ^ 1) * (kTile * NREC));
+    for (int idx = tid; idx < nt * nphp; idx += kBlock) {
+      const int t = idx / nphp, j = idx % nphp;
+      const double* R = s_rec + t * NREC;
+      dbl2 v; v.x = 0.0; v.y = 0.0;                        // padding: finite, never written out
+      double qv = 0.0;
+      if (j < A.nphi && R[R_KIND] != 0.0) {
+        const dbl2 tr = s_trig[j];
+        v = phiterms(MODE, R, pT, tr.x, tr.y, s_etab);
+        if (MODE >= PTM && R[R_KIND] == 2.0) qv = modqv(R, s_cs[j]);
+      }
+      s_bp[t * nphp + j] = v;
+      if (MODE >= PTM) s_qv[t * nphp + j] = qv;
+    }
+    for (int idx = tid; idx < nt * A.nq; idx += kBlock) {
+      const int t = idx / A.nq, q = idx % A.nq;
+      const double* R = s_rec + t * NREC;
+      if (R[R_KIND] != 0.0) {
+        const int kk = q / A.nl, l = q % A.nl;
+        const double y = s_grid[kk];
+        const double eta = (A.dim == 3) ? R[R_ETA] : s_grid[A.nk + l];
+        const double w = s_grid[A.nk + A.nl + l];
+        yterms(MODE, A.op, R, y, eta, w, s_y + ((long)t * A.nq + q) * kYRow);
+      }
+    }
+    lds_barrier();
+    if (active) {
+      for (int t = 0; t < nt; t++) {
+        const double* R = s_rec + t * NREC;
+        const double kind = R[R_KIND];
+        if (kind == 0.0) continue;
+        double rn_abs = R[R_RENORM];
+        if (MODE == PTM || MODE == PTB) {
+          const double rn = (MODE == PTM) ? A.renorm[(cb + t) * A.npart + s] : R[R_RENORM];
+          if (!isfinite(rn)) continue;    // species skipped (MomentumSpectra.cpp:828-832)
+          rn_abs = fabs(rn);
+        }
+        const dbl2* BP = s_bp + t * nphp + j0;
+        const double* Y = s_y + ((long)t * A.nq + q) * kYRow;
+        const bool sep = (MODE <= CE) || kind == 1.0 || Y[Y_NARROW] != 0.0;
+        if (sep) {
+          SepLane L;
+          sep_setup(sep_flavor(MODE), R, Y, mT, mT2, m2, mTb, pT, sign, baryon, s_etab, L);
+          if (L.skip) continue;
+          if (L.fast) sep_phi_loop<MODE, FLAGS, true, KJ>(L, s_cs + j0, BP, acc);
+          else sep_phi_loop<MODE, FLAGS, false, KJ>(L, s_cs + j0, BP, acc);
+        } else if (MODE >= PTM) {
+          ModLane M;
+          mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, s_etab, M);
+          if (M.skip) continue;
+          const dbl2* QV = (const dbl2*)(s_qv + t * nphp + j0);
+          if (M.clamp) mod_phi_loop<FLAGS, true, KJ>(M, s_cs + j0, QV, acc);
+          else mod_phi_loop<FLAGS, false, KJ>(M, s_cs + j0, QV, acc);
+        }
+      }
+    }
+  }
+  // partial sums, slab layout [split][pT][lane group][phi slot][lane]: every store of the wave is
+  // one contiguous 512-byte row; non-temporal so the stream does not evict the cell records the
+  // XCD's other workgroups are still reading from L2.  k_reduce scatters into the reference layout.
+  double* out = A.slab + (long)split * A.sstride + ((long)ipt * A.nbx + lane_group) * (KJ * kBlock) + tid;
+#pragma unroll
+  for (int jj = 0; jj < KJ; jj++) __builtin_nontemporal_store(acc[jj], out + jj * kBlock);
+}
+
+// ------------------------------------------------------------------------------------------
+// operation = 0: spacetime distributions dN/dX (SpacetimeDistribution.cpp:31-1250)
+// ------------------------------------------------------------------------------------------
+// Weighted phi sums: sum_j w_phi[j] x (w_eta p.dsigma f)(phi_j) for one lane and cell, with the
+// same per-point arithmetic as k_spectra (W = phi weights as {w_j, w_j+1} pairs, 0 in the padding).
+template <int MODE, int FLAGS, bool FAST, int KJ>
+__device__ __forceinline__ double sep_phi_wsum(const SepLane& L, const dbl2* CS, const dbl2* BP, const dbl2* W) {
+  constexpr int FL = (MODE == GRAD) ? SEP_GRAD : (MODE == CE || MODE == PTM) ? SEP_CE : (MODE == PTB) ? SEP_PTB : SEP_FEQ;
+  constexpr bool REG = (FLAGS & F_REG) != 0, OUT = (FLAGS & F_OUT) != 0;
+  double a0 = 0.0, a1 = 0.0;
+  if (FAST && IS3D_PAIR_RCP) {
+    dbl2 c0 = CS[0], b0 = BP[0], c1 = CS[1], b1 = BP[1];
+#pragma unroll
+    for (int jj = 0; jj < KJ; jj += 2) {
+      dbl2 n0 = c0, m0 = b0, n1 = c1, m1 = b1;
+      if (jj + 2 < KJ) { n0 = CS[jj + 2]; m0 = BP[jj + 2]; n1 = CS[jj + 3]; m1 = BP[jj + 3]; }
+      const dbl2 w = W[jj >> 1];
+      double v0, v1;
+      sep_pair_t<FL, REG, OUT>(L, c0, b0, c1, b1, v0, v1);
+      a0 = fma(w.x, v0, a0); a1 = fma(w.y, v1, a1);
+      c0 = n0; b0 = m0; c1 = n1; b1 = m1;
+    }
+    return a0 + a1;
+  }
+#pragma unroll
+  for (int jj = 0; jj < KJ; jj += 2) {
+    const dbl2 w = W[jj >> 1];
+    a0 = fma(w.x, sep_point_t<FL, REG, OUT, FAST>(L, CS[jj], BP[jj]), a0);
+    a1 = fma(w.y, sep_point_t<FL, REG, OUT, FAST>(L, CS[jj + 1], BP[jj + 1]), a1);
+  }
+  return a0 + a1;
+}
+
+template <int FLAGS, bool CLAMP, int KJ>
+__device__ __forceinline__ double mod_phi_wsum(const ModLane& M, const dbl2* CS, const dbl2* QV, const dbl2* W) {
+  constexpr bool OUT = (FLAGS & F_OUT) != 0;
+  double a0 = 0.0, a1 = 0.0;
+  dbl2 c0 = CS[0], c1 = CS[1], q = QV[0];
+#pragma unroll
+  for (int jj = 0; jj < KJ; jj += 2) {
+    dbl2 n0 = c0, n1 = c1, nq = q;
+    if (jj + 2 < KJ) { n0 = CS[jj + 2]; n1 = CS[jj + 3]; nq = QV[(jj >> 1) + 1]; }
+    const dbl2 w = W[jj >> 1];
+    double v0, v1;
+    mod_pair_t<OUT, CLAMP>(M, c0, c1, q, v0, v1);
+    a0 = fma(w.x, v0, a0); a1 = fma(w.y, v1, a1);
+    c0 = n0; c1 = n1; q = nq;
+  }
+  return a0 + a1;
+}
+
+
+
+// One workgroup = (species group of Sl mass-sorted species, cell chunk).  Lane = (species s_l, slot); the
+// 4 Yl slots of a workgroup stride over the species' tasks (y, phi block, eta node), so every wavefront
+// evaluates one task for Sl neighbouring species at a time -- the exp-underflow skip stays coherent as in
+// k_spectra.  The momentum loop (pT) is inside: per (cell tile, pT) the {b', Phi} phi-terms are rebuilt
+// in LDS and every lane adds w_pT x sum_phi w_phi (point) into its column of s_red; after the pT loop a
+// species' slot columns are summed in slot order.  No atomics: bit-reproducible.
+template <int MODE, int FLAGS, int KJ>
+__global__ __launch_bounds__(kBlock, dndx_waves<MODE>()) void k_dndx(DndxArgs A) {
+  extern __shared__ double smem[];
+  const int nphp = A.njb * KJ;
+  double* s_rec = smem;                                   // [kTile][NREC]
+  dbl2* s_trig = (dbl2*)(s_rec + kTile * NREC);           // [nphp] {cos, sin}
+  dbl2* s_cs = s_trig + nphp;                             // [nphp] {pT cos, pT sin} of the current pT
+  double* s_w = (double*)(s_cs + nphp);                   // [nphp] phi weights (0 in the padding)
+  dbl2* s_bp = (dbl2*)(s_w + nphp);                       // [kTile][nphp] {b', Phi} of the current pT
+  double* s_qv = (double*)(s_bp + kTile * nphp);         // [kTile][nphp] Qv of the current pT (modified path)
+  double* s_red = s_qv + kTile * nphp;                    // [kTile][kBlock] per-lane cell sums
+  double* s_grid = s_red + kTile * kBlock;                // y[nk] | eta[nl] | eta_w[nl]
+  double* s_y = s_grid + A.nk + 2 * A.nl;                 // [kTile][nq][kYRow]
+  double* s_etab = s_y + (long)kTile * A.nq * kYRow;      // [64] exp_tab's 2^(j/64)
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid < 64) s_etab[tid] = kExp2Tab64[tid];
+  const long nwg = (long)A.nbx * A.nchunk;
+  const long bid = blockIdx.x, q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
+  const long lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int grp = (int)(lid % A.nbx);
+  const long ch = lid / A.nbx;
+  const int s_l = lane % A.Sl, y_l = lane / A.Sl;
+  const int slot = wave * A.Yl + y_l, nslot = 4 * A.Yl;
+  const bool active = y_l < A.Yl && grp * A.Sl + s_l < A.npart;
+  const int s = active ? grp * A.Sl + s_l : 0;
+  const double mass = A.smass[s], m2 = mass * mass, sign = A.ssign[s], baryon = A.sbaryon[s];
+
+  for (int j = tid; j < nphp; j += kBlock) {
+    const bool in = j < A.nphi;
+    dbl2 v; v.x = in ? A.cphi[j] : 0.0; v.y = in ? A.sphi[j] : 0.0;
+    s_trig[j] = v;
+    s_w[j] = in ? A.phiw[j] : 0.0;
+  }
+  for (int i = tid; i < A.nk; i += kBlock) s_grid[i] = (A.dim == 3) ? A.yv[i] : 0.0;
+  for (int i = tid; i < A.nl; i += kBlock) {
+    s_grid[A.nk + i] = (A.dim == 3) ? 0.0 : A.etav[i];
+    s_grid[A.nk + A.nl + i] = (A.dim == 3) ? 1.0 : A.etaw[i];
+  }
+
+  const long c_begin = ch * A.cells_per_wg;
+  const long c_end = min(A.n, c_begin + A.cells_per_wg);
+  for (long cb = c_begin; cb < c_end; cb += kTile) {
+    const int nt = (int)min((long)kTile, c_end - cb);
+    __syncthreads();                                       // previous tile fully consumed
+    for (int i = tid; i < nt * NREC; i += kBlock) s_rec[i] = A.rec[cb * NREC + i];
+#pragma unroll
+    for (int t = 0; t < kTile; t++) s_red[t * kBlock + tid] = 0.0;
+    __syncthreads();
+    for (int idx = tid; idx < nt * A.nq; idx += kBlock) {
+      const int t = idx / A.nq, q = idx % A.nq;
+      const double* R = s_rec + t * NREC;
+      if (R[R_KIND] != 0.0) {
+        const int ky = q / A.nl, l = q % A.nl;
+        const double y = s_grid[ky];
+        const double eta = (A.dim == 3) ? R[R_ETA] : s_grid[A.nk + l];
+        const double w = s_grid[A.nk + A.nl + l];
+        yterms(MODE, 0, R, y, eta, w, s_y + ((long)t * A.nq + q) * kYRow);
+      }
+    }
+    for (int ipt = 0; ipt < A.npT; ipt++) {
+      const double pT = A.pT[ipt], wpT = A.pTw[ipt];
+      const double mT = sqrt(m2 + pT * pT), mT2 = mT * mT, mTb = mT * baryon;
+      __syncthreads();                                     // y-terms ready / previous pT's phi-terms consumed
+      for (int j = tid; j < nphp; j += kBlock) {
+        const dbl2 tr = s_trig[j];
+        dbl2 v; v.x = pT * tr.x; v.y = pT * tr.y;
+        s_cs[j] = v;
+      }
+      for (int idx = tid; idx < nt * nphp; idx += kBlock) {
+        const int t = idx / nphp, j = idx % nphp;
+        const double* R = s_rec + t * NREC;
+        dbl2 v; v.x = 0.0; v.y = 0.0;
+        double qv = 0.0;
+        if (j < A.nphi && R[R_KIND] != 0.0) {
+          const dbl2 tr = s_trig[j];
+          v = phiterms(MODE, R, pT, tr.x, tr.y, s_etab);
+          if (MODE >= PTM && R[R_KIND] == 2.0) {
+            dbl2 c; c.x = pT * tr.x; c.y = pT * tr.y;
+            qv = modqv(R, c);
+          }
+        }
+        s_bp[t * nphp + j] = v;
+        if (MODE >= PTM) s_qv[t * nphp + j] = qv;
+      }
+      __syncthreads();
+      if (!active) continue;
+      for (int t = 0; t < nt; t++) {
+        const double* R = s_rec + t * NREC;
+        const double kind = R[R_KIND];
+        if (kind == 0.0) continue;
+        double rn_abs = R[R_RENORM];
+        if (MODE == PTM || MODE == PTB) {
+          const double rn = (MODE == PTM) ? A.renorm[(cb + t) * A.npart + s] : R[R_RENORM];
+          if (!isfinite(rn)) continue;    // cell skipped for this species (SpacetimeDistribution.cpp:972-976)
+          rn_abs = fabs(rn);
+        }
+        double cell = 0.0;
+        for (int task = slot; task < A.ntask; task += nslot) {
+          const int kk = task / A.nl, l = task % A.nl;
+          const int k = kk % A.nk, jb = kk / A.nk, j0 = jb * KJ;
+          const double* Y = s_y + ((long)t * A.nq + k * A.nl + l) * kYRow;
+          const dbl2* BP = s_bp + t * nphp + j0;
+          const dbl2* W = (const dbl2*)(s_w + j0);
+          const bool sep = (MODE <= CE) || kind == 1.0 || Y[Y_NARROW] != 0.0;
+          if (sep) {
+            SepLane L;
+            sep_setup(sep_flavor(MODE), R, Y, mT, mT2, m2, mTb, pT, sign, baryon, s_etab, L);
+            if (L.skip) continue;
+            cell += L.fast ? sep_phi_wsum<MODE, FLAGS, true, KJ>(L, s_cs + j0, BP, W)
+                           : sep_phi_wsum<MODE, FLAGS, false, KJ>(L, s_cs + j0, BP, W);
+          } else if (MODE >= PTM) {
+            ModLane M;
+            mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, s_etab, M);
+            if (M.skip) continue;
+            const dbl2* QV = (const dbl2*)(s_qv + t * nphp + j0);
+            cell += M.clamp ? mod_phi_wsum<FLAGS, true, KJ>(M, s_cs + j0, QV, W)
+                            : mod_phi_wsum<FLAGS, false, KJ>(M, s_cs + j0, QV, W);
+          }
+        }
+        s_red[t * kBlock + tid] = fma(wpT, cell, s_red[t * kBlock + tid]);
+      }
+    }
+    __syncthreads();
+    // per (species, cell): sum of the species' slot columns in slot order (idle slots hold 0)
+    for (int idx = tid; idx < A.Sl * nt; idx += kBlock) {
+      const int sl = idx % A.Sl, t = idx / A.Sl;
+      const int s2 = grp * A.Sl + sl;
+      if (s2 >= A.npart) continue;
+      double acc = 0.0;
+      for (int w = 0; w < 4; w++)
+        for (int yl = 0; yl < A.Yl; yl++) acc += s_red[t * kBlock + w * 64 + yl * A.Sl + sl];
+      A.ycell[(long)s2 * A.n + cb + t] = acc;
+    }
+  }
+}
+
+}  // namespace
+
+template <int MODE, int KJ>
+void launch_spectra_kj(dim3 grid, size_t shmem, hipStream_t st, const SpecArgs& a, int flags) {
+  switch (flags) {
+    case 0: hipLaunchKernelGGL((k_spectra<MODE, 0, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+    case 1: hipLaunchKernelGGL((k_spectra<MODE, 1, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+    case 2: hipLaunchKernelGGL((k_spectra<MODE, 2, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+    default: hipLaunchKernelGGL((k_spectra<MODE, 3, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+  }
+}
+
+template <int MODE>
+void launch_spectra(dim3 grid, size_t shmem, hipStream_t st, const SpecArgs& a, int flags, int kj) {
+  switch (kj) {
+    case 32: launch_spectra_kj<MODE, 32>(grid, shmem, st, a, flags); break;
+    case 24: launch_spectra_kj<MODE, 24>(grid, shmem, st, a, flags); break;
+    case 8: launch_spectra_kj<MODE, 8>(grid, shmem, st, a, flags); break;
+    default: launch_spectra_kj<MODE, 2>(grid, shmem, st, a, flags); break;
+  }
+}
+
+
+template <int MODE, int KJ>
+void launch_dndx_kj(dim3 grid, size_t shmem, hipStream_t st, const DndxArgs& a, int flags) {
+  switch (flags) {
+    case 0: hipLaunchKernelGGL((k_dndx<MODE, 0, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+    case 1: hipLaunchKernelGGL((k_dndx<MODE, 1, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+    case 2: hipLaunchKernelGGL((k_dndx<MODE, 2, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+    default: hipLaunchKernelGGL((k_dndx<MODE, 3, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+  }
+}
+
+template <int MODE>
+void launch_dndx(dim3 grid, size_t shmem, hipStream_t st, const DndxArgs& a, int flags, int kj) {
+  switch (kj) {
+    case 32: launch_dndx_kj<MODE, 32>(grid, shmem, st, a, flags); break;
+    case 24: launch_dndx_kj<MODE, 24>(grid, shmem, st, a, flags); break;
+    case 8: launch_dndx_kj<MODE, 8>(grid, shmem, st, a, flags); break;
+    default: launch_dndx_kj<MODE, 2>(grid, shmem, st, a, flags); break;
+  }
+}
+
+#endif  // IS3D_KERNEL_DEFS
+
+}  // namespace kern
+}  // namespace is3d
