@@ -1089,15 +1089,17 @@ IS3D_HD double sep_fast_tail(const SepLane& L, dbl2 cs, dbl2 bp, double pds, dou
   return (OUT && pds <= 0.0) ? 0.0 : g;
 }
 
-// phi points per lane: the block size among 32, 24, 8, 2 with the least padding of the phi grid (ties
-// to the larger block, whose per-lane setup is spread over more points): 1 -> 2, 24 / 48 -> 24, 32 -> 32
+// phi points per lane: the block size among 32, 24, 8, 2 that minimises the padded points plus the
+// per-lane setup (~60 VALU ops, ~4.5 points' worth) of every block; ties to the larger block:
+// 1 -> 2, 16 -> 8, 24 / 48 -> 24, 32 -> 32, 100 -> 24
 IS3D_HD int spectra_kj(int nphi) {
+  const int cand[4] = {32, 24, 8, 2};
   int best = 32;
-  long best_pad = (long)((nphi + 31) / 32) * 32;
-  const int cand[3] = {24, 8, 2};
+  double best_cost = 1e300;
   for (int kj : cand) {
-    const long pad = (long)((nphi + kj - 1) / kj) * kj;
-    if (pad < best_pad) { best = kj; best_pad = pad; }
+    const long nb = (nphi + kj - 1) / kj;
+    const double cost = (double)(nb * kj) + 4.5 * (double)nb;
+    if (cost < best_cost) { best = kj; best_cost = cost; }
   }
   return best;
 }
