@@ -214,7 +214,7 @@ static_assert(NREC % 2 == 0, "records are moved as 16-byte pairs: keep NREC even
 // Y_S2, Y_S1, Y_SC1, Y_SS1, Y_L1: the (cell, y) factors of the separable lane coefficients
 // (sep_setup); Y_MUX..Y_MD, Y_NARROW: modified-momentum path.  Padded to 16 doubles.
 enum YT : int { Y_AT = 0, Y_A, Y_D, Y_WDX, Y_WDY, Y_S2, Y_S1, Y_SC1, Y_SS1, Y_L1,
-                Y_MUX, Y_MUY, Y_MUZ, Y_MD, Y_NARROW, Y_PAD, NYT };
+                Y_MUX, Y_MUY, Y_MUZ, Y_MD, Y_NARROW, Y_W, NYT };
 
 // surface field order (include/is3d_amd.h, is3d_surface)
 enum Surf : int {
@@ -938,7 +938,7 @@ IS3D_HD void yterms(int mode, int op, const double* R, double y, double eta, dou
   } else {
     Y[Y_MUX] = Y[Y_MUY] = Y[Y_MUZ] = Y[Y_MD] = Y[Y_NARROW] = 0.0;
   }
-  Y[Y_PAD] = 0.0;
+  Y[Y_W] = w;                      // w_eta (PD-table scale, sep_setup)
 }
 
 // phi-terms.  Everything the integrand needs per (cell, phi) except two numbers is linear in
@@ -982,6 +982,7 @@ struct SepLane {
   double c0;                   // PTB: constant added outside (1 - sign feq)
   double x, Zc, Zs;            // slow path: feq = 1/(exp(x - Zc pc - Zs ps) + sign)
   int skip, fast;
+  double escw;                 // 2^-k w_eta (PD-table scale)
 };
 
 // Per-(cell, q, species) setup for the separable integrand.  Returns skip=1 when every
@@ -1011,6 +1012,7 @@ IS3D_HD void sep_setup(int flavor, const double* R, const double* Y, double mT, 
   L.a = L.fast ? exp_tab(exp_tab_coef(), etab, xs * kInvLn2x64, k) : 0.0;
   const double esc = ldexp(1.0, -k);
   L.ssc = sign * esc;
+  L.escw = esc * Y[Y_W];
   if (!L.fast) { L.Zc = R[R_UX] * R[R_INVT]; L.Zs = R[R_UY] * R[R_INVT]; } else { L.Zc = L.Zs = 0.0; }
   L.D0 = esc * (mT * Y[Y_D]); L.Dc = esc * Y[Y_WDX]; L.Ds = esc * Y[Y_WDY];
   // fast lanes carry the delta-f coefficients pre-multiplied by a (see sep_fast_tail)
@@ -1179,6 +1181,79 @@ IS3D_HD void sep_pair(int flavor, const SepLane& L, dbl2 c0, dbl2 b0, dbl2 c1, d
   IS3D_PAIR_CASE(SEP_PTB)
   IS3D_PAIR_CASE(SEP_FEQ)
 #undef IS3D_PAIR_CASE
+}
+
+// p.dsigma b' table.  p.dsigma = mT Y_D + w_eta (dsigma_x pc + dsigma_y ps) (Y_D carries w_eta), so with
+//   PD = (dsigma_x pc + dsigma_y ps) b'        per (cell, phi), shared by every lane of the workgroup
+// a fast lane gets e^-S w p.dsigma b' = fma(D0, b', escw PD) (escw = 2^-k w_eta; D0 = 2^-k mT Y_D) in
+// two ops instead of two FMAs for p.dsigma and a multiply by b' (SC = false: a caller that knows
+// escw == 1 for the whole wave, one op).  The outflow cut tests p.dsigma b' <= 0: the same sign as
+// p.dsigma for b' > 0, and the point is 0 anyway at b' = 0.
+IS3D_HD double sep_pd(const double* R, dbl2 cs, double bpx) { return fma(R[R_DAX], cs.x, R[R_DAY] * cs.y) * bpx; }
+
+// sep_fast_tail with pb = p.dsigma b' given
+template <int FL, bool REG, bool OUT>
+IS3D_HD double sep_fast_tail_pb(const SepLane& L, dbl2 cs, dbl2 bp, double pb, double E, double rq) {
+  const bool needE = (FL == SEP_CE || FL == SEP_PTB);
+  const double w = needE ? pb * (E * rq) : pb * rq;
+  double g;
+  if (FL == SEP_FEQ) {
+    g = w;
+  } else {
+    double in = fma(L.a, bp.y, lin(L.S0, L.Sc, L.Ss, cs));
+    if (needE) in = fma(E, lin(L.L0, L.Lc, L.Ls, cs), in);
+    double t;
+    if (REG) {
+      double dfv = rq * in;
+      if (FL == SEP_PTB) dfv += L.c0;
+      t = 1.0 + fmax(-1.0, fmin(dfv, 1.0));
+    } else {
+      t = fma(rq, in, (FL == SEP_PTB) ? 1.0 + L.c0 : 1.0);
+    }
+    g = w * t;
+  }
+  return (OUT && pb <= 0.0) ? 0.0 : g;
+}
+
+// sep_quad_t with p.dsigma b' from the PD table (pd[i] = sep_pd of point i; SC: scale by escw)
+template <int FL, bool REG, bool OUT, bool SC = false>
+IS3D_HD void sep_quad_pd_t(const SepLane& L, const dbl2* c, const dbl2* b, const double* pd, double* v) {
+  const bool needE = (FL == SEP_CE || FL == SEP_PTB);
+  double pb[4], E[4], q[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    pb[i] = fma(L.D0, b[i].x, SC ? L.escw * pd[i] : pd[i]);
+    const double den = fma(L.ssc, b[i].x, L.a);
+    E[i] = needE ? lin(L.E0, L.Ec, L.Es, c[i]) : 1.0;
+    q[i] = needE ? den * E[i] : den;
+  }
+  const double q01 = q[0] * q[1], q23 = q[2] * q[3];
+  const double r = rcp1(q01 * q23);
+  const double r01 = r * q23, r23 = r * q01;
+  v[0] = sep_fast_tail_pb<FL, REG, OUT>(L, c[0], b[0], pb[0], E[0], r01 * q[1]);
+  v[1] = sep_fast_tail_pb<FL, REG, OUT>(L, c[1], b[1], pb[1], E[1], r01 * q[0]);
+  v[2] = sep_fast_tail_pb<FL, REG, OUT>(L, c[2], b[2], pb[2], E[2], r23 * q[3]);
+  v[3] = sep_fast_tail_pb<FL, REG, OUT>(L, c[3], b[3], pb[3], E[3], r23 * q[2]);
+}
+
+IS3D_HD void sep_quad_pd(int flavor, const SepLane& L, const dbl2* c, const dbl2* b, const double* pd, int regulate,
+                         int outflow, double* v) {
+#define IS3D_QUADPD_CASE(FLV)                                                                     \
+  if (flavor == FLV) {                                                                            \
+    if (regulate) {                                                                               \
+      if (outflow) sep_quad_pd_t<FLV, true, true, true>(L, c, b, pd, v);                              \
+      else sep_quad_pd_t<FLV, true, false, true>(L, c, b, pd, v);                                      \
+    } else {                                                                                      \
+      if (outflow) sep_quad_pd_t<FLV, false, true, true>(L, c, b, pd, v);                              \
+      else sep_quad_pd_t<FLV, false, false, true>(L, c, b, pd, v);                                      \
+    }                                                                                             \
+    return;                                                                                       \
+  }
+  IS3D_QUADPD_CASE(SEP_GRAD)
+  IS3D_QUADPD_CASE(SEP_CE)
+  IS3D_QUADPD_CASE(SEP_PTB)
+  IS3D_QUADPD_CASE(SEP_FEQ)
+#undef IS3D_QUADPD_CASE
 }
 
 IS3D_HD void sep_quad(int flavor, const SepLane& L, const dbl2* c, const dbl2* b, int regulate, int outflow, double* v) {

@@ -74,6 +74,12 @@ constexpr int F_REG = 1, F_OUT = 2;
 #ifndef IS3D_MOD_QUAD
 #define IS3D_MOD_QUAD 1       // modified path: four phi points per reciprocal when KJ % 4 == 0
 #endif
+#ifndef IS3D_PD_TABLE
+#define IS3D_PD_TABLE 1       // Grad / RTA-CE fast lanes: p.dsigma b' from the per-(cell, phi) PD table (sep_quad_pd_t)
+#endif
+#ifndef IS3D_PD_PREFETCH
+#define IS3D_PD_PREFETCH 0    // PD fours without the one-quad-ahead prefetch (with it Grad spilled 64 VGPRs)
+#endif
 #ifndef IS3D_PAIR_RCP
 #define IS3D_PAIR_RCP 1       // fast path: two phi points per reciprocal (sep_pair_t)
 #endif
@@ -161,6 +167,45 @@ __device__ __forceinline__ void sep_phi_loop(const SepLane& L, const dbl2* CS, c
     if (jj + 1 < KJ) { cn = CS[jj + 1]; bn = BP[jj + 1]; }
     acc[jj] += sep_point_t<FL, REG, OUT, FAST>(L, c, b);
     c = cn; b = bn;
+  }
+}
+
+// sep_phi_loop's fours for fast Grad / RTA-CE lanes with p.dsigma b' from the PD table (sep_quad_pd_t)
+template <int MODE, int FLAGS, int KJ, bool SC>
+__device__ __forceinline__ void sep_phi_loop_pd(const SepLane& L, const dbl2* CS, const dbl2* BP, const double* PD,
+                                                double* acc) {
+  constexpr int FL = (MODE == GRAD) ? SEP_GRAD : (MODE == CE || MODE == PTM) ? SEP_CE : (MODE == PTB) ? SEP_PTB : SEP_FEQ;
+  constexpr bool REG = (FLAGS & F_REG) != 0, OUT = (FLAGS & F_OUT) != 0;
+  if (!IS3D_PD_PREFETCH) {
+#pragma unroll
+    for (int jj = 0; jj < KJ; jj += 4) {
+      dbl2 c[4], b[4];
+      double pd[4], v[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) { c[i] = CS[jj + i]; b[i] = BP[jj + i]; pd[i] = PD[jj + i]; }
+      sep_quad_pd_t<FL, REG, OUT, SC>(L, c, b, pd, v);
+#pragma unroll
+      for (int i = 0; i < 4; i++) acc[jj + i] += v[i];
+    }
+    return;
+  }
+  dbl2 c[4], b[4];
+  double pd[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) { c[i] = CS[i]; b[i] = BP[i]; pd[i] = PD[i]; }
+#pragma unroll
+  for (int jj = 0; jj < KJ; jj += 4) {
+    dbl2 nc[4], nb[4];
+    double np[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      nc[i] = c[i]; nb[i] = b[i]; np[i] = pd[i];
+      if (jj + 4 < KJ) { nc[i] = CS[jj + 4 + i]; nb[i] = BP[jj + 4 + i]; np[i] = PD[jj + 4 + i]; }
+    }
+    double v[4];
+    sep_quad_pd_t<FL, REG, OUT, SC>(L, c, b, pd, v);
+#pragma unroll
+    for (int i = 0; i < 4; i++) { acc[jj + i] += v[i]; c[i] = nc[i]; b[i] = nb[i]; pd[i] = np[i]; }
   }
 }
 
@@ -314,7 +359,8 @@ __global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_spectra(SpecA
         if (MODE >= PTM && R[R_KIND] == 2.0) qv = modqv(R, s_cs[j]);
       }
       s_bp[t * nphp + j] = v;
-      if (MODE >= PTM) s_qv[t * nphp + j] = qv;
+      // s_qv holds Qv on the modified path and the PD table (sep_pd) for Grad / RTA-CE
+      s_qv[t * nphp + j] = (MODE >= PTM) ? qv : sep_pd(R, s_cs[j], v.x);
     }
     for (int idx = tid; idx < nt * A.nq; idx += kBlock) {
       const int t = idx / A.nq, q = idx % A.nq;
@@ -346,7 +392,10 @@ __global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_spectra(SpecA
           SepLane L;
           sep_setup(sep_flavor(MODE), R, Y, mT, mT2, m2, mTb, pT, sign, baryon, s_etab, L);
           if (L.skip) continue;
-          if (L.fast) sep_phi_loop<MODE, FLAGS, true, KJ>(L, s_cs + j0, BP, acc);
+          // wave-uniform choice (a mixed wave would run both loops): every active lane unscaled
+          if (IS3D_PD_TABLE && MODE <= CE && KJ % 4 == 0 && L.fast)
+            sep_phi_loop_pd<MODE, FLAGS, KJ, true>(L, s_cs + j0, BP, s_qv + t * nphp + j0, acc);
+          else if (L.fast) sep_phi_loop<MODE, FLAGS, true, KJ>(L, s_cs + j0, BP, acc);
           else sep_phi_loop<MODE, FLAGS, false, KJ>(L, s_cs + j0, BP, acc);
         } else if (MODE >= PTM) {
           ModLane M;

@@ -163,10 +163,18 @@ extern "C" int emu_spectra(const orc_params* p, const orc_setup* su, const orc_s
               // are multiples of 4) or pairs sharing one reciprocal (an odd tail point alone)
               int j = 0;
               if (L.fast) {
+                // k_spectra's PD-table fours (Grad / RTA-CE)
+                const bool pd = op != 0 && mode <= CE && spectra_kj(nphi) % 4 == 0;
                 if (op != 0 && sep_quads(mode, spectra_kj(nphi)))   // k_spectra; k_dndx pairs
                   for (; j + 3 < nphi; j += 4) {
                     double v[4];
-                    sep_quad(sep_flavor(mode), L, &CS[j], &BP[j], p->regulate_deltaf, p->outflow, v);
+                    if (pd) {
+                      double P[4];
+                      for (int i = 0; i < 4; i++) P[i] = sep_pd(R, CS[j + i], BP[j + i].x);
+                      sep_quad_pd(sep_flavor(mode), L, &CS[j], &BP[j], P, p->regulate_deltaf, p->outflow, v);
+                    } else {
+                      sep_quad(sep_flavor(mode), L, &CS[j], &BP[j], p->regulate_deltaf, p->outflow, v);
+                    }
                     for (int i = 0; i < 4; i++) a[j + i] += v[i];
                   }
                 for (; j + 1 < nphi; j += 2) {
