@@ -413,6 +413,7 @@ struct is3d_engine {
   DfTables dtb{};
   double* d_const = nullptr; size_t const_len = 0;    // species, grids, gla, pdg
   const double *d_smass = nullptr, *d_ssign = nullptr, *d_sbaryon = nullptr, *d_sdegen = nullptr, *d_degen_orig = nullptr;
+  const double* d_csg = nullptr;   // [npT][nphp] {pT cos, pT sin}
   const double *d_pT = nullptr, *d_cphi = nullptr, *d_sphi = nullptr, *d_y = nullptr, *d_eta = nullptr, *d_etaw = nullptr;
   const double *d_pTw = nullptr, *d_phiw = nullptr;
   const double *d_gla = nullptr;
@@ -691,6 +692,18 @@ static int finalize_tables(is3d_engine* e) {
   std::vector<double> pTw(e->pT.size(), 0.0), phiw(e->phi.size(), 0.0);
   if (e->have_weights) { pTw = e->pT_w; phiw = e->phi_w; }
   const size_t opw = cput(pTw.data(), pTw.size()), ophw = cput(phiw.data(), phiw.size());
+  // {pT cos phi, pT sin phi} per (pT, padded phi slot) for k_spectra's scalar loads (same products as
+  // its LDS copy s_cs); 16-byte aligned
+  if (cb.size() & 1) cb.push_back(0.0);
+  const int kj_cs = spectra_kj((int)e->phi.size());
+  const int nphp_cs = (int)((e->phi.size() + kj_cs - 1) / kj_cs) * kj_cs;
+  std::vector<double> csv((size_t)e->pT.size() * nphp_cs * 2, 0.0);
+  for (size_t i = 0; i < e->pT.size(); i++)
+    for (size_t j = 0; j < e->phi.size(); j++) {
+      csv[(i * nphp_cs + j) * 2] = e->pT[i] * cph[j];
+      csv[(i * nphp_cs + j) * 2 + 1] = e->pT[i] * sph[j];
+    }
+  const size_t ocs = cput(csv.data(), csv.size());
   const size_t og = cput(e->gla_r.data(), e->gla_r.size());
   cput(e->gla_w.data(), e->gla_w.size());
   const size_t opd = cput(e->pdg_mass.data(), e->pdg_mass.size());
@@ -711,6 +724,7 @@ static int finalize_tables(is3d_engine* e) {
   e->d_y = e->d_const + oy; e->d_eta = e->d_const + oe; e->d_etaw = e->d_const + ow;
   e->d_gla = e->d_const + og; e->d_pdg = e->d_const + opd;
   e->d_pTw = e->d_const + opw; e->d_phiw = e->d_const + ophw;
+  e->d_csg = e->d_const + ocs;
   e->tables_dirty = false;
   return IS3D_OK;
 }
@@ -869,6 +883,7 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   SpecArgs sa{};
   sa.rec = e->d_rec; sa.n = n; sa.renorm = e->d_renorm; sa.slab = e->d_slab; sa.outsize = outsize;
   sa.smass = e->d_smass; sa.ssign = e->d_ssign; sa.sbaryon = e->d_sbaryon; sa.sorig = e->d_sorig;
+  sa.csg = e->d_csg;
   sa.pT = e->d_pT; sa.cphi = e->d_cphi; sa.sphi = e->d_sphi; sa.yv = e->d_y; sa.etav = e->d_eta; sa.etaw = e->d_etaw;
   sa.npart = np; sa.npT = npT; sa.nphi = nphi; sa.ny_out = ny_out; sa.nk = nk; sa.nl = nl; sa.nq = nk * nl; sa.njb = njb;
   sa.ntask = ntask; sa.cells_per_split = cps; sa.nbx = (int)bx; sa.nsplit = (int)nsplit; sa.sstride = sstride;

@@ -50,6 +50,7 @@ struct SpecArgs {
   double* slab; long outsize;
   const double *smass, *ssign, *sbaryon; const int* sorig;
   const double *pT, *cphi, *sphi, *yv, *etav, *etaw;
+  const double* csg;          // [npT][nphp] {pT cos, pT sin} (read by scalar loads when njb == 1)
   int npart, npT, nphi, ny_out, nk, nl, nq, njb;
   long ntask;                 // npart * nq * njb lanes per pT: (species, q = y x eta node, phi block)
   long cells_per_split;
@@ -79,6 +80,9 @@ constexpr int F_REG = 1, F_OUT = 2;
 #endif
 #ifndef IS3D_PD_PREFETCH
 #define IS3D_PD_PREFETCH 0    // PD fours without the one-quad-ahead prefetch (with it Grad spilled 64 VGPRs)
+#endif
+#ifndef IS3D_CS_SCALAR
+#define IS3D_CS_SCALAR 1      // PD fours with one phi block: {pc, ps} by scalar loads (SGPR operands)
 #endif
 #ifndef IS3D_PAIR_RCP
 #define IS3D_PAIR_RCP 1       // fast path: two phi points per reciprocal (sep_pair_t)
@@ -170,9 +174,18 @@ __device__ __forceinline__ void sep_phi_loop(const SepLane& L, const dbl2* CS, c
   }
 }
 
+// {pc, ps} of phi slot k from LDS or, wave-uniform, from the constant address space (scalar loads)
+typedef const __attribute__((address_space(4))) double* cs_sptr;
+__device__ __forceinline__ dbl2 cs_at(const dbl2* p, int k) { return p[k]; }
+__device__ __forceinline__ dbl2 cs_at(cs_sptr p, int k) {
+  dbl2 v;
+  v.x = p[2 * k]; v.y = p[2 * k + 1];
+  return v;
+}
+
 // sep_phi_loop's fours for fast Grad / RTA-CE lanes with p.dsigma b' from the PD table (sep_quad_pd_t)
-template <int MODE, int FLAGS, int KJ, bool SC>
-__device__ __forceinline__ void sep_phi_loop_pd(const SepLane& L, const dbl2* CS, const dbl2* BP, const double* PD,
+template <int MODE, int FLAGS, int KJ, bool SC, typename CSP>
+__device__ __forceinline__ void sep_phi_loop_pd(const SepLane& L, CSP CS, const dbl2* BP, const double* PD,
                                                 double* acc) {
   constexpr int FL = (MODE == GRAD) ? SEP_GRAD : (MODE == CE || MODE == PTM) ? SEP_CE : (MODE == PTB) ? SEP_PTB : SEP_FEQ;
   constexpr bool REG = (FLAGS & F_REG) != 0, OUT = (FLAGS & F_OUT) != 0;
@@ -182,7 +195,7 @@ __device__ __forceinline__ void sep_phi_loop_pd(const SepLane& L, const dbl2* CS
       dbl2 c[4], b[4];
       double pd[4], v[4];
 #pragma unroll
-      for (int i = 0; i < 4; i++) { c[i] = CS[jj + i]; b[i] = BP[jj + i]; pd[i] = PD[jj + i]; }
+      for (int i = 0; i < 4; i++) { c[i] = cs_at(CS, jj + i); b[i] = BP[jj + i]; pd[i] = PD[jj + i]; }
       sep_quad_pd_t<FL, REG, OUT, SC>(L, c, b, pd, v);
 #pragma unroll
       for (int i = 0; i < 4; i++) acc[jj + i] += v[i];
@@ -192,7 +205,7 @@ __device__ __forceinline__ void sep_phi_loop_pd(const SepLane& L, const dbl2* CS
   dbl2 c[4], b[4];
   double pd[4];
 #pragma unroll
-  for (int i = 0; i < 4; i++) { c[i] = CS[i]; b[i] = BP[i]; pd[i] = PD[i]; }
+  for (int i = 0; i < 4; i++) { c[i] = cs_at(CS, i); b[i] = BP[i]; pd[i] = PD[i]; }
 #pragma unroll
   for (int jj = 0; jj < KJ; jj += 4) {
     dbl2 nc[4], nb[4];
@@ -200,7 +213,7 @@ __device__ __forceinline__ void sep_phi_loop_pd(const SepLane& L, const dbl2* CS
 #pragma unroll
     for (int i = 0; i < 4; i++) {
       nc[i] = c[i]; nb[i] = b[i]; np[i] = pd[i];
-      if (jj + 4 < KJ) { nc[i] = CS[jj + 4 + i]; nb[i] = BP[jj + 4 + i]; np[i] = PD[jj + 4 + i]; }
+      if (jj + 4 < KJ) { nc[i] = cs_at(CS, jj + 4 + i); nb[i] = BP[jj + 4 + i]; np[i] = PD[jj + 4 + i]; }
     }
     double v[4];
     sep_quad_pd_t<FL, REG, OUT, SC>(L, c, b, pd, v);
@@ -393,7 +406,12 @@ __global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_spectra(SpecA
           sep_setup(sep_flavor(MODE), R, Y, mT, mT2, m2, mTb, pT, sign, baryon, s_etab, L);
           if (L.skip) continue;
           // wave-uniform choice (a mixed wave would run both loops): every active lane unscaled
-          if (IS3D_PD_TABLE && MODE <= CE && KJ % 4 == 0 && L.fast)
+          if (IS3D_PD_TABLE && IS3D_CS_SCALAR && MODE <= CE && KJ % 4 == 0 && L.fast && A.njb == 1)
+            // one phi block: every lane reads the same {pc, ps}, so they come by scalar loads into SGPRs
+            // (VALU operands) instead of LDS
+            sep_phi_loop_pd<MODE, FLAGS, KJ, true>(L, (cs_sptr)A.csg + 2L * ipt * nphp,
+                                                   BP, s_qv + t * nphp, acc);
+          else if (IS3D_PD_TABLE && MODE <= CE && KJ % 4 == 0 && L.fast)
             sep_phi_loop_pd<MODE, FLAGS, KJ, true>(L, s_cs + j0, BP, s_qv + t * nphp + j0, acc);
           else if (L.fast) sep_phi_loop<MODE, FLAGS, true, KJ>(L, s_cs + j0, BP, acc);
           else sep_phi_loop<MODE, FLAGS, false, KJ>(L, s_cs + j0, BP, acc);
