@@ -84,6 +84,9 @@ constexpr int F_REG = 1, F_OUT = 2;
 #ifndef IS3D_CS_SCALAR
 #define IS3D_CS_SCALAR 1      // PD fours with one phi block: {pc, ps} by scalar loads (SGPR operands)
 #endif
+#ifndef IS3D_YQ_RANGE
+#define IS3D_YQ_RANGE 1       // k_spectra builds the y-terms of its lanes' q range only
+#endif
 #ifndef IS3D_PAIR_RCP
 #define IS3D_PAIR_RCP 1       // fast path: two phi points per reciprocal (sep_pair_t)
 #endif
@@ -326,6 +329,14 @@ __global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_spectra(SpecA
     jb = (int)(r / A.nq);
   }
   const int j0 = jb * KJ;
+  // q values this workgroup's lanes use: a contiguous range q0 .. q0 + nqw - 1 when its tasks lie in one
+  // phi block (the y-terms of the other q are not built), all nq otherwise
+  int q0 = 0, nqw = A.nq;
+  {
+    const long t0 = (long)lane_group * kBlock, t1 = min(A.ntask, t0 + kBlock) - 1;
+    const long r0 = t0 / A.npart, r1 = t1 / A.npart;
+    if (IS3D_YQ_RANGE && r0 / A.nq == r1 / A.nq) { q0 = (int)(r0 % A.nq); nqw = (int)(r1 - r0) + 1; }
+  }
   const double mass = A.smass[s], m2 = mass * mass, sign = A.ssign[s], baryon = A.sbaryon[s];
   const double mT = sqrt(m2 + pT * pT), mT2 = mT * mT, mTb = mT * baryon;
 
@@ -375,15 +386,15 @@ __global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_spectra(SpecA
       // s_qv holds Qv on the modified path and the PD table (sep_pd) for Grad / RTA-CE
       s_qv[t * nphp + j] = (MODE >= PTM) ? qv : sep_pd(R, s_cs[j], v.x);
     }
-    for (int idx = tid; idx < nt * A.nq; idx += kBlock) {
-      const int t = idx / A.nq, q = idx % A.nq;
+    for (int idx = tid; idx < nt * nqw; idx += kBlock) {
+      const int t = idx / nqw, qq = idx % nqw, q = q0 + qq;
       const double* R = s_rec + t * NREC;
       if (R[R_KIND] != 0.0) {
         const int kk = q / A.nl, l = q % A.nl;
         const double y = s_grid[kk];
         const double eta = (A.dim == 3) ? R[R_ETA] : s_grid[A.nk + l];
         const double w = s_grid[A.nk + A.nl + l];
-        yterms(MODE, A.op, R, y, eta, w, s_y + ((long)t * A.nq + q) * kYRow);
+        yterms(MODE, A.op, R, y, eta, w, s_y + ((long)t * nqw + qq) * kYRow);
       }
     }
     lds_barrier();
@@ -399,7 +410,7 @@ __global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_spectra(SpecA
           rn_abs = fabs(rn);
         }
         const dbl2* BP = s_bp + t * nphp + j0;
-        const double* Y = s_y + ((long)t * A.nq + q) * kYRow;
+        const double* Y = s_y + ((long)t * nqw + (q - q0)) * kYRow;
         const bool sep = (MODE <= CE) || kind == 1.0 || Y[Y_NARROW] != 0.0;
         if (sep) {
           SepLane L;
