@@ -305,10 +305,10 @@ __global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_spectra(SpecA
   double* s_qv = (double*)(s_bp + kTile * nphp);         // [kTile][nphp]  Qv (modified path)
   double* s_grid = s_qv + kTile * nphp;                   // y[nk] | eta[nl] | eta_w[nl]
   double* s_y = s_grid + A.nk + 2 * A.nl;                 // [kTile][nq][kYRow]
-  double* s_etab = s_y + (long)kTile * A.nq * kYRow;      // [64] exp_tab's 2^(j/64)
+  double* s_etab = s_y + (long)kTile * A.nq * kYRow;      // [kExpTabN] exp_tab's 2^(j/kExpTabN)
 
   const int tid = threadIdx.x;
-  if (tid < 64) s_etab[tid] = kExp2Tab64[tid];
+  for (int i = tid; i < kExpTabN; i += kBlock) s_etab[i] = kExp2Tab[i];
   // XCD-aware block order (cdna_hip_programming.md T1): blocks that share an XCD (same
   // blockIdx % 8) take one contiguous range of logical ids, and logical ids run split-major, so
   // each XCD's L2 sees only its own cell splits (sized to fit) instead of every split
@@ -517,10 +517,10 @@ __global__ __launch_bounds__(kBlock, dndx_waves<MODE>()) void k_dndx(DndxArgs A)
   double* s_red = s_qv + kTile * nphp;                    // [kTile][kBlock] per-lane cell sums
   double* s_grid = s_red + kTile * kBlock;                // y[nk] | eta[nl] | eta_w[nl]
   double* s_y = s_grid + A.nk + 2 * A.nl;                 // [kTile][nq][kYRow]
-  double* s_etab = s_y + (long)kTile * A.nq * kYRow;      // [64] exp_tab's 2^(j/64)
+  double* s_etab = s_y + (long)kTile * A.nq * kYRow;      // [kExpTabN] exp_tab's 2^(j/kExpTabN)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (tid < 64) s_etab[tid] = kExp2Tab64[tid];
+  for (int i = tid; i < kExpTabN; i += kBlock) s_etab[i] = kExp2Tab[i];
   const long nwg = (long)A.nbx * A.nchunk;
   const long bid = blockIdx.x, q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
   const long lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;

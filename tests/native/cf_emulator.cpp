@@ -130,7 +130,7 @@ extern "C" int emu_spectra(const orc_params* p, const orc_setup* su, const orc_s
       if (kind == 0.0) continue;
       for (int j = 0; j < nphi; j++) {
         CS[j].x = pT * cph[j]; CS[j].y = pT * sph[j];
-        BP[j] = phiterms(mode, R, pT, cph[j], sph[j], kExp2Tab64);
+        BP[j] = phiterms(mode, R, pT, cph[j], sph[j], kExp2Tab);
         QV[j] = (mode >= PTM && kind == 2.0) ? modqv(R, CS[j]) : 0.0;
       }
       for (int q = 0; q < nq; q++) {
@@ -157,7 +157,7 @@ extern "C" int emu_spectra(const orc_params* p, const orc_setup* su, const orc_s
             const bool sep = (mode <= CE) || kind == 1.0 || Y[Y_NARROW] != 0.0;
             if (sep) {
               SepLane L;
-              sep_setup(sep_flavor(mode), R, Y, mT, mT * mT, m2, mT * baryon, pT, sign, baryon, kExp2Tab64, L);
+              sep_setup(sep_flavor(mode), R, Y, mT, mT * mT, m2, mT * baryon, pT, sign, baryon, kExp2Tab, L);
               if (L.skip) continue;
               // same arithmetic as k_spectra: fast lanes evaluate phi points in fours (phi blocks that
               // are multiples of 4) or pairs sharing one reciprocal (an odd tail point alone)
@@ -187,7 +187,7 @@ extern "C" int emu_spectra(const orc_params* p, const orc_setup* su, const orc_s
                 a[j] += sep_point(sep_flavor(mode), L, CS[j], BP[j], p->regulate_deltaf, p->outflow);
             } else {
               ModLane M;
-              mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, kExp2Tab64, M);
+              mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, kExp2Tab, M);
               if (M.skip) continue;
               int j = 0;
               if (op != 0 && spectra_kj(nphi) % 4 == 0)       // k_spectra's fours; k_dndx pairs
@@ -257,7 +257,7 @@ extern "C" void emu_jonah_table(const orc_setup* su, double* l2, double* z, doub
 // the modified path's table exp (exp_tab) on x: the caller's scaling x 64/ln2 included
 extern "C" void emu_exp_tab(const double* x, long n, double* out) {
   const ExpTabCoef E = exp_tab_coef();
-  for (long i = 0; i < n; i++) out[i] = exp_tab(E, kExp2Tab64, x[i] * kInvLn2x64);
+  for (long i = 0; i < n; i++) out[i] = exp_tab(E, kExp2Tab, x[i] * kInvLn2xN);
 }
 
 // operation 2 yield estimate with the device math (k_densities + k_yield, sequential sums)
