@@ -1323,7 +1323,35 @@ IS3D_HD void sep_quad_pd_t(const SepLane& L, const dbl2* c, const dbl2* b, const
   v[3] = sep_fast_tail_pb<FL, REG, OUT>(L, c[3], b[3], pb[3], E[3], r23 * q[2]);
 }
 
-IS3D_HD void sep_quad_pd(int flavor, const SepLane& L, const dbl2* c, const dbl2* b, const double* pd, int regulate,
+// Grad fours with the linear delta-f part from the (cell, q, phi) table as well.  Without baryon
+// terms (include_baryon = 0: c1 = c3 = 0 and V = 0, so R_SCB = R_SSB = 0 exactly) the lane's
+// Sc pc + Ss ps = a mT (SC1 pc + SS1 ps), and T1 = SC1 pc + SS1 ps depends on (cell, y, phi) only,
+// so pt[i] = {PD, T1} (one LDS read, as PD alone) and
+//   a S = fma(a, fma(mT, T1, Phi), S0')     -- two ops per point instead of three.
+template <bool REG, bool OUT>
+IS3D_HD void sep_quad_tb_t(const SepLane& L, double mT, const dbl2* b, const dbl2* pt, double* v) {
+  double pb[4], q[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    pb[i] = fma(L.D0, b[i].x, L.escw * pt[i].x);
+    q[i] = fma(L.ssc, b[i].x, L.a);
+  }
+  const double q01 = q[0] * q[1], q23 = q[2] * q[3];
+  const double r = rcp1(q01 * q23);
+  const double r01 = r * q23, r23 = r * q01;
+  const double rq[4] = {r01 * q[1], r01 * q[0], r23 * q[3], r23 * q[2]};
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const double in = fma(L.a, fma(mT, pt[i].y, b[i].y), L.S0);
+    double t;
+    if (REG) t = 1.0 + fmax(-1.0, fmin(rq[i] * in, 1.0));
+    else t = fma(rq[i], in, 1.0);
+    const double g = (pb[i] * rq[i]) * t;
+    v[i] = (OUT && pb[i] <= 0.0) ? 0.0 : g;
+  }
+}
+
+IS3D_HD void sep_quad_pd(int flavor,const SepLane& L, const dbl2* c, const dbl2* b, const double* pd, int regulate,
                          int outflow, double* v) {
 #define IS3D_QUADPD_CASE(FLV)                                                                     \
   if (flavor == FLV) {                                                                            \

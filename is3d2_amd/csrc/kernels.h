@@ -61,7 +61,10 @@ struct SpecArgs {
 };
 
 // flag bits of the spectra kernel instantiation
-constexpr int F_REG = 1, F_OUT = 2;
+// F_TB (Grad, include_baryon = 0, one phi block, KJ % 4 == 0): linear delta-f part from the
+// (cell, q, phi) {PD, T1} table (sep_quad_tb_t); a workgroup then uses at most kTbQ q values
+constexpr int F_REG = 1, F_OUT = 2, F_TB = 4;
+constexpr int kTbQ = 4;
 
 #ifndef IS3D_SPLIT_BYTES
 #define IS3D_SPLIT_BYTES (2L << 20)   // record bytes per cell split (k_spectra grid sizing)
@@ -83,6 +86,9 @@ constexpr int F_REG = 1, F_OUT = 2;
 #endif
 #ifndef IS3D_CS_SCALAR
 #define IS3D_CS_SCALAR 1      // PD fours with one phi block: {pc, ps} by scalar loads (SGPR operands)
+#endif
+#ifndef IS3D_GRAD_TB
+#define IS3D_GRAD_TB 1        // Grad without baryon: the F_TB {PD, T1} table launch (engine.hip)
 #endif
 #ifndef IS3D_YQ_RANGE
 #define IS3D_YQ_RANGE 1       // k_spectra builds the y-terms of its lanes' q range only
@@ -225,6 +231,24 @@ __device__ __forceinline__ void sep_phi_loop_pd(const SepLane& L, CSP CS, const 
   }
 }
 
+// fast Grad lanes of an F_TB launch: fours from the {b', Phi} and {PD, T1} tables (sep_quad_tb_t)
+template <int FLAGS, int KJ>
+__device__ __forceinline__ void sep_phi_loop_tb(const SepLane& L, double mT, const dbl2* BP, const dbl2* PT,
+                                                double* acc) {
+  constexpr bool REG = (FLAGS & F_REG) != 0, OUT = (FLAGS & F_OUT) != 0;
+  static_assert(KJ % 4 == 0, "F_TB needs phi blocks of fours");
+#pragma unroll
+  for (int jj = 0; jj < KJ; jj += 4) {
+    dbl2 b[4], pt[4];
+    double v[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) { b[i] = BP[jj + i]; pt[i] = PT[jj + i]; }
+    sep_quad_tb_t<REG, OUT>(L, mT, b, pt, v);
+#pragma unroll
+    for (int i = 0; i < 4; i++) acc[jj + i] += v[i];
+  }
+}
+
 template <int FLAGS, bool CLAMP, int KJ>
 __device__ __forceinline__ void mod_phi_loop(const ModLane& M, const dbl2* CS, const dbl2* QV, double* acc) {
   constexpr bool OUT = (FLAGS & F_OUT) != 0;
@@ -305,7 +329,11 @@ __global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_spectra(SpecA
   double* s_qv = (double*)(s_bp + kTile * nphp);         // [kTile][nphp]  Qv (modified path)
   double* s_grid = s_qv + kTile * nphp;                   // y[nk] | eta[nl] | eta_w[nl]
   double* s_y = s_grid + A.nk + 2 * A.nl;                 // [kTile][nq][kYRow]
-  double* s_etab = s_y + (long)kTile * A.nq * kYRow;      // [kExpTabN] exp_tab's 2^(j/kExpTabN)
+  constexpr bool TB = MODE == GRAD && (FLAGS & F_TB) != 0 && KJ % 4 == 0;
+  double* s_etab = s_y + (long)kTile * (TB ? kTbQ : A.nq) * kYRow;   // [kExpTabN] exp_tab's 2^(j/kExpTabN)
+  // TB: [kTile][kTbQ][nphp] {PD, T1}, 16-byte aligned for ds_read_b128 (s_grid's nk + 2 nl doubles
+  // can leave s_etab at an odd double; misaligned dbl2 reads ran the kernel 3.5x slower)
+  dbl2* s_pt = (dbl2*)(smem + (((s_etab + kExpTabN) - smem + 1) & ~1L));
 
   const int tid = threadIdx.x;
   for (int i = tid; i < kExpTabN; i += kBlock) s_etab[i] = kExp2Tab[i];
@@ -398,6 +426,19 @@ __global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_spectra(SpecA
       }
     }
     lds_barrier();
+    if constexpr (TB) {
+      // {PD, T1 = SC1 pc + SS1 ps} per (cell, q, phi) (rows of skipped cells are never read)
+      for (int idx = tid; idx < nt * nqw * nphp; idx += kBlock) {
+        const int j = idx % nphp, r = idx / nphp, qq = r % nqw, t = r / nqw;
+        const double* Y = s_y + ((long)t * nqw + qq) * kYRow;
+        const dbl2 c = s_cs[j];
+        dbl2 v;
+        v.x = s_qv[t * nphp + j];
+        v.y = fma(Y[Y_SC1], c.x, Y[Y_SS1] * c.y);
+        s_pt[((long)t * kTbQ + qq) * nphp + j] = v;
+      }
+      lds_barrier();
+    }
     if (active) {
       for (int t = 0; t < nt; t++) {
         const double* R = s_rec + t * NREC;
@@ -416,8 +457,10 @@ __global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_spectra(SpecA
           SepLane L;
           sep_setup(sep_flavor(MODE), R, Y, mT, mT2, m2, mTb, pT, sign, baryon, s_etab, L);
           if (L.skip) continue;
-          // wave-uniform choice (a mixed wave would run both loops): every active lane unscaled
-          if (IS3D_PD_TABLE && IS3D_CS_SCALAR && MODE <= CE && KJ % 4 == 0 && L.fast && A.njb == 1)
+          if constexpr (TB) {
+            if (L.fast) sep_phi_loop_tb<FLAGS, KJ>(L, mT, BP, s_pt + ((long)t * kTbQ + (q - q0)) * nphp, acc);
+            else sep_phi_loop<MODE, FLAGS, false, KJ>(L, s_cs + j0, BP, acc);
+          } else if (IS3D_PD_TABLE && IS3D_CS_SCALAR && MODE <= CE && KJ % 4 == 0 && L.fast && A.njb == 1)
             // one phi block: every lane reads the same {pc, ps}, so they come by scalar loads into SGPRs
             // (VALU operands) instead of LDS
             sep_phi_loop_pd<MODE, FLAGS, KJ, true>(L, (cs_sptr)A.csg + 2L * ipt * nphp,
@@ -645,7 +688,18 @@ __global__ __launch_bounds__(kBlock, dndx_waves<MODE>()) void k_dndx(DndxArgs A)
 
 template <int MODE, int KJ>
 void launch_spectra_kj(dim3 grid, size_t shmem, hipStream_t st, const SpecArgs& a, int flags) {
-  switch (flags) {
+  if constexpr (MODE == GRAD && KJ % 4 == 0) {
+    if (flags & F_TB) {
+      switch (flags & 3) {
+        case 0: hipLaunchKernelGGL((k_spectra<MODE, 4, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+        case 1: hipLaunchKernelGGL((k_spectra<MODE, 5, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+        case 2: hipLaunchKernelGGL((k_spectra<MODE, 6, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+        default: hipLaunchKernelGGL((k_spectra<MODE, 7, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+      }
+      return;
+    }
+  }
+  switch (flags & 3) {
     case 0: hipLaunchKernelGGL((k_spectra<MODE, 0, KJ>), grid, dim3(kBlock), shmem, st, a); break;
     case 1: hipLaunchKernelGGL((k_spectra<MODE, 1, KJ>), grid, dim3(kBlock), shmem, st, a); break;
     case 2: hipLaunchKernelGGL((k_spectra<MODE, 2, KJ>), grid, dim3(kBlock), shmem, st, a); break;
