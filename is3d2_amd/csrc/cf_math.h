@@ -1328,13 +1328,19 @@ IS3D_HD void sep_quad_pd_t(const SepLane& L, const dbl2* c, const dbl2* b, const
 // Sc pc + Ss ps = a mT (SC1 pc + SS1 ps), and T1 = SC1 pc + SS1 ps depends on (cell, y, phi) only,
 // so pt[i] = {PD, T1} (one LDS read, as PD alone) and
 //   a S = fma(a, fma(mT, T1, Phi), S0')     -- two ops per point instead of three.
-template <bool REG, bool OUT>
-IS3D_HD void sep_quad_tb_t(const SepLane& L, double mT, const dbl2* b, const dbl2* pt, double* v) {
-  double pb[4], q[4];
+// RTA-CE (SEP_CE) in the same launch also takes, per (cell, phi), pe = {TE, T2} with
+// TE = -(u^x pc + u^y ps) and T2 = LC pc + LS ps (cell-only lane coefficients, sep_cell_consts):
+//   E = E0 + TE,  a (L0 + Lc pc + Ls ps) = fma(a, T2, L0')   -- five ops per point instead of eight.
+template <int FL, bool REG, bool OUT>
+IS3D_HD void sep_quad_tb_t(const SepLane& L, double mT, const dbl2* b, const dbl2* pt, const dbl2* pe, double* v) {
+  constexpr bool needE = FL == SEP_CE;
+  double pb[4], q[4], E[4];
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     pb[i] = fma(L.D0, b[i].x, L.escw * pt[i].x);
-    q[i] = fma(L.ssc, b[i].x, L.a);
+    const double den = fma(L.ssc, b[i].x, L.a);
+    E[i] = needE ? L.E0 + pe[i].x : 1.0;
+    q[i] = needE ? den * E[i] : den;
   }
   const double q01 = q[0] * q[1], q23 = q[2] * q[3];
   const double r = rcp1(q01 * q23);
@@ -1342,11 +1348,12 @@ IS3D_HD void sep_quad_tb_t(const SepLane& L, double mT, const dbl2* b, const dbl
   const double rq[4] = {r01 * q[1], r01 * q[0], r23 * q[3], r23 * q[2]};
 #pragma unroll
   for (int i = 0; i < 4; i++) {
-    const double in = fma(L.a, fma(mT, pt[i].y, b[i].y), L.S0);
+    double in = fma(L.a, fma(mT, pt[i].y, b[i].y), L.S0);
+    if (needE) in = fma(E[i], fma(L.a, pe[i].y, L.L0), in);
     double t;
     if (REG) t = 1.0 + fmax(-1.0, fmin(rq[i] * in, 1.0));
     else t = fma(rq[i], in, 1.0);
-    const double g = (pb[i] * rq[i]) * t;
+    const double g = (needE ? pb[i] * (E[i] * rq[i]) : pb[i] * rq[i]) * t;
     v[i] = (OUT && pb[i] <= 0.0) ? 0.0 : g;
   }
 }

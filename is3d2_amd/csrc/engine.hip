@@ -891,12 +891,13 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   // Grad {PD, T1} table (F_TB, sep_quad_tb_t): exact only without baryon terms (R_SCB = R_SSB = 0);
   // needs one phi block of fours, and the 256 tasks of a workgroup span at most
   // (kBlock - 1) / np + 2 <= kTbQ q values
-  const int tb = (IS3D_GRAD_TB && mode == GRAD && !e->p.include_baryon && njb == 1 && KJ % 4 == 0 &&
+  const int tb = (IS3D_GRAD_TB && (mode == GRAD || (mode == CE && IS3D_CE_TB)) && !e->p.include_baryon && njb == 1 && KJ % 4 == 0 &&
                   (kBlock - 1) / np + 2 <= kTbQ) ? F_TB : 0;
   const size_t shmem = sizeof(double) * (2 * (size_t)kTile * NREC + 2 * (size_t)(kTile + 2) * njb * KJ +
                                          (size_t)kTile * njb * KJ + (size_t)(nk + 2 * nl) +
                                          (size_t)kTile * (tb ? kTbQ : sa.nq) * kYRow + kExpTabN +
-                                         (tb ? 2 * (size_t)kTile * kTbQ * KJ + 1 : 0));
+                                         (tb ? 2 * (size_t)kTile * kTbQ * KJ + 1 : 0) +
+                                         (tb && mode == CE ? 2 * (size_t)kTile * KJ : 0));
   if (shmem > 160 * 1024) return e->fail(IS3D_ERR_ARG, "momentum grid too large for the LDS tile");
   const dim3 grid((unsigned)(bx * npT * nsplit));
   const int kflags = (e->p.regulate_deltaf ? F_REG : 0) | (e->p.outflow ? F_OUT : 0) | tb;

@@ -61,7 +61,7 @@ struct SpecArgs {
 };
 
 // flag bits of the spectra kernel instantiation
-// F_TB (Grad, include_baryon = 0, one phi block, KJ % 4 == 0): linear delta-f part from the
+// F_TB (Grad / RTA-CE, include_baryon = 0, one phi block, KJ % 4 == 0): linear delta-f part from the
 // (cell, q, phi) {PD, T1} table (sep_quad_tb_t); a workgroup then uses at most kTbQ q values
 constexpr int F_REG = 1, F_OUT = 2, F_TB = 4;
 constexpr int kTbQ = 4;
@@ -89,6 +89,9 @@ constexpr int kTbQ = 4;
 #endif
 #ifndef IS3D_GRAD_TB
 #define IS3D_GRAD_TB 1        // Grad without baryon: the F_TB {PD, T1} table launch (engine.hip)
+#endif
+#ifndef IS3D_CE_TB
+#define IS3D_CE_TB 1          // RTA-CE without baryon also takes the F_TB launch ({PD, T1} + {TE, T2} tables)
 #endif
 #ifndef IS3D_YQ_RANGE
 #define IS3D_YQ_RANGE 1       // k_spectra builds the y-terms of its lanes' q range only
@@ -232,18 +235,22 @@ __device__ __forceinline__ void sep_phi_loop_pd(const SepLane& L, CSP CS, const 
 }
 
 // fast Grad lanes of an F_TB launch: fours from the {b', Phi} and {PD, T1} tables (sep_quad_tb_t)
-template <int FLAGS, int KJ>
+template <int MODE, int FLAGS, int KJ>
 __device__ __forceinline__ void sep_phi_loop_tb(const SepLane& L, double mT, const dbl2* BP, const dbl2* PT,
-                                                double* acc) {
+                                                const dbl2* PE, double* acc) {
+  constexpr int FL = (MODE == GRAD) ? SEP_GRAD : SEP_CE;
   constexpr bool REG = (FLAGS & F_REG) != 0, OUT = (FLAGS & F_OUT) != 0;
   static_assert(KJ % 4 == 0, "F_TB needs phi blocks of fours");
 #pragma unroll
   for (int jj = 0; jj < KJ; jj += 4) {
-    dbl2 b[4], pt[4];
+    dbl2 b[4], pt[4], pe[4];
     double v[4];
 #pragma unroll
-    for (int i = 0; i < 4; i++) { b[i] = BP[jj + i]; pt[i] = PT[jj + i]; }
-    sep_quad_tb_t<REG, OUT>(L, mT, b, pt, v);
+    for (int i = 0; i < 4; i++) {
+      b[i] = BP[jj + i]; pt[i] = PT[jj + i];
+      if (FL == SEP_CE) pe[i] = PE[jj + i];
+    }
+    sep_quad_tb_t<FL, REG, OUT>(L, mT, b, pt, pe, v);
 #pragma unroll
     for (int i = 0; i < 4; i++) acc[jj + i] += v[i];
   }
@@ -329,11 +336,12 @@ __global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_spectra(SpecA
   double* s_qv = (double*)(s_bp + kTile * nphp);         // [kTile][nphp]  Qv (modified path)
   double* s_grid = s_qv + kTile * nphp;                   // y[nk] | eta[nl] | eta_w[nl]
   double* s_y = s_grid + A.nk + 2 * A.nl;                 // [kTile][nq][kYRow]
-  constexpr bool TB = MODE == GRAD && (FLAGS & F_TB) != 0 && KJ % 4 == 0;
+  constexpr bool TB = (MODE == GRAD || MODE == CE) && (FLAGS & F_TB) != 0 && KJ % 4 == 0;
   double* s_etab = s_y + (long)kTile * (TB ? kTbQ : A.nq) * kYRow;   // [kExpTabN] exp_tab's 2^(j/kExpTabN)
   // TB: [kTile][kTbQ][nphp] {PD, T1}, 16-byte aligned for ds_read_b128 (s_grid's nk + 2 nl doubles
   // can leave s_etab at an odd double; misaligned dbl2 reads ran the kernel 3.5x slower)
   dbl2* s_pt = (dbl2*)(smem + (((s_etab + kExpTabN) - smem + 1) & ~1L));
+  dbl2* s_pe = s_pt + kTile * kTbQ * nphp;                // TB, RTA-CE: [kTile][nphp] {TE, T2}
 
   const int tid = threadIdx.x;
   for (int i = tid; i < kExpTabN; i += kBlock) s_etab[i] = kExp2Tab[i];
@@ -413,6 +421,13 @@ __global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_spectra(SpecA
       s_bp[t * nphp + j] = v;
       // s_qv holds Qv on the modified path and the PD table (sep_pd) for Grad / RTA-CE
       s_qv[t * nphp + j] = (MODE >= PTM) ? qv : sep_pd(R, s_cs[j], v.x);
+      if constexpr (TB && MODE == CE) {
+        const dbl2 c = s_cs[j];
+        dbl2 e;
+        e.x = -fma(R[R_UX], c.x, R[R_UY] * c.y);
+        e.y = fma(R[R_LC], c.x, R[R_LS] * c.y);
+        s_pe[t * nphp + j] = e;
+      }
     }
     for (int idx = tid; idx < nt * nqw; idx += kBlock) {
       const int t = idx / nqw, qq = idx % nqw, q = q0 + qq;
@@ -458,7 +473,8 @@ __global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_spectra(SpecA
           sep_setup(sep_flavor(MODE), R, Y, mT, mT2, m2, mTb, pT, sign, baryon, s_etab, L);
           if (L.skip) continue;
           if constexpr (TB) {
-            if (L.fast) sep_phi_loop_tb<FLAGS, KJ>(L, mT, BP, s_pt + ((long)t * kTbQ + (q - q0)) * nphp, acc);
+            if (L.fast) sep_phi_loop_tb<MODE, FLAGS, KJ>(L, mT, BP, s_pt + ((long)t * kTbQ + (q - q0)) * nphp,
+                                                         s_pe + t * nphp, acc);
             else sep_phi_loop<MODE, FLAGS, false, KJ>(L, s_cs + j0, BP, acc);
           } else if (IS3D_PD_TABLE && IS3D_CS_SCALAR && MODE <= CE && KJ % 4 == 0 && L.fast && A.njb == 1)
             // one phi block: every lane reads the same {pc, ps}, so they come by scalar loads into SGPRs
@@ -688,7 +704,7 @@ __global__ __launch_bounds__(kBlock, dndx_waves<MODE>()) void k_dndx(DndxArgs A)
 
 template <int MODE, int KJ>
 void launch_spectra_kj(dim3 grid, size_t shmem, hipStream_t st, const SpecArgs& a, int flags) {
-  if constexpr (MODE == GRAD && KJ % 4 == 0) {
+  if constexpr ((MODE == GRAD || MODE == CE) && KJ % 4 == 0) {
     if (flags & F_TB) {
       switch (flags & 3) {
         case 0: hipLaunchKernelGGL((k_spectra<MODE, 4, KJ>), grid, dim3(kBlock), shmem, st, a); break;

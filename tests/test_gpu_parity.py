@@ -36,12 +36,12 @@ def test_spectra_parity(dim, mode):
         assert st["iterations"] == rst[3]
 
 
-@pytest.mark.parametrize("reg_out", [(0, 0), (1, 0), (0, 1), (1, 1)])
-def test_smash_3d_grad_subset(reg_out):
+@pytest.mark.parametrize("mode,reg_out", [(1, (0, 0)), (1, (1, 0)), (1, (0, 1)), (1, (1, 1)), (2, (0, 0)), (2, (1, 1))])
+def test_smash_3d_grad_subset(mode, reg_out):
     # many species (mass-sorted lanes, several wavefronts per y) on the config-2 grid; with >= 86
-    # species and no baryon this is the F_TB {PD, T1} table launch, in each regulate/outflow variant
+    # species and no baryon this is the F_TB table launch (Grad, RTA-CE), per regulate/outflow variant
     s = synth.as_read(synth.surface(64, seed=2, dimension=3))
-    spec = make_spec(hrg_eos=2, chosen="smash", df_mode=1, dimension=3, pT="pT48", phi="phi32", y="y21",
+    spec = make_spec(hrg_eos=2, chosen="smash", df_mode=mode, dimension=3, pT="pT48", phi="phi32", y="y21",
                      regulate_deltaf=reg_out[0], outflow=reg_out[1])
     ref = O.spectra(spec, s, threads=8)
     got, _ = run_gpu(spec, s)
@@ -210,10 +210,11 @@ def test_smash_2d_eta_lanes(mode):
     assert parity(got, ref)[0] < TOL
 
 
-def test_smash_2d_grad_table_phi32():
+@pytest.mark.parametrize("mode", [1, 2])
+def test_smash_2d_grad_table_phi32(mode):
     # 2+1D F_TB launch: eta-node lanes (escw = w_eta != 1 scales the PD half of the table)
     s = synth.as_read(synth.surface(16, seed=12))
-    spec = make_spec(hrg_eos=2, chosen="smash", df_mode=1, dimension=2, phi="phi32")
+    spec = make_spec(hrg_eos=2, chosen="smash", df_mode=mode, dimension=2, phi="phi32")
     ref = O.spectra(spec, s, threads=8)
     got, _ = run_gpu(spec, s)
     assert parity(got, ref)[0] < TOL
