@@ -27,6 +27,7 @@ sys.path.insert(0, ROOT)
 
 FLOPS_PER_NODE = {1: 65, 2: 67, 3: 140, 4: 140, 5: 140}   # SURVEY.md 8(d), frozen algorithmic counts
 FP64_PEAK_TFLOPS = 78.6                                     # MI355X FP64 vector (= FP64 matrix) dense peak
+FP64_LANE_OPS_PEAK = 256 * 4 * 16 * 2.4e9                  # FP64 VALU lane-ops/s: 16 lanes/clk per SIMD
 HBM_PEAK_BPS = 8.0e12                                       # MI355X HBM3E
 MODE_NAMES = {1: "grad14", 2: "rta-ce", 3: "ptm", 4: "ptb", 5: "ptma"}
 
@@ -58,10 +59,34 @@ def make_surface(cfg, rank, world, dim, baryon):
     return synth.as_read(synth.surface(cfg["cells"], seed=7 + rank, dimension=dim, baryon=baryon, full3d=(dim == 3)))
 
 
-def cpu_baseline(spec, surf, units_per_cell, target_s=15.0, operation=1):
-    """Oracle ('port' of the reference loop) on the host cores, on a cell prefix of the same workload."""
+def _host_cpu():
+    """CPU model, logical CPUs of the host (nproc), CPUs this process may run on, and the cgroup CPU quota."""
+    model = ""
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        quota = None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    return model, os.cpu_count() or 1, len(os.sched_getaffinity(0)), quota
+
+
+def cpu_baseline(spec, surf, units_per_cell, n_full, target_s=25.0, operation=1):
+    """Oracle (a C/OpenMP 'port' of the reference loop, oracle/Makefile flags) on the host cores, on a
+    cell prefix of the same workload sized to >= target_s, extrapolated linearly to the full shard
+    (the cost is linear in the cell count).  Threads: OMP_NUM_THREADS when set (the GPU
+    pool sets it to the box's CPU share, 16 per GPU; nproc there counts the whole host), else every
+    CPU in this process's affinity mask."""
     from oracle import oracle as O
-    threads = int(os.environ.get("OMP_NUM_THREADS") or min(16, os.cpu_count() or 1))
+    model, nproc, affinity, quota = _host_cpu()
+    threads = int(os.environ.get("OMP_NUM_THREADS") or affinity)
     T_avg = O.averages(surf)[0]
 
     def run(sample):
@@ -75,15 +100,153 @@ def cpu_baseline(spec, surf, units_per_cell, target_s=15.0, operation=1):
     t = time.perf_counter()
     run(probe)
     dt = time.perf_counter() - t
-    n = int(min(len(surf["tau"]), max(n_probe, n_probe * target_s / max(dt, 1e-3))))
+    n = int(min(len(surf["tau"]), max(n_probe, 1.15 * n_probe * target_s / max(dt, 1e-3))))
     n = max(threads, (n // threads) * threads)
     sample = {k: v[:n] for k, v in surf.items()}
     t = time.perf_counter()
     run(sample)
     dt = time.perf_counter() - t
+    flags = ""
+    try:
+        mk = open(os.path.join(ROOT, "oracle", "Makefile")).read()
+        flags = [ln.split("=", 1)[1].strip() for ln in mk.splitlines() if ln.startswith("CFLAGS")][0]
+    except (OSError, IndexError):
+        pass
     return dict(value=n * units_per_cell / dt, unit="cell-species-mom-points/s", cores=threads, kind="port",
-                sample="first %d cells of rank 0's shard, same species/grid/df mode; %.1f s with %d OpenMP threads"
-                       % (n, dt, threads))
+                sample="first %d cells of rank 0's shard (same species/grid/df mode): %.1f s with %d OpenMP threads"
+                       % (n, dt, threads),
+                sample_cells=n, sample_s=dt, extrapolated_s=dt * n_full / n, extrapolated_cells=n_full,
+                nproc=nproc, affinity_cpus=affinity, cgroup_cpu_quota=quota, cpu_model=model,
+                compiler="gcc " + flags)
+
+
+def executed_roofline(args, mode, ms_spectra, ms_total, neta, units_local, n_local, outsize, kernel):
+    """Roofline record of the dominant kernel (k_spectra).  The kernel is FP64-VALU bound (SURVEY.md 8d:
+    ~1e-5 B per unit), so `achieved` is the FP64 work the kernel EXECUTES per launch -- the hardware
+    counter SQ_INSTS_VALU_FLOPS_FP64 (FMA = 2) from the committed rocprofv3 pass of this workload
+    (profiles/pmc_valu.json) -- over the launch's average duration measured live here with HIP events on
+    the launch stream, against the 78.6 TFLOP/s FP64 vector peak.  fp64_pipe_frac counts issue slots
+    instead (every FP64 add / mul / fma / transcendental wave-instruction takes the pipe for 4 cycles).
+    The reference-loop operation count of SURVEY.md 8d (F flops per node) is reported separately as
+    reference_equivalent_tflops: the factorised kernel executes ~1/4 of those operations, so that rate
+    is not a fraction of any peak."""
+    key = "%s_mode%d" % (args.config, mode) if args.operation == 1 else "%s_op0_mode%d" % (args.config, mode)
+    pmc = {}
+    for name in ("pmc_traffic", "pmc_valu"):
+        path = os.path.join(ROOT, "profiles", name + ".json")
+        pmc[name] = json.load(open(path)).get(key) if os.path.exists(path) else None
+    traffic, ex = pmc["pmc_traffic"], pmc["pmc_valu"]
+    t = ms_spectra * 1e-3
+    ref_flops = FLOPS_PER_NODE[mode] * neta * units_local
+    algo_bytes = 200.0 * n_local + 8.0 * outsize           # surface read once + spectra written once
+    r = {"bound": "valu", "pipe": "fp64 vector ALU (k_spectra issues no MFMA)", "kernel": kernel,
+         "achieved": None, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": None, "traffic": traffic,
+         "kernel_ms": ms_spectra, "pass_ms": ms_total,
+         "reference_equivalent_tflops": ref_flops / t / 1e12, "reference_flops_per_node": FLOPS_PER_NODE[mode] * neta,
+         "algorithmic_bytes": algo_bytes,
+         "traffic_over_algorithmic": None if traffic is None else traffic / algo_bytes,
+         "hbm_gbs": None if traffic is None else traffic / t / 1e9,
+         "hbm_frac": None if traffic is None else traffic / t / HBM_PEAK_BPS}
+    if ex is not None:
+        if "fp64_flops_per_launch" in ex:
+            r["achieved"] = ex["fp64_flops_per_launch"] / t / 1e12
+            r["frac"] = r["achieved"] / FP64_PEAK_TFLOPS
+            r["executed_flops_per_unit"] = ex["fp64_flops_per_launch"] / units_local
+        if "fma_f64_insts_per_launch" in ex:
+            ins = sum(ex.get(c + "_insts_per_launch", 0.0) for c in ("add_f64", "mul_f64", "fma_f64", "trans_f64"))
+            r["fp64_pipe_frac"] = 64.0 * ins / (t * FP64_LANE_OPS_PEAK)
+        r["executed"] = dict(ex, note="rocprofv3 PMC passes of this workload (tag); counts per k_spectra launch")
+    return r
+
+
+def run_workload(args, cfg_name, mode, steps, warmup, rank, world, local_rank, dev, dist):
+    """Build the engine for one workload on this rank's shard, run `warmup` untimed and `steps` timed
+    passes (barrier + synchronize on both sides, max over ranks) and return the measurement."""
+    import torch
+    from is3d2_amd import build_engine, make_spec
+    from is3d2_amd import dist as D
+
+    cfg = dict(CONFIGS[cfg_name])
+    if args.cells and cfg_name == args.config:
+        cfg["cells"] = args.cells
+    if args.chosen and cfg_name == args.config:
+        cfg["chosen"] = args.chosen
+    mode = mode or cfg["mode"]
+    flags = dict(cfg["flags"])
+    if mode == 4:
+        flags.pop("include_baryon", None); flags.pop("include_baryondiff_deltaf", None)
+    spec = make_spec(hrg_eos=cfg["hrg"], chosen=cfg["chosen"], pT=cfg["pT"], phi=cfg["phi"], y="y21", eta="eta24",
+                     dimension=cfg["dim"], df_mode=mode, gla_points=cfg.get("gla", 32), **flags)
+    surf = make_surface(cfg, rank, world, cfg["dim"], bool(flags.get("include_baryon", 0)))
+    n_local = len(surf["tau"])
+    reduce = D.torch_all_reduce(dist, dev) if world > 1 else (lambda a: a)
+    T_avg = D.global_averages(D.average_sums(surf, flags.get("include_baryon", 0)), reduce)[0]
+
+    eng = build_engine(spec, surf, T_avg=T_avg, device=local_rank)
+    outsize = eng.output_size()
+    out = torch.zeros(outsize, dtype=torch.float64, device=dev)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+
+    nsp, npT, nphi = len(spec["species"]["mass"]), len(spec["pT"]), len(spec["phi"])
+    ny = len(spec["y"]) if cfg["dim"] == 3 else 1
+    neta = 1 if cfg["dim"] == 3 else len(spec["eta"])
+    units_per_cell = nsp * npT * nphi * ny
+    units_local = n_local * units_per_cell
+    operation = args.operation if cfg_name == args.config else 1
+    if operation == 0 and world > 1 and spec["bins"].get("threads", 0):
+        raise SystemExit("operation 0 with reference thread emulation runs on one rank")
+
+    def step():
+        if operation == 0:
+            t, r, ph = eng.calculate_dN_dX()      # synchronous: device passes + small host binning epilogue
+            if world > 1:
+                binned = torch.from_numpy(np.concatenate([t.ravel(), r.ravel(), ph.ravel()])).to(dev)
+                dist.all_reduce(binned)
+            return eng.stats()
+        eng.launch(out.data_ptr(), stream)
+        if world > 1:
+            dist.all_reduce(out)
+        eng.finish()
+        return eng.stats()
+
+    for _ in range(warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    kstats = [step() for _ in range(steps)]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    units_all = torch.tensor([float(units_local)], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        dist.all_reduce(units_all)
+    elapsed = tmax.item()
+    total_units = units_all.item() * steps
+    eng.close()
+    del out
+
+    ms_spectra = float(np.mean([s["ms_spectra"] for s in kstats]))
+    ms_total = float(np.mean([s["ms_total"] for s in kstats]))
+    kernel = "k_spectra" if operation == 1 else "k_dndx"
+    sub = argparse.Namespace(config=cfg_name, operation=operation)
+    roofline = executed_roofline(sub, mode, ms_spectra, ms_total, neta, units_local, n_local, outsize, kernel)
+    config = {
+        "workload": "%s%s: %s %s synthetic freeze-out cells%s x %s HRG (%d species) x %s delta-f, %d pT x %d phi x %d y%s"
+                    % (cfg_name, " operation 0 (dN/dX)" if operation == 0 else "", cfg["cells"],
+                       "3+1D" if cfg["dim"] == 3 else "2+1D", " per GPU" if cfg["scaling"] == "weak" else " total",
+                       "SMASH" if cfg["hrg"] == 2 else "UrQMD", nsp, MODE_NAMES[mode], npT, nphi, ny,
+                       "" if neta == 1 else " x %d eta" % neta),
+        "operation": operation,
+        "cells_per_gpu": n_local, "species": nsp, "grid": [npT, nphi, ny, neta], "df_mode": mode,
+        "parallelism": "dp%d (cell shards + RCCL all-reduce of spectra)" % world if world > 1 else "1 GPU",
+    }
+    return dict(value=total_units / elapsed, elapsed=elapsed, steps=steps, warmup=warmup, cfg=cfg, config=config,
+                roofline=roofline, spec=spec, surf=surf, units_per_cell=units_per_cell, n_local=n_local)
 
 
 def main():
@@ -99,6 +262,9 @@ def main():
                     help="1 continuous spectra (default, the BASELINE metric); 0 spacetime distributions dN/dX")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=25.0)
+    ap.add_argument("--north-star-steps", type=int, default=3,
+                    help="timed passes of the north_star workload (config4: 10^6 3+1D cells, SMASH, RTA-CE, "
+                         "sharded over the ranks) reported beside the main line; 0 skips it")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -115,126 +281,38 @@ def main():
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
 
-    from is3d2_amd import build_engine, make_spec
-
-    cfg = dict(CONFIGS[args.config])
-    if args.cells:
-        cfg["cells"] = args.cells
-    if args.chosen:
-        cfg["chosen"] = args.chosen
-    mode = args.df_mode or cfg["mode"]
-    flags = dict(cfg["flags"])
-    if mode == 4:
-        flags.pop("include_baryon", None); flags.pop("include_baryondiff_deltaf", None)
-    spec = make_spec(hrg_eos=cfg["hrg"], chosen=cfg["chosen"], pT=cfg["pT"], phi=cfg["phi"], y="y21", eta="eta24",
-                     dimension=cfg["dim"], df_mode=mode, gla_points=cfg.get("gla", 32), **flags)
-    surf = make_surface(cfg, rank, world, cfg["dim"], bool(flags.get("include_baryon", 0)))
-    n_local = len(surf["tau"])
-    from is3d2_amd import dist as D
-    reduce = D.torch_all_reduce(dist, dev) if world > 1 else (lambda a: a)
-    T_avg = D.global_averages(D.average_sums(surf, flags.get("include_baryon", 0)), reduce)[0]
-
-    eng = build_engine(spec, surf, T_avg=T_avg, device=local_rank)
-    outsize = eng.output_size()
-    out = torch.zeros(outsize, dtype=torch.float64, device=dev)
-    stream = torch.cuda.current_stream(dev).cuda_stream
-
-    nsp, npT, nphi = len(spec["species"]["mass"]), len(spec["pT"]), len(spec["phi"])
-    ny = len(spec["y"]) if cfg["dim"] == 3 else 1
-    neta = 1 if cfg["dim"] == 3 else len(spec["eta"])
-    units_per_cell = nsp * npT * nphi * ny
-    units_local = n_local * units_per_cell
-
-    def step():
-        if args.operation == 0:
-            t, r, ph = eng.calculate_dN_dX()      # synchronous: device passes + small host binning epilogue
-            if world > 1:
-                binned = torch.from_numpy(np.concatenate([t.ravel(), r.ravel(), ph.ravel()])).to(dev)
-                dist.all_reduce(binned)
-            return eng.stats()
-        eng.launch(out.data_ptr(), stream)
-        if world > 1:
-            dist.all_reduce(out)
-        eng.finish()
-        return eng.stats()
-
-    for _ in range(args.warmup):
-        step()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    kstats = [step() for _ in range(args.steps)]
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
-    tmax = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    units_all = torch.tensor([float(units_local)], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-        dist.all_reduce(units_all)
-    elapsed = tmax.item()
-    total_units = units_all.item() * args.steps
-
-    if args.operation == 0 and world > 1 and spec["bins"].get("threads", 0):
-        raise SystemExit("operation 0 with reference thread emulation runs on one rank")
-    ms_spectra = float(np.mean([s["ms_spectra"] for s in kstats]))
-    ms_total = float(np.mean([s["ms_total"] for s in kstats]))
-    flops = FLOPS_PER_NODE[mode] * neta * units_local
-    achieved = flops / (ms_spectra * 1e-3) / 1e12
-    traffic, executed = None, None
-    key = "%s_mode%d" % (args.config, mode) if args.operation == 1 else "%s_op0_mode%d" % (args.config, mode)
-    pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(pmc):
-        traffic = json.load(open(pmc)).get(key)
-    pv = os.path.join(ROOT, "profiles", "pmc_valu.json")
-    if os.path.exists(pv):
-        executed = json.load(open(pv)).get(key)
-    if executed is not None:
-        executed = dict(executed, note="PMC pass (tag) of this workload: share of SIMD cycles issuing VALU; "
-                                       "achieved/frac above use the reference's frozen flop counts")
-
+    m = run_workload(args, args.config, args.df_mode, args.steps, args.warmup, rank, world, local_rank, dev, dist)
+    ns = None
+    if args.north_star_steps > 0 and args.config != "config4" and args.operation == 1:
+        n = run_workload(args, "config4", 0, args.north_star_steps, 1, rank, world, local_rank, dev, dist)
+        ns = {"metric": "freezeout-cell-species-mom-points/sec", "value": n["value"],
+              "unit": "cell-species-mom-points/s", "steps": n["steps"], "warmup": n["warmup"],
+              "ms_per_step": 1e3 * n["elapsed"] / n["steps"], "scaling": n["cfg"]["scaling"], "config": n["config"],
+              "roofline": n["roofline"],
+              "note": "north_star target workload (BASELINE config 4) timed in this same run, same clock rules"}
     if rank == 0:
         res = {
             "metric": "freezeout-cell-species-mom-points/sec",
-            "value": total_units / elapsed,
+            "value": m["value"],
             "unit": "cell-species-mom-points/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": 1e3 * elapsed / args.steps,
+            "ms_per_step": 1e3 * m["elapsed"] / args.steps,
             "higher_is_better": True,
-            "scaling": cfg["scaling"],
+            "scaling": m["cfg"]["scaling"],
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (SURVEY.md 8d surface generator, seed 7+rank)",
-            "config": {
-                "workload": "%s%s: %s %s synthetic freeze-out cells%s x %s HRG (%d species) x %s delta-f, %d pT x %d phi x %d y%s"
-                            % (args.config, " operation 0 (dN/dX)" if args.operation == 0 else "", cfg["cells"],
-                               "3+1D" if cfg["dim"] == 3 else "2+1D", " per GPU" if cfg["scaling"] == "weak" else " total",
-                               "SMASH" if cfg["hrg"] == 2 else "UrQMD", nsp, MODE_NAMES[mode], npT, nphi, ny,
-                               "" if neta == 1 else " x %d eta" % neta),
-                "operation": args.operation,
-                "cells_per_gpu": n_local, "species": nsp, "grid": [npT, nphi, ny, neta], "df_mode": mode,
-                "parallelism": "dp%d (cell shards + RCCL all-reduce of spectra)" % world if world > 1 else "1 GPU",
-            },
-            "roofline": {
-                "bound": "mfma", "pipe": "fp64 (vector ALU; MI355X FP64 vector peak = FP64 matrix peak)",
-                "kernel": "k_spectra" if args.operation == 1 else "k_dndx", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
-                "algorithmic_flops_per_launch": flops, "flops_per_point": FLOPS_PER_NODE[mode] * neta,
-                "kernel_ms": ms_spectra, "pass_ms": ms_total, "executed": executed,
-                # HBM view (north_star): PMC bytes per launch over the live kernel time, vs 8 TB/s
-                "hbm_gbs": None if traffic is None else traffic / (ms_spectra * 1e-3) / 1e9,
-                "hbm_frac": None if traffic is None else traffic / (ms_spectra * 1e-3) / HBM_PEAK_BPS,
-            },
+            "config": m["config"],
+            "roofline": m["roofline"],
         }
+        if ns is not None:
+            res["north_star"] = ns
         if world == 1 and not args.no_cpu_baseline:
-            res["cpu_baseline"] = cpu_baseline(spec, surf, units_per_cell, args.cpu_seconds, args.operation)
+            res["cpu_baseline"] = cpu_baseline(m["spec"], m["surf"], m["units_per_cell"], m["n_local"], args.cpu_seconds,
+                                               args.operation)
         print(json.dumps(res), flush=True)
-    eng.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -622,6 +622,8 @@ IS3D_HD int prep_grad_ce(const PrepConsts& k, const DfTables& tb, const double* 
   if (err) return err;
   rec_common(R, tau, eta, ut, un, ux, uy, dat, dax, day, dan, T);
   rec_pi(R, tau, pitt, pitx, pity, pitn, pixx, pixy, pixn, piyy, piyn, pinn);
+  // V^mu is nonzero only with include_baryon && include_diff; with include_baryon = 0 it and c1 = c3 = 0
+  // (df_eval) make sep_cell_consts' R_SCB = R_SSB = 0, which the F_TB launch relies on (engine.hip)
   R[R_VT] = Vt; R[R_TVN] = tau * Vn; R[R_VX] = Vx; R[R_VY] = Vy;
   R[R_CHEM] = alphaB;
   if (k.df_mode == GRAD) {
@@ -1069,8 +1071,25 @@ struct SepLane {
   double c0;                   // PTB: constant added outside (1 - sign feq)
   double x, Zc, Zs;            // slow path: feq = 1/(exp(x - Zc pc - Zs ps) + sign)
   int skip, fast;
+  int tail;                    // Boltzmann tail (sep_setup, allow_tail): a + ssc b' == a at every phi point
   double escw;                 // 2^-k w_eta (PD-table scale)
 };
+
+// Boltzmann-tail bound: for an exponent x >= kTailX, e^-x < 2^-54, so exp(x) + sign == exp(x) and
+// 1 - sign f_eq == 1 in FP64 exactly (the sum rounds back to the larger term); a lane whose smallest
+// exponent over phi exceeds it needs no per-point reciprocal at all
+static constexpr double kTailX = 37.5;
+
+// 1/d for finite normal d: v_rcp_f64 (measured max rel. error 4.5e-8 on gfx950) + one
+// Newton step (~2e-15); IEEE division on the host.  Callers guarantee d is finite.
+IS3D_HD double rcp1(double d) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  const double r = __builtin_amdgcn_rcp(d);
+  return fma(r, fma(-d, r, 1.0), r);
+#else
+  return 1.0 / d;
+#endif
+}
 
 // Per-(cell, q, species) setup for the separable integrand.  Returns skip=1 when every
 // phi point underflows (exp argument > 709.78 for all phi: contributes exactly 0).
@@ -1081,8 +1100,14 @@ struct SepLane {
 //   CE    S  = (S0 + Phi + Sc pc + Ss ps) / E + L0 + Lc pc + Ls ps,   E = mT A - ux pc - uy ps
 //   PTB   as CE, delta-f = (1 - sign feq) S + dz - 3 dlambda
 // mT2 = mT * mT and mTb = mT * b are per-lane constants hoisted by the caller.
+//
+// allow_tail (callers with a tail loop, sep_quad_tb_tail_t): lanes whose smallest exponent xs = x - zb
+// exceeds kTailX get tail = 1; their den = a + ssc b' equals a for every phi (kTailX), so f_eq = b'/a and
+// 1 - sign f_eq = 1 exactly, and the lane keeps the delta-f coefficients unscaled (sa = 1) and 1/a
+// folded into the p.dsigma coefficients D0, Dc, Ds, escw: a point is (w p.dsigma f_eq)(1 + delta-f)
+// with no reciprocal (Grad: 5 VALU ops instead of 12).
 IS3D_HD void sep_setup(int flavor, const double* R, const double* Y, double mT, double mT2, double m2, double mTb,
-                       double pT, double sign, double baryon, const double* etab, SepLane& L) {
+                       double pT, double sign, double baryon, const double* etab, SepLane& L, int allow_tail = 0) {
   L.sign = sign;
   L.x = fma(mT, Y[Y_AT], -baryon * R[R_CHEM]);
   const double zb = pT * R[R_ZB];                 // >= max_j |pT B_j / T|
@@ -1095,6 +1120,7 @@ IS3D_HD void sep_setup(int flavor, const double* R, const double* Y, double mT, 
   // a = e^(x - zb) 2^-k is as accurate as e^(x - zb) itself (table exp, ~1 ulp)
   const double xs = L.x - zb;
   L.fast = (xs >= -300.0) ? 1 : 0;
+  L.tail = (allow_tail && xs > kTailX) ? 1 : 0;
   const int k = (L.fast && xs > 150.0) ? (int)((xs - 150.0) * 1.4426950408889634) : 0;
   L.a = L.fast ? exp_tab(exp_tab_coef(), etab, xs * kInvLn2xN, k) : 0.0;
   const double esc = ldexp(1.0, -k);
@@ -1103,24 +1129,17 @@ IS3D_HD void sep_setup(int flavor, const double* R, const double* Y, double mT, 
   if (!L.fast) { L.Zc = R[R_UX] * R[R_INVT]; L.Zs = R[R_UY] * R[R_INVT]; } else { L.Zc = L.Zs = 0.0; }
   L.D0 = esc * (mT * Y[Y_D]); L.Dc = esc * Y[Y_WDX]; L.Ds = esc * Y[Y_WDY];
   // fast lanes carry the delta-f coefficients pre-multiplied by a (see sep_fast_tail)
-  const double sa = L.fast ? L.a : 1.0;
+  const double sa = (L.fast && !L.tail) ? L.a : 1.0;
   L.S0 = sa * fma(mT2, Y[Y_S2], fma(mTb, Y[Y_S1], m2 * R[R_S0M2]));
   L.Sc = sa * fma(mT, Y[Y_SC1], baryon * R[R_SCB]);
   L.Ss = sa * fma(mT, Y[Y_SS1], baryon * R[R_SSB]);
   L.E0 = mT * Y[Y_A]; L.Ec = -R[R_UX]; L.Es = -R[R_UY];
   L.L0 = sa * fma(mT, Y[Y_L1], baryon * R[R_L0B]); L.Lc = sa * R[R_LC]; L.Ls = sa * R[R_LS];
   L.c0 = (flavor == SEP_PTB) ? R[R_DZ] - 3.0 * R[R_DLAM] : 0.0;
-}
-
-// 1/d for finite normal d: v_rcp_f64 (measured max rel. error 4.5e-8 on gfx950) + one
-// Newton step (~2e-15); IEEE division on the host.  Callers guarantee d is finite.
-IS3D_HD double rcp1(double d) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  const double r = __builtin_amdgcn_rcp(d);
-  return fma(r, fma(-d, r, 1.0), r);
-#else
-  return 1.0 / d;
-#endif
+  if (L.tail) {   // f_eq = b' / a: fold 1/a into the p.dsigma coefficients (both carry the same 2^-k)
+    const double ra = rcp1(L.a);
+    L.D0 *= ra; L.Dc *= ra; L.Ds *= ra; L.escw *= ra;
+  }
 }
 
 IS3D_HD double lin(double c0, double cc, double cs, dbl2 p) { return fma(cc, p.x, fma(cs, p.y, c0)); }
@@ -1358,6 +1377,57 @@ IS3D_HD void sep_quad_tb_t(const SepLane& L, double mT, const dbl2* b, const dbl
   }
 }
 
+// sep_quad_tb_t for a Boltzmann-tail lane (sep_setup allow_tail, L.tail = 1): den == a at every point,
+// so with 1/a folded into D0 / escw and the delta-f coefficients unscaled,
+//   Grad    acc += pb (1 + S),            S = S0 + mT T1 + Phi                     5 ops per point
+//   RTA-CE  acc += pb (1 + L + S / E),    L = L0 + T2, E = E0 + TE, one 1/E per four points
+// (pb = w p.dsigma f_eq; regulate clamps delta-f to [-1, 1]; outflow drops points with pb <= 0).
+template <int FL, bool REG, bool OUT>
+IS3D_HD void sep_quad_tb_tail_t(const SepLane& L, double mT, const dbl2* b, const dbl2* pt, const dbl2* pe, double* acc) {
+  constexpr bool needE = FL == SEP_CE;
+  double rE[4] = {0.0, 0.0, 0.0, 0.0};
+  if (needE) {
+    double E[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) E[i] = L.E0 + pe[i].x;
+    const double e01 = E[0] * E[1], e23 = E[2] * E[3];
+    const double r = rcp1(e01 * e23);
+    const double r01 = r * e23, r23 = r * e01;
+    rE[0] = r01 * E[1]; rE[1] = r01 * E[0]; rE[2] = r23 * E[3]; rE[3] = r23 * E[2];
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    double pb = fma(L.D0, b[i].x, L.escw * pt[i].x);
+    if (OUT) pb = (pb <= 0.0) ? 0.0 : pb;
+    const double S = fma(mT, pt[i].y, b[i].y) + L.S0;
+    double t;
+    if (REG) {
+      const double dfv = needE ? fma(S, rE[i], L.L0 + pe[i].y) : S;
+      t = 1.0 + fmax(-1.0, fmin(dfv, 1.0));
+    } else {
+      t = needE ? fma(S, rE[i], (1.0 + L.L0) + pe[i].y) : S + 1.0;
+    }
+    acc[i] = fma(pb, t, acc[i]);
+  }
+}
+
+// Boltzmann-tail Grad fours with the PD table (pd[i]) and {pc, ps} (c[i], SGPR operands when read by
+// scalar loads) instead of the {PD, T1} table: 6 VALU ops and 6 LDS-array cycles per point (b128 + b64)
+// where sep_quad_tb_tail_t needs 5 ops but 8 LDS cycles -- the tail loop is LDS-bound otherwise.
+// acc += pb (1 + S), S = S0 + Sc pc + Ss ps + Phi (unscaled coefficients, sep_setup allow_tail)
+template <bool REG, bool OUT>
+IS3D_HD void sep_quad_pd_tail_t(const SepLane& L, const dbl2* c, const dbl2* b, const double* pd, double* acc) {
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    double pb = fma(L.D0, b[i].x, L.escw * pd[i]);
+    if (OUT) pb = (pb <= 0.0) ? 0.0 : pb;
+    double t;
+    if (REG) t = 1.0 + fmax(-1.0, fmin(lin(L.S0, L.Sc, L.Ss, c[i]) + b[i].y, 1.0));
+    else t = lin(L.S0 + 1.0, L.Sc, L.Ss, c[i]) + b[i].y;
+    acc[i] = fma(pb, t, acc[i]);
+  }
+}
+
 IS3D_HD void sep_quad_pd(int flavor,const SepLane& L, const dbl2* c, const dbl2* b, const double* pd, int regulate,
                          int outflow, double* v) {
 #define IS3D_QUADPD_CASE(FLV)                                                                     \
@@ -1448,6 +1518,7 @@ struct ModLane {
   ExpTabCoef et;               // pinned once per lane setup, reused by every phi point
   const double* etab;          // 2^(j/64) table (LDS on the device)
   int skip, clamp;   // clamp: some point's exp argument may leave exp_tab's domain (exp_clamped instead)
+  int tail;          // Boltzmann tail: en < 2^-54 at every phi point, so 1 + sign en == 1 (mod_quad_tail_t)
 };
 
 // Qv = |pc Vc + ps Vs|^2 for one (cell, phi)
@@ -1481,6 +1552,7 @@ IS3D_HD void mod_setup(const double* R, const double* Y, double mT, double m2, d
   L.skip = (emin * L.invTm - L.chemm > kExpMax + 1.0) ? 1 : 0;
   const double xlo = L.chemm - sqrt(m2 + hi * hi) * L.invTm;
   L.clamp = (xlo > -1.0e6 && L.chemm < 700.0) ? 0 : 1;
+  L.tail = (!L.clamp && emin * L.invTm - L.chemm > kTailX) ? 1 : 0;
 }
 
 // en = exp(chem - E_mod / T_mod) at one phi point (qv = modqv of the cell at this phi)
@@ -1527,6 +1599,20 @@ IS3D_HD void mod_quad_t(const ModLane& L, const dbl2* c, dbl2 qa, dbl2 qb, doubl
     const double pds = lin(L.D0, L.Dc, L.Ds, c[i]);
     const double g = pds * (en[i] * rq[i]);
     v[i] = (OUT && pds <= 0.0) ? 0.0 : g;
+  }
+}
+
+// four points of a Boltzmann-tail lane (L.tail): f = |renorm| en exactly (1 + sign en rounds to 1),
+// accumulated straight into acc -- no reciprocal
+template <bool OUT>
+IS3D_HD void mod_quad_tail_t(const ModLane& L, const dbl2* c, dbl2 qa, dbl2 qb, double* acc) {
+  const double qv[4] = {qa.x, qa.y, qb.x, qb.y};
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const double en = mod_en<false>(L, c[i], qv[i]);
+    double pds = lin(L.D0, L.Dc, L.Ds, c[i]);
+    if (OUT) pds = (pds <= 0.0) ? 0.0 : pds;
+    acc[i] = fma(pds, en, acc[i]);
   }
 }
 

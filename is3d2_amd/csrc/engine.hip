@@ -891,8 +891,12 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   // Grad {PD, T1} table (F_TB, sep_quad_tb_t): exact only without baryon terms (R_SCB = R_SSB = 0);
   // needs one phi block of fours, and the 256 tasks of a workgroup span at most
   // (kBlock - 1) / np + 2 <= kTbQ q values
-  const int tb = (IS3D_GRAD_TB && (mode == GRAD || (mode == CE && IS3D_CE_TB)) && !e->p.include_baryon && njb == 1 && KJ % 4 == 0 &&
-                  (kBlock - 1) / np + 2 <= kTbQ) ? F_TB : 0;
+  // (that span bound holds only when k_spectra builds the y-terms of its lanes' q range, IS3D_YQ_RANGE;
+  // otherwise a workgroup touches all nq rows and the kTbQ-row LDS regions would overflow).
+  // include_baryon = 0 is what makes R_SCB = R_SSB = 0: V^mu and alphaB are only packed when
+  // include_baryon && include_baryondiff_deltaf (prep_grad_ce), and df_eval leaves c1 = c3 = 0 without baryons
+  const int tb = (IS3D_GRAD_TB && IS3D_YQ_RANGE && (mode == GRAD || (mode == CE && IS3D_CE_TB)) && !e->p.include_baryon &&
+                  njb == 1 && KJ % 4 == 0 && (kBlock - 1) / np + 2 <= kTbQ) ? F_TB : 0;
   const size_t shmem = sizeof(double) * (2 * (size_t)kTile * NREC + 2 * (size_t)(kTile + 2) * njb * KJ +
                                          (size_t)kTile * njb * KJ + (size_t)(nk + 2 * nl) +
                                          (size_t)kTile * (tb ? kTbQ : sa.nq) * kYRow + kExpTabN +

@@ -57,7 +57,7 @@ EmissionFunctionArray::EmissionFunctionArray(const ParameterReader& params, cons
 }
 
 static void set_or_throw(is3d_engine* e, int rc) {
-  if (rc != IS3D_OK) throw std::runtime_error(std::string("is3d engine: ") + is3d_last_error(e));
+  if (rc != IS3D_OK) throw EngineError(rc, std::string("is3d engine: ") + is3d_last_error(e));
 }
 
 static is3d_params engine_params(const ParameterReader& p, int operation, int dimension) {
@@ -91,7 +91,8 @@ static is3d_spacetime_bins spacetime_bins(const ParameterReader& p) {
 void EmissionFunctionArray::run_sharded(const RunOptions& opt, int operation) {
   const is3d_params prm = engine_params(p_, operation, dimension_);
   const is3d_spacetime_bins bins = spacetime_bins(p_);
-  const int ndev = std::max(1, opt.num_devices);
+  const int ndev = opt.devices.empty() ? std::max(1, opt.num_devices) : (int)opt.devices.size();
+  auto dev_of = [&](int k) { return opt.devices.empty() ? opt.device + k : opt.devices[k]; };
   std::vector<double> pTv(pT_.cols[0]), phiv(phi_.cols[0]), yv(y_.cols[0]), etav(eta_.cols[0]), etaw(eta_.cols[1]);
   std::vector<double> pTw(pT_.ncols() > 1 ? pT_.cols[1] : std::vector<double>(pTv.size(), 0.0));
   std::vector<double> phiw(phi_.ncols() > 1 ? phi_.cols[1] : std::vector<double>(phiv.size(), 0.0));
@@ -99,10 +100,11 @@ void EmissionFunctionArray::run_sharded(const RunOptions& opt, int operation) {
   const int np = (int)mass_.size();
   std::vector<std::vector<double>> parts(ndev);
   std::vector<std::string> errs(ndev);
+  std::vector<int> codes(ndev, IS3D_ERR_ARG);
   auto t0 = std::chrono::steady_clock::now();
   auto work = [&](int k) {
-    is3d_engine* e = is3d_create(opt.device + k);
-    if (!e) { errs[k] = "is3d_create(" + std::to_string(opt.device + k) + ") failed"; return; }
+    is3d_engine* e = is3d_create(dev_of(k));
+    if (!e) { errs[k] = "is3d_create(" + std::to_string(dev_of(k)) + ") failed"; codes[k] = IS3D_ERR_DEVICE; return; }
     try {
       set_or_throw(e, is3d_set_params(e, &prm));
       set_or_throw(e, is3d_set_species(e, np, mass_.data(), sign_.data(), degen_.data(), baryon_.data()));
@@ -134,6 +136,9 @@ void EmissionFunctionArray::run_sharded(const RunOptions& opt, int operation) {
         parts[k].assign(nt + nr + (long)np * bins.phip_bins, 0.0);
         set_or_throw(e, is3d_calculate_dN_dX(e, parts[k].data(), parts[k].data() + nt, parts[k].data() + nt + nr));
       }
+    } catch (const EngineError& ex) {
+      errs[k] = ex.what();
+      codes[k] = ex.code;
     } catch (const std::exception& ex) {
       errs[k] = ex.what();
     }
@@ -146,7 +151,7 @@ void EmissionFunctionArray::run_sharded(const RunOptions& opt, int operation) {
   std::vector<std::thread> th;
   for (int k = 0; k < ndev; k++) th.emplace_back(work, k);
   for (auto& t : th) t.join();
-  for (int k = 0; k < ndev; k++) if (!errs[k].empty()) throw std::runtime_error(errs[k]);
+  for (int k = 0; k < ndev; k++) if (!errs[k].empty()) throw EngineError(codes[k], errs[k]);
   std::vector<double> sum(parts[0].size(), 0.0);
   for (int k = 0; k < ndev; k++)
     for (size_t i = 0; i < sum.size(); i++) sum[i] += parts[k][i];
@@ -291,13 +296,10 @@ static void put_err(char* buf, int len, const std::string& msg) {
   if (buf && len > 0) { std::strncpy(buf, msg.c_str(), (size_t)len - 1); buf[len - 1] = 0; }
 }
 
-extern "C" int is3d_host_run_particlization(const char* workdir, int device, int num_devices, double* dN_out,
-                                            long out_capacity, char* err, int errlen) {
+static int run_particlization_opt(const char* workdir, RunOptions opt, double* dN_out, long out_capacity, char* err,
+                                  int errlen) {
   try {
     IS3D run(workdir ? workdir : ".");
-    RunOptions opt;
-    opt.device = device;
-    opt.num_devices = num_devices;
     opt.quiet = true;
     run.run_particlization(1, opt);
     const auto& dN = run.spectra();
@@ -306,10 +308,29 @@ extern "C" int is3d_host_run_particlization(const char* workdir, int device, int
       std::copy(dN.begin(), dN.end(), dN_out);
     }
     return IS3D_OK;
+  } catch (const EngineError& ex) {
+    put_err(err, errlen, ex.what());
+    return ex.code;
   } catch (const std::exception& ex) {
     put_err(err, errlen, ex.what());
     return IS3D_ERR_ARG;
   }
+}
+
+extern "C" int is3d_host_run_particlization(const char* workdir, int device, int num_devices, double* dN_out,
+                                            long out_capacity, char* err, int errlen) {
+  RunOptions opt;
+  opt.device = device;
+  opt.num_devices = num_devices;
+  return run_particlization_opt(workdir, opt, dN_out, out_capacity, err, errlen);
+}
+
+extern "C" int is3d_host_run_particlization_devices(const char* workdir, const int* devices, int num_devices,
+                                                    double* dN_out, long out_capacity, char* err, int errlen) {
+  if (!devices || num_devices <= 0) { put_err(err, errlen, "empty device list"); return IS3D_ERR_ARG; }
+  RunOptions opt;
+  opt.devices.assign(devices, devices + num_devices);
+  return run_particlization_opt(workdir, opt, dN_out, out_capacity, err, errlen);
 }
 
 extern "C" int is3d_host_total_yield(const char* workdir, int device, int num_devices, double* n_total,

@@ -12,6 +12,8 @@
 // cells may be sharded over several GPUs in one process.
 #pragma once
 #include <string>
+#include <stdexcept>
+#include <string>
 #include <vector>
 
 #include "../../../include/is3d_amd.h"
@@ -20,9 +22,16 @@
 namespace is3d {
 namespace host {
 
+// engine failure with the is3d_amd.h return code (IS3D_ERR_DF_RANGE for the reference's GSL abort, ...)
+struct EngineError : std::runtime_error {
+  int code;
+  EngineError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
 struct RunOptions {
   int device = 0;          // first HIP device
   int num_devices = 1;     // cells sharded over devices [device, device + num_devices)
+  std::vector<int> devices;  // if not empty: shard k runs on devices[k] (an index may repeat)
   bool write_files = true;
   bool quiet = false;
 };

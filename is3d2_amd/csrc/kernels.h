@@ -96,6 +96,18 @@ constexpr int kTbQ = 4;
 #ifndef IS3D_YQ_RANGE
 #define IS3D_YQ_RANGE 1       // k_spectra builds the y-terms of its lanes' q range only
 #endif
+#ifndef IS3D_TAIL
+#define IS3D_TAIL 1           // Boltzmann-tail lanes skip the per-point reciprocal (kTailX): Grad F_TB 497 -> 481 ms (r2d)
+#endif
+#ifndef IS3D_TAIL_PD
+#define IS3D_TAIL_PD 0        // Grad tail lanes: PD table + scalar {pc, ps} instead of {PD, T1}: 2.2% slower (r2d A/B)
+#endif
+#ifndef IS3D_TAIL_CE
+#define IS3D_TAIL_CE 0        // RTA-CE tail lanes (sep_quad_tb_tail_t): 3% slower on MI355X (r2d A/B: 697 vs 675 ms)
+#endif
+#ifndef IS3D_TAIL_MOD
+#define IS3D_TAIL_MOD 0       // modified-path tail loop (mod_quad_tail_t): 2.5% fewer VALU but 11% slower (r2d: 1445 vs 1297 ms)
+#endif
 #ifndef IS3D_PAIR_RCP
 #define IS3D_PAIR_RCP 1       // fast path: two phi points per reciprocal (sep_pair_t)
 #endif
@@ -256,6 +268,55 @@ __device__ __forceinline__ void sep_phi_loop_tb(const SepLane& L, double mT, con
   }
 }
 
+// Boltzmann-tail lanes of an F_TB launch (sep_setup allow_tail): sep_quad_tb_tail_t, no reciprocal per point
+template <int MODE, int FLAGS, int KJ>
+__device__ __forceinline__ void sep_phi_loop_tb_tail(const SepLane& L, double mT, const dbl2* BP, const dbl2* PT,
+                                                     const dbl2* PE, double* acc) {
+  constexpr int FL = (MODE == GRAD) ? SEP_GRAD : SEP_CE;
+  constexpr bool REG = (FLAGS & F_REG) != 0, OUT = (FLAGS & F_OUT) != 0;
+  static_assert(KJ % 4 == 0, "F_TB needs phi blocks of fours");
+#pragma unroll
+  for (int jj = 0; jj < KJ; jj += 4) {
+    dbl2 b[4], pt[4], pe[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      b[i] = BP[jj + i]; pt[i] = PT[jj + i];
+      if (FL == SEP_CE) pe[i] = PE[jj + i];
+    }
+    sep_quad_tb_tail_t<FL, REG, OUT>(L, mT, b, pt, pe, acc + jj);
+  }
+}
+
+// Boltzmann-tail Grad lanes of an F_TB launch, PD-table form: {b', Phi} and PD from LDS, {pc, ps} by scalar
+// loads (sep_quad_pd_tail_t; 6 LDS-array cycles per point instead of 8)
+template <int FLAGS, int KJ, typename CSP>
+__device__ __forceinline__ void sep_phi_loop_pd_tail(const SepLane& L, CSP CS, const dbl2* BP, const double* PD,
+                                                     double* acc) {
+  constexpr bool REG = (FLAGS & F_REG) != 0, OUT = (FLAGS & F_OUT) != 0;
+#pragma unroll
+  for (int jj = 0; jj < KJ; jj += 4) {
+    dbl2 c[4], b[4];
+    double pd[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) { c[i] = cs_at(CS, jj + i); b[i] = BP[jj + i]; pd[i] = PD[jj + i]; }
+    sep_quad_pd_tail_t<REG, OUT>(L, c, b, pd, acc + jj);
+  }
+}
+
+// Boltzmann-tail modified lanes (M.tail): f = |renorm| en, no reciprocal (mod_quad_tail_t)
+template <int FLAGS, int KJ>
+__device__ __forceinline__ void mod_phi_loop_tail(const ModLane& M, const dbl2* CS, const dbl2* QV, double* acc) {
+  constexpr bool OUT = (FLAGS & F_OUT) != 0;
+  static_assert(KJ % 4 == 0, "tail loop needs phi blocks of fours");
+#pragma unroll
+  for (int jj = 0; jj < KJ; jj += 4) {
+    dbl2 c[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) c[i] = CS[jj + i];
+    mod_quad_tail_t<OUT>(M, c, QV[jj >> 1], QV[(jj >> 1) + 1], acc + jj);
+  }
+}
+
 template <int FLAGS, bool CLAMP, int KJ>
 __device__ __forceinline__ void mod_phi_loop(const ModLane& M, const dbl2* CS, const dbl2* QV, double* acc) {
   constexpr bool OUT = (FLAGS & F_OUT) != 0;
@@ -337,6 +398,8 @@ __global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_spectra(SpecA
   double* s_grid = s_qv + kTile * nphp;                   // y[nk] | eta[nl] | eta_w[nl]
   double* s_y = s_grid + A.nk + 2 * A.nl;                 // [kTile][nq][kYRow]
   constexpr bool TB = (MODE == GRAD || MODE == CE) && (FLAGS & F_TB) != 0 && KJ % 4 == 0;
+  // the TB LDS rows hold kTbQ q values: only the lanes' own q range (IS3D_YQ_RANGE) keeps nqw <= kTbQ
+  static_assert(!TB || IS3D_YQ_RANGE, "the F_TB launch needs IS3D_YQ_RANGE");
   double* s_etab = s_y + (long)kTile * (TB ? kTbQ : A.nq) * kYRow;   // [kExpTabN] exp_tab's 2^(j/kExpTabN)
   // TB: [kTile][kTbQ][nphp] {PD, T1}, 16-byte aligned for ds_read_b128 (s_grid's nk + 2 nl doubles
   // can leave s_etab at an odd double; misaligned dbl2 reads ran the kernel 3.5x slower)
@@ -470,11 +533,18 @@ __global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_spectra(SpecA
         const bool sep = (MODE <= CE) || kind == 1.0 || Y[Y_NARROW] != 0.0;
         if (sep) {
           SepLane L;
-          sep_setup(sep_flavor(MODE), R, Y, mT, mT2, m2, mTb, pT, sign, baryon, s_etab, L);
+          sep_setup(sep_flavor(MODE), R, Y, mT, mT2, m2, mTb, pT, sign, baryon, s_etab, L,
+                    TB && IS3D_TAIL && (MODE == GRAD || IS3D_TAIL_CE));
           if (L.skip) continue;
           if constexpr (TB) {
-            if (L.fast) sep_phi_loop_tb<MODE, FLAGS, KJ>(L, mT, BP, s_pt + ((long)t * kTbQ + (q - q0)) * nphp,
-                                                         s_pe + t * nphp, acc);
+            const dbl2* PT = s_pt + ((long)t * kTbQ + (q - q0)) * nphp;
+            if (IS3D_TAIL && L.tail) {
+              if (MODE == GRAD && IS3D_TAIL_PD)
+                sep_phi_loop_pd_tail<FLAGS, KJ>(L, (cs_sptr)A.csg + 2L * ipt * nphp, BP, s_qv + t * nphp, acc);
+              else
+                sep_phi_loop_tb_tail<MODE, FLAGS, KJ>(L, mT, BP, PT, s_pe + t * nphp, acc);
+            }
+            else if (L.fast) sep_phi_loop_tb<MODE, FLAGS, KJ>(L, mT, BP, PT, s_pe + t * nphp, acc);
             else sep_phi_loop<MODE, FLAGS, false, KJ>(L, s_cs + j0, BP, acc);
           } else if (IS3D_PD_TABLE && IS3D_CS_SCALAR && MODE <= CE && KJ % 4 == 0 && L.fast && A.njb == 1)
             // one phi block: every lane reads the same {pc, ps}, so they come by scalar loads into SGPRs
@@ -490,6 +560,9 @@ __global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_spectra(SpecA
           mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, s_etab, M);
           if (M.skip) continue;
           const dbl2* QV = (const dbl2*)(s_qv + t * nphp + j0);
+          if constexpr (IS3D_TAIL && IS3D_TAIL_MOD && KJ % 4 == 0) {
+            if (M.tail) { mod_phi_loop_tail<FLAGS, KJ>(M, s_cs + j0, QV, acc); continue; }
+          }
           if (M.clamp) mod_phi_loop<FLAGS, true, KJ>(M, s_cs + j0, QV, acc);
           else mod_phi_loop<FLAGS, false, KJ>(M, s_cs + j0, QV, acc);
         }

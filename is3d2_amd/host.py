@@ -17,6 +17,8 @@ def load():
         lib = C.CDLL(LIB_PATH)
         PD, PL, PI = C.POINTER(C.c_double), C.POINTER(C.c_long), C.POINTER(C.c_int)
         lib.is3d_host_run_particlization.argtypes = [C.c_char_p, C.c_int, C.c_int, PD, C.c_long, C.c_char_p, C.c_int]
+        lib.is3d_host_run_particlization_devices.argtypes = [C.c_char_p, PI, C.c_int, PD, C.c_long, C.c_char_p,
+                                                             C.c_int]
         lib.is3d_host_read_surface.restype = C.c_long
         lib.is3d_host_read_surface.argtypes = [C.c_char_p, C.c_int, C.c_int, C.c_int, PD, PD]
         lib.is3d_host_read_pdg.argtypes = [C.c_char_p, C.c_int, C.c_int, PL, PD, PI, PI, PI]
@@ -58,14 +60,34 @@ def param(path, key):
     return v.value
 
 
+class HostError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(msg)
+        self.code = code
+
+
 def run_particlization(workdir, out_size, device=0, num_devices=1):
+    """IS3D::run_particlization on devices [device, device + num_devices); returns the spectra."""
     lib = load()
     out = np.zeros(out_size)
     err = C.create_string_buffer(512)
     rc = lib.is3d_host_run_particlization(workdir.encode(), device, num_devices,
                                           out.ctypes.data_as(C.POINTER(C.c_double)), out_size, err, 512)
     if rc:
-        raise RuntimeError(err.value.decode())
+        raise HostError(rc, err.value.decode())
+    return out
+
+
+def run_particlization_devices(workdir, out_size, devices):
+    """The same with cell shard k on devices[k] (indices may repeat)."""
+    lib = load()
+    out = np.zeros(out_size)
+    err = C.create_string_buffer(512)
+    dv = np.ascontiguousarray(devices, dtype=np.int32)
+    rc = lib.is3d_host_run_particlization_devices(workdir.encode(), dv.ctypes.data_as(C.POINTER(C.c_int)), len(dv),
+                                                  out.ctypes.data_as(C.POINTER(C.c_double)), out_size, err, 512)
+    if rc:
+        raise HostError(rc, err.value.decode())
     return out
 
 

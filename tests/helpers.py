@@ -22,8 +22,9 @@ def emulator():
     return lib
 
 
-def emu_spectra(spec, surf, chains=1, T_avg=None, op=1):
-    """op = 1: spectra [species][pT][phi][y]; op = 0: dN_dy_cell [species][cell]."""
+def emu_spectra(spec, surf, chains=1, T_avg=None, op=1, variant=0):
+    """op = 1: spectra [species][pT][phi][y]; op = 0: dN_dy_cell [species][cell].  variant bits: 1 = the
+    F_TB table algebra (Grad / RTA-CE without baryon), 2 = Boltzmann-tail lanes (cf_emulator.cpp)."""
     lib = emulator()
     inp = O._Inputs(spec, surf, T_avg, 1)
     p = spec["params"]
@@ -33,8 +34,8 @@ def emu_spectra(spec, surf, chains=1, T_avg=None, op=1):
     else:
         out = np.zeros(len(spec["species"]["mass"]) * len(spec["pT"]) * len(spec["phi"]) * ny)
     st = (C.c_long * 4)()
-    rc = lib.emu_spectra(C.byref(inp.params), C.byref(inp.setup), C.byref(inp.surf), int(chains), int(op),
-                         O._p(out), st)
+    rc = lib.emu_spectra_v(C.byref(inp.params), C.byref(inp.setup), C.byref(inp.surf), int(chains), int(op),
+                           O._p(out), st, int(variant))
     if rc:
         raise RuntimeError("emulator rc=%d" % rc)
     return out, list(st)

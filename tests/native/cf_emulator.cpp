@@ -60,8 +60,11 @@ struct EmuTables {
 
 // op = 1: out = dN/(pT dpT dphi dy)[species][pT][phi][y];  op = 0: out = dN_dy_cell[species][cell]
 // (sum over pT, phi, y of w_pT w_phi (w_eta p.dsigma f) x prefactor g, as k_dndx)
-extern "C" int emu_spectra(const orc_params* p, const orc_setup* su, const orc_surface* S, int chains, int op,
-                           double* out, long* stats) {
+// variant bits (k_spectra's launch variants, checked on the CPU): 1 = the F_TB table algebra for Grad /
+// RTA-CE fast lanes without baryon terms (sep_quad_tb_t, phi counts that are multiples of 4), 2 = the
+// Boltzmann-tail lanes (sep_setup allow_tail + sep_quad_tb_tail_t under bit 1; mod_quad_tail_t)
+extern "C" int emu_spectra_v(const orc_params* p, const orc_setup* su, const orc_surface* S, int chains, int op,
+                             double* out, long* stats, int variant) {
   const int mode = p->df_mode, dim = p->dimension;
   const long n = S->n;
   const int np = su->npart, npT = su->npT, nphi = su->nphi;
@@ -120,6 +123,9 @@ extern "C" int emu_spectra(const orc_params* p, const orc_setup* su, const orc_s
   std::vector<double> Yall((size_t)nq * NYT);
   std::vector<dbl2> CS(nphi), BP(nphi);
   std::vector<double> QV(nphi + 1);
+  std::vector<dbl2> PE(nphi), PTq((size_t)nq * nphi);
+  const bool use_tb = (variant & 1) && op != 0 && mode <= CE && !p->include_baryon && nphi % 4 == 0;
+  const bool tail = (variant & 2) != 0 && op != 0;
   std::vector<double> acc((size_t)np * nk * nphi);
   for (int i = 0; i < npT; i++) {
     const double pT = su->pT[i];
@@ -139,7 +145,19 @@ extern "C" int emu_spectra(const orc_params* p, const orc_setup* su, const orc_s
         const double eta = (dim == 3) ? R[R_ETA] : su->eta[l];
         const double w = (dim == 3) ? 1.0 : su->eta_w[l];
         yterms(mode, op, R, y, eta, w, &Yall[(size_t)q * NYT]);
+        if (use_tb) {   // k_spectra's {PD, T1} rows
+          const double* Yq = &Yall[(size_t)q * NYT];
+          for (int j = 0; j < nphi; j++) {
+            PTq[(size_t)q * nphi + j].x = sep_pd(R, CS[j], BP[j].x);
+            PTq[(size_t)q * nphi + j].y = fma(Yq[Y_SC1], CS[j].x, Yq[Y_SS1] * CS[j].y);
+          }
+        }
       }
+      if (use_tb && mode == CE)   // {TE, T2}
+        for (int j = 0; j < nphi; j++) {
+          PE[j].x = -fma(R[R_UX], CS[j].x, R[R_UY] * CS[j].y);
+          PE[j].y = fma(R[R_LC], CS[j].x, R[R_LS] * CS[j].y);
+        }
       if (op == 0) std::fill(acc.begin(), acc.end(), 0.0);
       for (int s = 0; s < np; s++) {
         const double mass = su->mass[s], m2 = mass * mass, sign = su->sign[s], baryon = su->baryon[s];
@@ -157,8 +175,33 @@ extern "C" int emu_spectra(const orc_params* p, const orc_setup* su, const orc_s
             const bool sep = (mode <= CE) || kind == 1.0 || Y[Y_NARROW] != 0.0;
             if (sep) {
               SepLane L;
-              sep_setup(sep_flavor(mode), R, Y, mT, mT * mT, m2, mT * baryon, pT, sign, baryon, kExp2Tab, L);
+              sep_setup(sep_flavor(mode), R, Y, mT, mT * mT, m2, mT * baryon, pT, sign, baryon, kExp2Tab, L,
+                        use_tb && tail);
               if (L.skip) continue;
+              if (use_tb && L.fast) {   // k_spectra's F_TB fours (normal or Boltzmann-tail lanes)
+                const dbl2* PT = &PTq[(size_t)(kk * nl + l) * nphi];
+                for (int j4 = 0; j4 < nphi; j4 += 4) {
+                  const int rg = p->regulate_deltaf, of = p->outflow;
+                  if (L.tail) {
+#define EMU_TAIL(FLV, RG, OF) sep_quad_tb_tail_t<FLV, RG, OF>(L, mT, &BP[j4], &PT[j4], &PE[j4], &a[j4])
+                    if (mode == GRAD) { if (rg) { if (of) EMU_TAIL(SEP_GRAD, true, true); else EMU_TAIL(SEP_GRAD, true, false); }
+                                        else { if (of) EMU_TAIL(SEP_GRAD, false, true); else EMU_TAIL(SEP_GRAD, false, false); } }
+                    else { if (rg) { if (of) EMU_TAIL(SEP_CE, true, true); else EMU_TAIL(SEP_CE, true, false); }
+                           else { if (of) EMU_TAIL(SEP_CE, false, true); else EMU_TAIL(SEP_CE, false, false); } }
+#undef EMU_TAIL
+                  } else {
+                    double v[4];
+#define EMU_TB(FLV, RG, OF) sep_quad_tb_t<FLV, RG, OF>(L, mT, &BP[j4], &PT[j4], &PE[j4], v)
+                    if (mode == GRAD) { if (rg) { if (of) EMU_TB(SEP_GRAD, true, true); else EMU_TB(SEP_GRAD, true, false); }
+                                        else { if (of) EMU_TB(SEP_GRAD, false, true); else EMU_TB(SEP_GRAD, false, false); } }
+                    else { if (rg) { if (of) EMU_TB(SEP_CE, true, true); else EMU_TB(SEP_CE, true, false); }
+                           else { if (of) EMU_TB(SEP_CE, false, true); else EMU_TB(SEP_CE, false, false); } }
+#undef EMU_TB
+                    for (int i = 0; i < 4; i++) a[j4 + i] += v[i];
+                  }
+                }
+                continue;
+              }
               // same arithmetic as k_spectra: fast lanes evaluate phi points in fours (phi blocks that
               // are multiples of 4) or pairs sharing one reciprocal (an odd tail point alone)
               int j = 0;
@@ -190,6 +233,12 @@ extern "C" int emu_spectra(const orc_params* p, const orc_setup* su, const orc_s
               mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, kExp2Tab, M);
               if (M.skip) continue;
               int j = 0;
+              if (tail && M.tail && spectra_kj(nphi) % 4 == 0)     // k_spectra's tail fours
+                for (; j + 3 < nphi; j += 4) {
+                  dbl2 qa, qb; qa.x = QV[j]; qa.y = QV[j + 1]; qb.x = QV[j + 2]; qb.y = QV[j + 3];
+                  if (p->outflow) mod_quad_tail_t<true>(M, &CS[j], qa, qb, &a[j]);
+                  else mod_quad_tail_t<false>(M, &CS[j], qa, qb, &a[j]);
+                }
               if (op != 0 && spectra_kj(nphi) % 4 == 0)       // k_spectra's fours; k_dndx pairs
                 for (; j + 3 < nphi; j += 4) {
                   double v[4];
@@ -233,6 +282,11 @@ extern "C" int emu_spectra(const orc_params* p, const orc_setup* su, const orc_s
   }
   if (stats) { stats[0] = st_break; stats[1] = st_pl; stats[2] = st_fail; stats[3] = st_it; }
   return 0;
+}
+
+extern "C" int emu_spectra(const orc_params* p, const orc_setup* su, const orc_surface* S, int chains, int op,
+                           double* out, long* stats) {
+  return emu_spectra_v(p, su, S, chains, op, out, stats, 0);
 }
 
 // the device exp used by the spectra kernel (exp_dom690 / exp_clamped), evaluated on the host

@@ -150,3 +150,58 @@ def test_dropin_oversampling_estimate_matches_oracle(tmp_path, dim, mode, oversa
     ref, _ = O.total_yield(spec, surf, avg, y_cut=0.75)
     assert abs(ntot - ref) <= 1e-12 * abs(ref)
     assert nev == int(min(np.ceil(1.0e7 / ref), 1.0e4))
+
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def _shipped_surface_run_dir(tmp_path):
+    """A run directory around the reference's only shipped input, input/surface.dat (one 26-column
+    cell in the retired GPU-VH layout, kept as data in tests/golden/reference_input_surface.dat), read
+    as BASELINE config 1 reads it: mode 1, 2+1D, pikp, Grad."""
+    s = synth.surface(4, seed=1, dimension=2)
+    params = dict(dimension=2, df_mode=1, include_baryon=0, include_bulk_deltaf=1, include_shear_deltaf=1,
+                  include_baryondiff_deltaf=0, regulate_deltaf=0, outflow=0, deta_min=1e-5, mass_pion0=0.138)
+    d = rundir.write_run_dir(str(tmp_path), s, params, hrg_eos=2, chosen="pikp", surface_format=1)
+    with open(os.path.join(GOLDEN, "reference_input_surface.dat")) as f, \
+            open(os.path.join(d, "input", "surface.dat"), "w") as g:
+        g.write(f.read())
+    return d
+
+
+@need_ref
+def test_shipped_surface_reader_matches_reference(tmp_path):
+    # the mis-parse pinned bit for bit: column 13 (1.40186 fm^-1) is read as T, so T = 0.2766 GeV
+    d = _shipped_surface_run_dir(tmp_path)
+    out = harness(["surface"], d).strip().split("\n")
+    assert int(out[0]) == 1
+    ref = np.array([float(v) for v in out[1].split()])
+    ref_avg = np.array([float(v) for v in out[2].split()])
+    fields, avg = host.read_surface(d, 1, 2, 0)
+    for k, name in enumerate(synth.FIELDS):
+        if name in ("muB", "nB", "Vx", "Vy", "Vn"):
+            continue
+        assert fields[k][0] == ref[k], name
+    np.testing.assert_array_equal(avg, ref_avg)
+    assert abs(fields[synth.FIELDS.index("T")][0] - 1.40186 * 0.197327053) < 1e-15
+
+
+def test_shipped_surface_is_outside_the_df_tables_in_the_oracle(tmp_path):
+    # the reference aborts in gsl_spline_eval ("interpolation error"): T = 0.2766 GeV > 0.2 GeV table edge
+    d = _shipped_surface_run_dir(tmp_path)
+    fields, avg = host.read_surface(d, 1, 2, 0)
+    surf = {k: fields[i] for i, k in enumerate(synth.FIELDS)}
+    spec = make_spec(hrg_eos=2, chosen="pikp", df_mode=1, dimension=2)
+    with pytest.raises(RuntimeError, match="interpolation"):
+        O.spectra(spec, surf, T_avg=avg[0])
+
+
+@pytest.mark.gpu
+def test_shipped_surface_dropin_returns_df_range_error(tmp_path):
+    # the drop-in workflow on the reference's own input: IS3D_ERR_DF_RANGE with the GSL message
+    # instead of the reference's abort
+    from is3d2_amd import _lib
+    d = _shipped_surface_run_dir(tmp_path)
+    with pytest.raises(host.HostError, match="interpolation") as ei:
+        host.run_particlization(d, 3 * 24 * 24)
+    assert ei.value.code == _lib.IS3D_ERR_DF_RANGE

@@ -105,3 +105,36 @@ def test_kernel_sinh_cosh_accuracy():
     assert (np.abs(sh[nz] - np.sinh(x[nz])) <= 4 * np.spacing(np.abs(np.sinh(x[nz])))).all()
     assert (np.abs(ch - np.cosh(x)) <= 4 * np.spacing(np.cosh(x))).all()
     assert sh[x == 0].tolist() == [0.0] and ch[x == 0].tolist() == [1.0]
+
+
+@pytest.mark.parametrize("dim,mode,reg_out", [(3, 1, (0, 0)), (3, 1, (1, 1)), (3, 1, (1, 0)), (3, 1, (0, 1)),
+                                               (3, 2, (0, 0)), (3, 2, (1, 1)), (2, 1, (0, 0)), (2, 2, (1, 0))])
+def test_table_and_tail_algebra(dim, mode, reg_out):
+    """k_spectra's F_TB algebra (variant 1, sep_quad_tb_t: linear delta-f part from the {PD, T1} / {TE, T2}
+    tables) and its Boltzmann-tail lanes (variant 3, sep_quad_tb_tail_t: den == a, no reciprocal) on the
+    host, against the oracle: every regulate / outflow variant, 2+1D lanes with w_eta != 1 (escw), and the
+    3+1D grid's 2^-k-scaled lanes (x - zb > 150).  Same bar as the GPU tier: entries that sum
+    mixed-sign contributions keep ~1e-10 relative (measured 1e-10..3e-9 for every variant alike)."""
+    s = synth.as_read(synth.surface(6, seed=19, dimension=dim, full3d=(dim == 3)))
+    spec = make_spec(hrg_eos=2, chosen="smash", df_mode=mode, dimension=dim, pT="pT24", phi="phi24",
+                     regulate_deltaf=reg_out[0], outflow=reg_out[1])
+    ref = O.spectra(spec, s, threads=1)
+    base, _ = emu_spectra(spec, s)
+    for variant in (1, 3):
+        got, _ = emu_spectra(spec, s, variant=variant)
+        rel, zr, zg = parity(got, ref, floor=1e-290)
+        assert rel < 1e-8, (variant, rel)
+        assert zr == zg
+        assert not np.array_equal(got, base)       # the variant's arithmetic really ran
+
+
+@pytest.mark.parametrize("mode", [3, 4, 5])
+def test_modified_tail_lanes(mode):
+    """mod_quad_tail_t (f = |renorm| en where 1 + sign en == 1) against the oracle on the config-2 grid."""
+    s = synth.as_read(synth.surface(6, seed=23, dimension=3, full3d=True))
+    spec = make_spec(hrg_eos=2, chosen="smash", df_mode=mode, dimension=3, pT="pT24", phi="phi32", famod_chains=1)
+    ref = O.spectra(spec, s, threads=1)
+    got, _ = emu_spectra(spec, s, chains=1, variant=2)
+    rel, zr, zg = parity(got, ref, floor=1e-290)
+    assert rel < 1e-8, rel
+    assert zr == zg

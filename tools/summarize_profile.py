@@ -1,12 +1,13 @@
 #!/usr/bin/env python3
-"""Fold a tools/profile_round.sh output directory into committed summaries under profiles/.
+"""Fold a tools/profile_round.sh / profile_modes.sh output directory into committed summaries under profiles/.
 
   profiles/<tag>_kernel_stats.csv   rocprofv3 --kernel-trace --stats summary (verbatim)
   profiles/<tag>_pmc.json           per-kernel averages of the PMC passes
   profiles/pmc_traffic.json         HBM bytes per k_spectra launch, keyed "<config>_mode<m>",
                                     read by bench.py for roofline.traffic
-  profiles/pmc_valu.json            k_spectra VALU instructions, issue fraction and clock, same keys,
-                                    read by bench.py for roofline.executed
+  profiles/pmc_valu.json            k_spectra executed-work counters (VALU instructions, the FP64
+                                    ADD/MUL/FMA/TRANS mix, FP64 flops, issue fraction, clock), same
+                                    keys, read by bench.py for the executed roofline (roofline.achieved)
 
 HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (KiB -> B): on gfx950 FETCH_SIZE counts
 half the bytes of wide coalesced reads (MI355X_MICROARCH.md, HBM section); WRITE_SIZE is exact
@@ -49,7 +50,7 @@ def main():
     os.makedirs(prof, exist_ok=True)
     shutil.copy(os.path.join(d, "trace", "run_kernel_stats.csv"), os.path.join(prof, "%s_kernel_stats.csv" % tag))
     out = {}
-    for sub in ("pmcA", "pmcB", "pmcC", "pmcD"):
+    for sub in ("pmcA", "pmcB", "pmcC", "pmcD", "pmcE"):
         p = os.path.join(d, sub, "run_counter_collection.csv")
         if not os.path.exists(p):
             continue
@@ -86,6 +87,13 @@ def main():
         e = out[spec[0]]
         v[key] = {"tag": tag, "valu_insts_per_launch": e["SQ_INSTS_VALU"], "valu_issue_frac": e["valu_issue_frac"],
                   "clock_ghz": e["clock_ghz"]}
+        for c in ("ADD_F64", "MUL_F64", "FMA_F64", "TRANS_F64", "INT32", "INT64", "CVT"):
+            if "SQ_INSTS_VALU_" + c in e:
+                v[key][c.lower() + "_insts_per_launch"] = e["SQ_INSTS_VALU_" + c]
+        if "SQ_INSTS_VALU_FLOPS_FP64" in e:
+            v[key]["fp64_flops_per_launch"] = e["SQ_INSTS_VALU_FLOPS_FP64"]
+        if "SQ_LDS_BANK_CONFLICT" in e:
+            v[key]["lds_bank_conflict_cycles"] = e["SQ_LDS_BANK_CONFLICT"]
         json.dump(v, open(vp, "w"), indent=1, sort_keys=True)
     for k, e in sorted(out.items()):
         print(k, {c: round(v, 3) for c, v in e.items()})
