@@ -1514,6 +1514,7 @@ IS3D_HD double sqrt_nr(double v) {
 // where the reference's exp overflows to 1/inf = 0.  |renorm| is folded into p.dsigma.
 struct ModLane {
   double E0, Ec, Es, D0, Dc, Ds, invTm, chemm, sign;
+  double mT, Dw;               // table form (mod_quad_tab_t): E_mod^2 = E0 + Qv + mT T2, p.dsigma = D0 + Dw PDm
   double invTmN, chemmN;       // invTm, chemm x 64/ln2 (exp_tab's scaled argument)
   ExpTabCoef et;               // pinned once per lane setup, reused by every phi point
   const double* etab;          // 2^(j/64) table (LDS on the device)
@@ -1538,6 +1539,7 @@ IS3D_HD void mod_setup(const double* R, const double* Y, double mT, double m2, d
   L.Ec = tm * fma(ux, R[R_VCX], fma(uy, R[R_VCY], uz * R[R_VCZ]));
   L.Es = tm * fma(ux, R[R_VSX], fma(uy, R[R_VSY], uz * R[R_VSZ]));
   L.D0 = renorm_abs * (mT * Y[Y_MD]); L.Dc = renorm_abs * Y[Y_WDX]; L.Ds = renorm_abs * Y[Y_WDY];
+  L.mT = mT; L.Dw = renorm_abs * Y[Y_W];
   L.sign = sign;
   L.invTm = R[R_INVTM]; L.chemm = baryon * R[R_CHEMM];
   L.invTmN = L.invTm * kInvLn2xN; L.chemmN = L.chemm * kInvLn2xN;
@@ -1600,6 +1602,66 @@ IS3D_HD void mod_quad_t(const ModLane& L, const dbl2* c, dbl2 qa, dbl2 qb, doubl
     const double g = pds * (en[i] * rq[i]);
     v[i] = (OUT && pds <= 0.0) ? 0.0 : g;
   }
+}
+
+// ---- table form of the modified path (k_spectra).  Per (cell, phi) the workgroup stores
+//   MW = {PDm, Qv},  PDm = dsigma_x pc + dsigma_y ps,  Qv = |W|^2  (W = pc Vc + ps Vs)
+// and per (cell, q, phi)  T2 = 2 U_q . W  (modt2), so a point needs
+//   E_mod^2 = fma(mT, T2, E0 + Qv)   and   p.dsigma |renorm| = fma(Dw, PDm, D0)
+// -- 3 VALU ops where the lane's linear forms took 5 -- and no {pc, ps} operands.
+IS3D_HD double modpdm(const double* R, dbl2 cs) { return fma(R[R_DAX], cs.x, R[R_DAY] * cs.y); }
+IS3D_HD double modt2(const double* R, const double* Y, dbl2 cs) {
+  const double wx = fma(cs.x, R[R_VCX], cs.y * R[R_VSX]);
+  const double wy = fma(cs.x, R[R_VCY], cs.y * R[R_VSY]);
+  const double wz = fma(cs.x, R[R_VCZ], cs.y * R[R_VSZ]);
+  return 2.0 * fma(Y[Y_MUX], wx, fma(Y[Y_MUY], wy, Y[Y_MUZ] * wz));
+}
+
+// en = exp(chem - sqrt(X) / T_mod): one Newton step of the v_rsq_f64 estimate y folded into the exp
+// argument, sqrt(X) = g v with g = X y, v = 1.5 - 0.5 g y (5 ops where sqrt_nr + fma took 6)
+template <bool CLAMP>
+IS3D_HD double mod_en_x(const ModLane& L, double X) {
+  if (CLAMP) return exp_clamped(exp_coef(), fma(-sqrt_nr(X), L.invTm, L.chemm));
+#if defined(__HIP_DEVICE_COMPILE__)
+  const double y = __builtin_amdgcn_rsq(X);
+#else
+  const double y = 1.0 / sqrt(X);
+#endif
+  const double g = X * y;
+  const double v = fma(-0.5, g * y, 1.5);
+  return exp_tab(L.et, L.etab, fma(-(g * L.invTmN), v, L.chemmN));
+}
+
+template <bool OUT, bool CLAMP>
+IS3D_HD void mod_quad_tab_t(const ModLane& L, const dbl2* mw, const double* mt, double* v) {
+  double en[4], q[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    en[i] = mod_en_x<CLAMP>(L, fma(L.mT, mt[i], L.E0 + mw[i].y));
+    q[i] = fma(L.sign, en[i], 1.0);
+  }
+  const double q01 = q[0] * q[1], q23 = q[2] * q[3];
+  const double r = rcp1(q01 * q23);
+  const double r01 = r * q23, r23 = r * q01;
+  const double rq[4] = {r01 * q[1], r01 * q[0], r23 * q[3], r23 * q[2]};
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const double pds = fma(L.Dw, mw[i].x, L.D0);
+    const double g = pds * (en[i] * rq[i]);
+    v[i] = (OUT && pds <= 0.0) ? 0.0 : g;
+  }
+}
+
+template <bool OUT, bool CLAMP>
+IS3D_HD void mod_pair_tab_t(const ModLane& L, dbl2 mw0, dbl2 mw1, double mt0, double mt1, double& v0, double& v1) {
+  const double en0 = mod_en_x<CLAMP>(L, fma(L.mT, mt0, L.E0 + mw0.y));
+  const double en1 = mod_en_x<CLAMP>(L, fma(L.mT, mt1, L.E0 + mw1.y));
+  const double q0 = fma(L.sign, en0, 1.0), q1 = fma(L.sign, en1, 1.0);
+  const double r = rcp1(q0 * q1);
+  const double pds0 = fma(L.Dw, mw0.x, L.D0), pds1 = fma(L.Dw, mw1.x, L.D0);
+  const double g0 = pds0 * (en0 * (r * q1)), g1 = pds1 * (en1 * (r * q0));
+  v0 = (OUT && pds0 <= 0.0) ? 0.0 : g0;
+  v1 = (OUT && pds1 <= 0.0) ? 0.0 : g1;
 }
 
 // four points of a Boltzmann-tail lane (L.tail): f = |renorm| en exactly (1 + sign en rounds to 1),

@@ -895,13 +895,19 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   // otherwise a workgroup touches all nq rows and the kTbQ-row LDS regions would overflow).
   // include_baryon = 0 is what makes R_SCB = R_SSB = 0: V^mu and alphaB are only packed when
   // include_baryon && include_baryondiff_deltaf (prep_grad_ce), and df_eval leaves c1 = c3 = 0 without baryons
+  // q rows one workgroup's 256 consecutive tasks can span: with one phi block they are a contiguous q range
+  // of at most (kBlock - 1) / np + 2 values (IS3D_YQ_RANGE), otherwise every q
+  const int nqmax = (IS3D_YQ_RANGE && njb == 1) ? (int)std::min<long>(sa.nq, (kBlock - 1) / np + 2) : sa.nq;
+  sa.nqmax = nqmax;
   const int tb = (IS3D_GRAD_TB && IS3D_YQ_RANGE && (mode == GRAD || (mode == CE && IS3D_CE_TB)) && !e->p.include_baryon &&
-                  njb == 1 && KJ % 4 == 0 && (kBlock - 1) / np + 2 <= kTbQ) ? F_TB : 0;
-  const size_t shmem = sizeof(double) * (2 * (size_t)kTile * NREC + 2 * (size_t)(kTile + 2) * njb * KJ +
-                                         (size_t)kTile * njb * KJ + (size_t)(nk + 2 * nl) +
-                                         (size_t)kTile * (tb ? kTbQ : sa.nq) * kYRow + kExpTabN +
-                                         (tb ? 2 * (size_t)kTile * kTbQ * KJ + 1 : 0) +
-                                         (tb && mode == CE ? 2 * (size_t)kTile * KJ : 0));
+                  njb == 1 && KJ % 4 == 0 && nqmax <= kTbQ) ? F_TB : 0;
+  const size_t nphp = (size_t)njb * KJ;
+  const size_t shmem = sizeof(double) * (2 * (size_t)kTile * NREC + 2 * (size_t)(kTile + 2) * nphp +
+                                         2 * (size_t)kTile * nphp + (size_t)(nk + 2 * nl) +
+                                         (size_t)kTile * nqmax * kYRow + kExpTabN +
+                                         (tb ? 2 * (size_t)kTile * nqmax * nphp + 1 : 0) +
+                                         (tb && mode == CE ? 2 * (size_t)kTile * nphp : 0) +
+                                         (mode >= PTM ? (size_t)kTile * nqmax * nphp + 1 : 0));
   if (shmem > 160 * 1024) return e->fail(IS3D_ERR_ARG, "momentum grid too large for the LDS tile");
   const dim3 grid((unsigned)(bx * npT * nsplit));
   const int kflags = (e->p.regulate_deltaf ? F_REG : 0) | (e->p.outflow ? F_OUT : 0) | tb;

@@ -52,6 +52,7 @@ struct SpecArgs {
   const double *pT, *cphi, *sphi, *yv, *etav, *etaw;
   const double* csg;          // [npT][nphp] {pT cos, pT sin} (read by scalar loads when njb == 1)
   int npart, npT, nphi, ny_out, nk, nl, nq, njb;
+  int nqmax;                  // q rows a workgroup's lanes can span (LDS rows of the y-term / q tables)
   long ntask;                 // npart * nq * njb lanes per pT: (species, q = y x eta node, phi block)
   long cells_per_split;
   int nbx, nsplit;            // lane groups per pT, cell splits (1-D grid of nbx * npT * nsplit)
@@ -317,6 +318,40 @@ __device__ __forceinline__ void mod_phi_loop_tail(const ModLane& M, const dbl2* 
   }
 }
 
+// modified lanes of k_spectra, table form: {PDm, Qv} (MW) and T2 (MT) rows, four points per reciprocal
+template <int FLAGS, bool CLAMP, int KJ>
+__device__ __forceinline__ void mod_phi_loop_tab(const ModLane& M, const dbl2* MW, const double* MT, double* acc) {
+  constexpr bool OUT = (FLAGS & F_OUT) != 0;
+  if (IS3D_MOD_QUAD && KJ % 4 == 0) {
+    // the next four points' table rows are loaded before the current four are evaluated (at 2 waves per
+    // SIMD the LDS latency is not hidden by other waves)
+    dbl2 mw[4];
+    double mt[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) { mw[i] = MW[i]; mt[i] = MT[i]; }
+#pragma unroll
+    for (int jj = 0; jj < KJ; jj += 4) {
+      dbl2 nw[4];
+      double nt[4], v[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        nw[i] = mw[i]; nt[i] = mt[i];
+        if (jj + 4 < KJ) { nw[i] = MW[jj + 4 + i]; nt[i] = MT[jj + 4 + i]; }
+      }
+      mod_quad_tab_t<OUT, CLAMP>(M, mw, mt, v);
+#pragma unroll
+      for (int i = 0; i < 4; i++) { acc[jj + i] += v[i]; mw[i] = nw[i]; mt[i] = nt[i]; }
+    }
+    return;
+  }
+#pragma unroll
+  for (int jj = 0; jj < KJ; jj += 2) {
+    double v0, v1;
+    mod_pair_tab_t<OUT, CLAMP>(M, MW[jj], MW[jj + 1], MT[jj], MT[jj + 1], v0, v1);
+    acc[jj] += v0; acc[jj + 1] += v1;
+  }
+}
+
 template <int FLAGS, bool CLAMP, int KJ>
 __device__ __forceinline__ void mod_phi_loop(const ModLane& M, const dbl2* CS, const dbl2* QV, double* acc) {
   constexpr bool OUT = (FLAGS & F_OUT) != 0;
@@ -394,17 +429,21 @@ __global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_spectra(SpecA
   dbl2* s_trig = (dbl2*)(s_recb + 2 * kTile * NREC);      // [nphp]        {cos, sin}
   dbl2* s_cs = s_trig + nphp;                             // [nphp]        {pT cos, pT sin}
   dbl2* s_bp = s_cs + nphp;                               // [kTile][nphp] {b', Phi}
-  double* s_qv = (double*)(s_bp + kTile * nphp);         // [kTile][nphp]  Qv (modified path)
-  double* s_grid = s_qv + kTile * nphp;                   // y[nk] | eta[nl] | eta_w[nl]
-  double* s_y = s_grid + A.nk + 2 * A.nl;                 // [kTile][nq][kYRow]
+  // Grad / RTA-CE: [kTile][nphp] PD table; modified path: [kTile][nphp] {PDm, Qv} pairs (s_mw)
+  double* s_qv = (double*)(s_bp + kTile * nphp);
+  dbl2* s_mw = (dbl2*)s_qv;
+  double* s_grid = s_qv + 2 * kTile * nphp;               // y[nk] | eta[nl] | eta_w[nl]
+  const int nqm = A.nqmax;                                // q rows per cell (>= every workgroup's nqw)
+  double* s_y = s_grid + A.nk + 2 * A.nl;                 // [kTile][nqm][kYRow]
   constexpr bool TB = (MODE == GRAD || MODE == CE) && (FLAGS & F_TB) != 0 && KJ % 4 == 0;
-  // the TB LDS rows hold kTbQ q values: only the lanes' own q range (IS3D_YQ_RANGE) keeps nqw <= kTbQ
+  // the q-row tables hold nqm <= nq rows: only the lanes' own q range (IS3D_YQ_RANGE) bounds nqw below nq
   static_assert(!TB || IS3D_YQ_RANGE, "the F_TB launch needs IS3D_YQ_RANGE");
-  double* s_etab = s_y + (long)kTile * (TB ? kTbQ : A.nq) * kYRow;   // [kExpTabN] exp_tab's 2^(j/kExpTabN)
-  // TB: [kTile][kTbQ][nphp] {PD, T1}, 16-byte aligned for ds_read_b128 (s_grid's nk + 2 nl doubles
+  double* s_etab = s_y + (long)kTile * nqm * kYRow;       // [kExpTabN] exp_tab's 2^(j/kExpTabN)
+  // TB: [kTile][nqm][nphp] {PD, T1}, 16-byte aligned for ds_read_b128 (s_grid's nk + 2 nl doubles
   // can leave s_etab at an odd double; misaligned dbl2 reads ran the kernel 3.5x slower)
   dbl2* s_pt = (dbl2*)(smem + (((s_etab + kExpTabN) - smem + 1) & ~1L));
-  dbl2* s_pe = s_pt + kTile * kTbQ * nphp;                // TB, RTA-CE: [kTile][nphp] {TE, T2}
+  dbl2* s_pe = s_pt + kTile * nqm * nphp;                 // TB, RTA-CE: [kTile][nphp] {TE, T2}
+  double* s_mt = (double*)s_pt;                           // modified path: [kTile][nqm][nphp] T2 = 2 U_q . W
 
   const int tid = threadIdx.x;
   for (int i = tid; i < kExpTabN; i += kBlock) s_etab[i] = kExp2Tab[i];
@@ -482,8 +521,12 @@ __global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_spectra(SpecA
         if (MODE >= PTM && R[R_KIND] == 2.0) qv = modqv(R, s_cs[j]);
       }
       s_bp[t * nphp + j] = v;
-      // s_qv holds Qv on the modified path and the PD table (sep_pd) for Grad / RTA-CE
-      s_qv[t * nphp + j] = (MODE >= PTM) ? qv : sep_pd(R, s_cs[j], v.x);
+      if constexpr (MODE >= PTM) {
+        dbl2 mw; mw.x = modpdm(R, s_cs[j]); mw.y = qv;     // zero rows / padding give 0
+        s_mw[t * nphp + j] = mw;
+      } else {
+        s_qv[t * nphp + j] = sep_pd(R, s_cs[j], v.x);     // PD table (sep_pd)
+      }
       if constexpr (TB && MODE == CE) {
         const dbl2 c = s_cs[j];
         dbl2 e;
@@ -504,6 +547,16 @@ __global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_spectra(SpecA
       }
     }
     lds_barrier();
+    if constexpr (MODE >= PTM) {
+      // T2 = 2 U_q . W per (cell, q, phi) of the modified cells (mod_quad_tab_t)
+      for (int idx = tid; idx < nt * nqw * nphp; idx += kBlock) {
+        const int j = idx % nphp, r = idx / nphp, qq = r % nqw, t = r / nqw;
+        const double* R = s_rec + t * NREC;
+        if (R[R_KIND] != 2.0) continue;
+        s_mt[((long)t * nqw + qq) * nphp + j] = modt2(R, s_y + ((long)t * nqw + qq) * kYRow, s_cs[j]);
+      }
+      lds_barrier();
+    }
     if constexpr (TB) {
       // {PD, T1 = SC1 pc + SS1 ps} per (cell, q, phi) (rows of skipped cells are never read)
       for (int idx = tid; idx < nt * nqw * nphp; idx += kBlock) {
@@ -513,7 +566,7 @@ __global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_spectra(SpecA
         dbl2 v;
         v.x = s_qv[t * nphp + j];
         v.y = fma(Y[Y_SC1], c.x, Y[Y_SS1] * c.y);
-        s_pt[((long)t * kTbQ + qq) * nphp + j] = v;
+        s_pt[((long)t * nqw + qq) * nphp + j] = v;
       }
       lds_barrier();
     }
@@ -537,7 +590,7 @@ __global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_spectra(SpecA
                     TB && IS3D_TAIL && (MODE == GRAD || IS3D_TAIL_CE));
           if (L.skip) continue;
           if constexpr (TB) {
-            const dbl2* PT = s_pt + ((long)t * kTbQ + (q - q0)) * nphp;
+            const dbl2* PT = s_pt + ((long)t * nqw + (q - q0)) * nphp;
             if (IS3D_TAIL && L.tail) {
               if (MODE == GRAD && IS3D_TAIL_PD)
                 sep_phi_loop_pd_tail<FLAGS, KJ>(L, (cs_sptr)A.csg + 2L * ipt * nphp, BP, s_qv + t * nphp, acc);
@@ -559,12 +612,10 @@ __global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_spectra(SpecA
           ModLane M;
           mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, s_etab, M);
           if (M.skip) continue;
-          const dbl2* QV = (const dbl2*)(s_qv + t * nphp + j0);
-          if constexpr (IS3D_TAIL && IS3D_TAIL_MOD && KJ % 4 == 0) {
-            if (M.tail) { mod_phi_loop_tail<FLAGS, KJ>(M, s_cs + j0, QV, acc); continue; }
-          }
-          if (M.clamp) mod_phi_loop<FLAGS, true, KJ>(M, s_cs + j0, QV, acc);
-          else mod_phi_loop<FLAGS, false, KJ>(M, s_cs + j0, QV, acc);
+          const dbl2* MW = s_mw + t * nphp + j0;
+          const double* MT = s_mt + ((long)t * nqw + (q - q0)) * nphp + j0;
+          if (M.clamp) mod_phi_loop_tab<FLAGS, true, KJ>(M, MW, MT, acc);
+          else mod_phi_loop_tab<FLAGS, false, KJ>(M, MW, MT, acc);
         }
       }
     }

@@ -62,7 +62,8 @@ struct EmuTables {
 // (sum over pT, phi, y of w_pT w_phi (w_eta p.dsigma f) x prefactor g, as k_dndx)
 // variant bits (k_spectra's launch variants, checked on the CPU): 1 = the F_TB table algebra for Grad /
 // RTA-CE fast lanes without baryon terms (sep_quad_tb_t, phi counts that are multiples of 4), 2 = the
-// Boltzmann-tail lanes (sep_setup allow_tail + sep_quad_tb_tail_t under bit 1; mod_quad_tail_t)
+// Boltzmann-tail lanes (sep_setup allow_tail + sep_quad_tb_tail_t under bit 1; mod_quad_tail_t),
+// 4 = the modified path's table form (mod_quad_tab_t / mod_pair_tab_t)
 extern "C" int emu_spectra_v(const orc_params* p, const orc_setup* su, const orc_surface* S, int chains, int op,
                              double* out, long* stats, int variant) {
   const int mode = p->df_mode, dim = p->dimension;
@@ -233,6 +234,38 @@ extern "C" int emu_spectra_v(const orc_params* p, const orc_setup* su, const orc
               mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, kExp2Tab, M);
               if (M.skip) continue;
               int j = 0;
+              if ((variant & 4) && op != 0) {   // k_spectra's table form: {PDm, Qv} and T2 rows
+                std::vector<dbl2> MW(nphi);
+                std::vector<double> MT(nphi);
+                for (int jj = 0; jj < nphi; jj++) {
+                  MW[jj].x = modpdm(R, CS[jj]); MW[jj].y = QV[jj];
+                  MT[jj] = modt2(R, Y, CS[jj]);
+                }
+                const bool of = p->outflow != 0;
+                if (spectra_kj(nphi) % 4 == 0)
+                  for (; j + 3 < nphi; j += 4) {
+                    double v[4];
+                    if (M.clamp) { if (of) mod_quad_tab_t<true, true>(M, &MW[j], &MT[j], v); else mod_quad_tab_t<false, true>(M, &MW[j], &MT[j], v); }
+                    else { if (of) mod_quad_tab_t<true, false>(M, &MW[j], &MT[j], v); else mod_quad_tab_t<false, false>(M, &MW[j], &MT[j], v); }
+                    for (int i = 0; i < 4; i++) a[j + i] += v[i];
+                  }
+                for (; j + 1 < nphi; j += 2) {
+                  double v0, v1;
+                  if (M.clamp) { if (of) mod_pair_tab_t<true, true>(M, MW[j], MW[j + 1], MT[j], MT[j + 1], v0, v1); else mod_pair_tab_t<false, true>(M, MW[j], MW[j + 1], MT[j], MT[j + 1], v0, v1); }
+                  else { if (of) mod_pair_tab_t<true, false>(M, MW[j], MW[j + 1], MT[j], MT[j + 1], v0, v1); else mod_pair_tab_t<false, false>(M, MW[j], MW[j + 1], MT[j], MT[j + 1], v0, v1); }
+                  a[j] += v0; a[j + 1] += v1;
+                }
+                // an odd last point: k_spectra pads the phi row (zero {PDm, Qv, T2} rows contribute 0)
+                if (j < nphi) {
+                  dbl2 z; z.x = 0.0; z.y = 0.0;
+                  double v0, v1;
+                  if (M.clamp) mod_pair_tab_t<false, true>(M, MW[j], z, MT[j], 0.0, v0, v1);
+                  else mod_pair_tab_t<false, false>(M, MW[j], z, MT[j], 0.0, v0, v1);
+                  if (of && fma(M.Dw, MW[j].x, M.D0) <= 0.0) v0 = 0.0;
+                  a[j] += v0;
+                  j++;
+                }
+              }
               if (tail && M.tail && spectra_kj(nphi) % 4 == 0)     // k_spectra's tail fours
                 for (; j + 3 < nphi; j += 4) {
                   dbl2 qa, qb; qa.x = QV[j]; qa.y = QV[j + 1]; qb.x = QV[j + 2]; qb.y = QV[j + 3];

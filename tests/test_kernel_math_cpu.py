@@ -16,10 +16,12 @@ def test_factorised_math_matches_oracle(dim, mode):
     s = synth.as_read(synth.surface(150, seed=11, dimension=dim, full3d=(dim == 3)))
     spec = make_spec(hrg_eos=2, chosen="pikp", df_mode=mode, dimension=dim, pT="pT24", phi="phi24")
     ref = O.spectra(spec, s, threads=1)
-    got, _ = emu_spectra(spec, s, chains=1)
-    rel, zr, zg = parity(got, ref)
-    assert rel < 1e-9, rel
-    assert zr == zg
+    # variant 0: per-lane linear forms (k_dndx's form); 4: k_spectra's table form of the modified path
+    for variant in ((0, 4) if mode >= 3 else (0,)):
+        got, _ = emu_spectra(spec, s, chains=1, variant=variant)
+        rel, zr, zg = parity(got, ref)
+        assert rel < 1e-9, (variant, rel)
+        assert zr == zg
 
 
 @pytest.mark.parametrize("mode", [1, 2, 3])
