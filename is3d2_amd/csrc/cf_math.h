@@ -1212,6 +1212,22 @@ IS3D_HD int spectra_kj(int nphi) {
   return best;
 }
 
+// spectra_kj with lane fill: k_spectra runs lanes x ceil(nphi / KJ) tasks per pT in 256-lane workgroups,
+// so for few (species x q) lanes (pikp 2+1D: 3 x 24 = 72) a 24-point block leaves 72% of a workgroup
+// idle and a smaller block fills it: cost = lane slots actually launched x (KJ + the 4.5-point setup)
+IS3D_HD int spectra_kj_fill(int nphi, long lanes) {
+  const int cand[4] = {32, 24, 8, 2};
+  int best = 32;
+  double best_cost = 1e300;
+  for (int kj : cand) {
+    const long nb = (nphi + kj - 1) / kj;
+    const long slots = (lanes * nb + 255) / 256 * 256;
+    const double cost = (double)slots * ((double)kj + 4.5);
+    if (cost < best_cost) { best = kj; best_cost = cost; }
+  }
+  return best;
+}
+
 // Fast separable lanes take their phi points four per reciprocal (sep_quad_t) when the phi block is a
 // multiple of 4, pairs otherwise (MI355X A/B: RTA-CE +5.5%, profiles/round1_r1q_ab_quad.log; Grad +1.2%
 // without prefetch while it spilled, round1_r1t_ab_gq.log, +1.2% more with it once spill-free, round1_r1w_ab_gpf.log)

@@ -201,6 +201,39 @@ __global__ __launch_bounds__(256) void k_reduce(ReduceArgs A) {
   A.out[(((long)so * A.npT + ipt) * A.nphi + j) * A.ny_out + k] = A.prefactor * A.degen_orig[so] * acc;
 }
 
+// The same sum with one wavefront per output entry, for slabs with many (eta node, cell split) terms per
+// output (2+1D: 24 eta nodes x hundreds of splits -- the per-thread loop above ran 8k dependent loads per
+// output and took 2.4 ms for pikp 1e5 cells): lane i adds terms i, i + 64, ... of the (l, split) list,
+// then a fixed xor-shuffle tree combines the lanes, so the order stays fixed (bit-reproducible).
+__global__ __launch_bounds__(256) void k_reduce_wave(ReduceArgs A) {
+  const long o = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  const long nout = (long)A.npart * A.npT * A.nphi * A.ny_out;
+  if (o >= nout) return;                                   // whole wavefronts exit together
+  const int k = (int)(o % A.ny_out);
+  const long r1 = o / A.ny_out;
+  const int j = (int)(r1 % A.nphi);
+  const long r2 = r1 / A.nphi;
+  const int ipt = (int)(r2 % A.npT), s = (int)(r2 / A.npT);
+  const int KJ = A.kj, jb = j / KJ, jj = j % KJ;
+  const long nq = (long)A.nk * A.nl;
+  const long task0 = s + (long)A.npart * (k * A.nl + nq * jb);
+  const long nterm = (long)A.nl * A.nsplit;
+  double acc = 0.0;
+  for (long m = lane; m < nterm; m += 64) {
+    const int l = (int)(m / A.nsplit), z = (int)(m % A.nsplit);
+    const long tl = task0 + (long)l * A.npart;
+    const long el = ((long)ipt * A.nbx + tl / kBlock) * ((long)KJ * kBlock) + (long)jj * kBlock + tl % kBlock;
+    acc += A.slab[(long)z * A.sstride + el];
+  }
+#pragma unroll
+  for (int w = 32; w >= 1; w >>= 1) acc += __shfl_xor(acc, w, 64);
+  if (lane == 0) {
+    const int so = A.sorig[s];
+    A.out[(((long)so * A.npT + ipt) * A.nphi + j) * A.ny_out + k] = A.prefactor * A.degen_orig[so] * acc;
+  }
+}
+
 // per-cell spacetime bin indices (SpacetimeDistribution.cpp:380-392): keys[0..2][c] = itau, ir, iphi (-1 outside)
 struct KeyArgs {
   const double *tau, *x, *y; long n;
@@ -615,6 +648,12 @@ static int device_jonah_table(is3d_engine* e, const double* r2, const double* w2
   return IS3D_OK;
 }
 
+// phi points per k_spectra lane for this engine's species / rapidity grid (spectra_kj_fill)
+static int engine_kj(const is3d_engine* e) {
+  const long nq = (e->p.dimension == 3) ? (long)e->y.size() : (long)e->eta.size();
+  return spectra_kj_fill((int)e->phi.size(), (long)e->mass.size() * nq);
+}
+
 static int finalize_tables(is3d_engine* e) {
   if (!e->have_params) return e->fail(IS3D_ERR_STATE, "is3d_set_params not called");
   if (!e->have_species) return e->fail(IS3D_ERR_STATE, "is3d_set_species not called");
@@ -695,7 +734,7 @@ static int finalize_tables(is3d_engine* e) {
   // {pT cos phi, pT sin phi} per (pT, padded phi slot) for k_spectra's scalar loads (same products as
   // its LDS copy s_cs); 16-byte aligned
   if (cb.size() & 1) cb.push_back(0.0);
-  const int kj_cs = spectra_kj((int)e->phi.size());
+  const int kj_cs = engine_kj(e);
   const int nphp_cs = (int)((e->phi.size() + kj_cs - 1) / kj_cs) * kj_cs;
   std::vector<double> csv((size_t)e->pT.size() * nphp_cs * 2, 0.0);
   for (size_t i = 0; i < e->pT.size(); i++)
@@ -861,7 +900,7 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   }
   HIPCHK(e, hipEventRecord(e->ev[1], st));
   // --- main integral
-  const int KJ = spectra_kj(nphi);
+  const int KJ = engine_kj(e);
   const int njb = (nphi + KJ - 1) / KJ;
   const long ntask = (long)np * nk * nl * njb;
   const long bx = (ntask + kBlock - 1) / kBlock;
@@ -926,7 +965,12 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   ra.ntask = ntask;
   ra.sorig = e->d_sorig; ra.degen_orig = e->d_degen_orig; ra.prefactor = std::pow(2.0 * M_PI * kHbarC, -3);
   ra.out = dev_out;
-  hipLaunchKernelGGL(k_reduce, dim3((unsigned)((sstride + 255) / 256)), dim3(256), 0, st, ra);
+  if ((long)nl * nsplit >= 128) {
+    const long nout = (long)np * npT * nphi * ny_out;
+    hipLaunchKernelGGL(k_reduce_wave, dim3((unsigned)((nout + 3) / 4)), dim3(256), 0, st, ra);
+  } else {
+    hipLaunchKernelGGL(k_reduce, dim3((unsigned)((sstride + 255) / 256)), dim3(256), 0, st, ra);
+  }
   HIPCHK(e, hipGetLastError());
   HIPCHK(e, hipEventRecord(e->ev[3], st));
   e->launched = true;
