@@ -95,12 +95,12 @@ def cpu_baseline(spec, surf, units_per_cell, n_full, target_s=25.0, operation=1)
         else:
             O.spectra(spec, sample, T_avg=T_avg, threads=threads, omp_threads=threads)
 
-    n_probe = min(len(surf["tau"]), max(2 * threads, 32))
+    n_probe = min(len(surf["tau"]), max(8 * threads, 64))      # ~4 s: thread start-up stays negligible
     probe = {k: v[:n_probe] for k, v in surf.items()}
     t = time.perf_counter()
     run(probe)
     dt = time.perf_counter() - t
-    n = int(min(len(surf["tau"]), max(n_probe, 1.15 * n_probe * target_s / max(dt, 1e-3))))
+    n = int(min(len(surf["tau"]), max(n_probe, n_probe * target_s / max(dt, 1e-3))))
     n = max(threads, (n // threads) * threads)
     sample = {k: v[:n] for k, v in surf.items()}
     t = time.perf_counter()
@@ -117,7 +117,9 @@ def cpu_baseline(spec, surf, units_per_cell, n_full, target_s=25.0, operation=1)
                        % (n, dt, threads),
                 sample_cells=n, sample_s=dt, extrapolated_s=dt * n_full / n, extrapolated_cells=n_full,
                 nproc=nproc, affinity_cpus=affinity, cgroup_cpu_quota=quota, cpu_model=model,
-                compiler="gcc " + flags)
+                compiler="gcc " + flags,
+                note="cores = OMP_NUM_THREADS when set: the GPU pool gives a one-GPU box a 16-CPU share "
+                     "(cgroup_cpu_quota) of a host whose nproc counts every CPU")
 
 
 def executed_roofline(args, mode, ms_spectra, ms_total, neta, units_local, n_local, outsize, kernel):
@@ -130,7 +132,8 @@ def executed_roofline(args, mode, ms_spectra, ms_total, neta, units_local, n_loc
     The reference-loop operation count of SURVEY.md 8d (F flops per node) is reported separately as
     reference_equivalent_tflops: the factorised kernel executes ~1/4 of those operations, so that rate
     is not a fraction of any peak."""
-    key = "%s_mode%d" % (args.config, mode) if args.operation == 1 else "%s_op0_mode%d" % (args.config, mode)
+    cfg = args.config + ("_cells%d" % args.cells if getattr(args, "cells", 0) else "")
+    key = "%s_mode%d" % (cfg, mode) if args.operation == 1 else "%s_op0_mode%d" % (cfg, mode)
     pmc = {}
     for name in ("pmc_traffic", "pmc_valu"):
         path = os.path.join(ROOT, "profiles", name + ".json")
@@ -233,7 +236,7 @@ def run_workload(args, cfg_name, mode, steps, warmup, rank, world, local_rank, d
     ms_spectra = float(np.mean([s["ms_spectra"] for s in kstats]))
     ms_total = float(np.mean([s["ms_total"] for s in kstats]))
     kernel = "k_spectra" if operation == 1 else "k_dndx"
-    sub = argparse.Namespace(config=cfg_name, operation=operation)
+    sub = argparse.Namespace(config=cfg_name, operation=operation, cells=args.cells if cfg_name == args.config else 0)
     roofline = executed_roofline(sub, mode, ms_spectra, ms_total, neta, units_local, n_local, outsize, kernel)
     config = {
         "workload": "%s%s: %s %s synthetic freeze-out cells%s x %s HRG (%d species) x %s delta-f, %d pT x %d phi x %d y%s"

@@ -15,6 +15,9 @@
 //                 per-(cell,y/eta) factors are built cooperatively in LDS (see
 //                 cf_math.h for the factorisation); no atomics, fixed summation order
 //   k_reduce      sum of the cell-split partial slabs x (2 pi hbarc)^-3 x g
+#ifndef IS3D_MAX_SPLITS
+#define IS3D_MAX_SPLITS 64    // cap on k_spectra's cell splits (one output-sized slab each)
+#endif
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -907,11 +910,11 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   const long wgs = bx * npT;
   // cell splits: enough workgroups to fill the chip (>= 8k), and each split's records small enough
   // (~2 MB) to stay in one XCD's 4 MB L2 while that XCD's workgroups stream them; a multiple of 8
-  // so every XCD owns whole splits; at most 64 slabs
+  // so every XCD owns whole splits; at most IS3D_MAX_SPLITS slabs (each one output-sized)
   const long max_split = (n + kTile - 1) / kTile;
   const long by_fill = (8192 + wgs - 1) / wgs;
   const long by_l2 = ((long)NREC * 8 * n + IS3D_SPLIT_BYTES - 1) / IS3D_SPLIT_BYTES;
-  long nsplit = std::max(by_fill, std::min(by_l2, 64L));
+  long nsplit = std::max(by_fill, std::min(by_l2, (long)IS3D_MAX_SPLITS));
   if (nsplit >= 8) nsplit = (nsplit + 7) / 8 * 8;
   nsplit = std::max(1L, std::min(nsplit, max_split));
   long cps = (n + nsplit - 1) / nsplit;
@@ -965,7 +968,8 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   ra.ntask = ntask;
   ra.sorig = e->d_sorig; ra.degen_orig = e->d_degen_orig; ra.prefactor = std::pow(2.0 * M_PI * kHbarC, -3);
   ra.out = dev_out;
-  if ((long)nl * nsplit >= 128) {
+  // one wavefront per output when each output sums many (eta node, split) terms and there are few outputs
+  if ((long)nl * nsplit >= 128 && sstride / nl < (1L << 20)) {
     const long nout = (long)np * npT * nphi * ny_out;
     hipLaunchKernelGGL(k_reduce_wave, dim3((unsigned)((nout + 3) / 4)), dim3(256), 0, st, ra);
   } else {

@@ -13,7 +13,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd /tmp && export TMPDIR=/tmp
 PY=$(command -v python3)
 for M in $MODES; do
-  OUT=$R/gpurun_out/prof_${TAG}_m$M
+  OUT=$R/gpurun_out/prof_${TAG}_${CFG}_m$M
   mkdir -p "$OUT"
   B="$R/bench.py --no-cpu-baseline --north-star-steps 0 --config $CFG --df-mode $M --steps 2 --warmup 1 $*"
   timeout -s KILL 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- "$PY" $B > "$OUT/trace.log" 2>&1

@@ -91,9 +91,15 @@ def main():
             if "SQ_INSTS_VALU_" + c in e:
                 v[key][c.lower() + "_insts_per_launch"] = e["SQ_INSTS_VALU_" + c]
         if "SQ_INSTS_VALU_FLOPS_FP64" in e:
-            v[key]["fp64_flops_per_launch"] = e["SQ_INSTS_VALU_FLOPS_FP64"]
+            # the counter adds FMA x 2 + ADD + MUL + TRANS per WAVE-instruction (it equals that sum of the
+            # per-type counters); x 64 lanes = flops (rocprofv3's derived FLOP metrics scale it the same way)
+            v[key]["fp64_flops_per_launch"] = 64.0 * e["SQ_INSTS_VALU_FLOPS_FP64"]
         if "SQ_LDS_BANK_CONFLICT" in e:
             v[key]["lds_bank_conflict_cycles"] = e["SQ_LDS_BANK_CONFLICT"]
+        if "SQ_LDS_IDX_ACTIVE" in e and "clock_ghz" in e:
+            # LDS-array cycles summed over the 256 CUs / (256 x kernel cycles)
+            v[key]["lds_busy_frac"] = e["SQ_LDS_IDX_ACTIVE"] / (256.0 * e["avg_ns_pmc_pass"] * e["clock_ghz"])
+        v[key]["kernel_ns_pmc_pass"] = e["avg_ns_pmc_pass"]
         json.dump(v, open(vp, "w"), indent=1, sort_keys=True)
     for k, e in sorted(out.items()):
         print(k, {c: round(v, 3) for c, v in e.items()})
