@@ -1415,13 +1415,14 @@ IS3D_HD void sep_quad_tb_tail_t(const SepLane& L, double mT, const dbl2* b, cons
   for (int i = 0; i < 4; i++) {
     double pb = fma(L.D0, b[i].x, L.escw * pt[i].x);
     if (OUT) pb = (pb <= 0.0) ? 0.0 : pb;
-    const double S = fma(mT, pt[i].y, b[i].y) + L.S0;
+    const double P = fma(mT, pt[i].y, b[i].y);
     double t;
     if (REG) {
+      const double S = P + L.S0;
       const double dfv = needE ? fma(S, rE[i], L.L0 + pe[i].y) : S;
       t = 1.0 + fmax(-1.0, fmin(dfv, 1.0));
-    } else {
-      t = needE ? fma(S, rE[i], (1.0 + L.L0) + pe[i].y) : S + 1.0;
+    } else {   // 1 + S0 and 1 + L0 are lane constants (hoisted by the compiler)
+      t = needE ? fma(P + L.S0, rE[i], (1.0 + L.L0) + pe[i].y) : P + (1.0 + L.S0);
     }
     acc[i] = fma(pb, t, acc[i]);
   }
@@ -1675,6 +1676,20 @@ IS3D_HD void mod_pair_tab_t(const ModLane& L, dbl2 mw0, dbl2 mw1, double mt0, do
   const double q0 = fma(L.sign, en0, 1.0), q1 = fma(L.sign, en1, 1.0);
   const double r = rcp1(q0 * q1);
   const double pds0 = fma(L.Dw, mw0.x, L.D0), pds1 = fma(L.Dw, mw1.x, L.D0);
+  const double g0 = pds0 * (en0 * (r * q1)), g1 = pds1 * (en1 * (r * q0));
+  v0 = (OUT && pds0 <= 0.0) ? 0.0 : g0;
+  v1 = (OUT && pds1 <= 0.0) ? 0.0 : g1;
+}
+
+// two points of a modified lane from its linear forms and Qv (no q-row table): as mod_pair_t with the
+// exp argument of mod_en_x
+template <bool OUT, bool CLAMP>
+IS3D_HD void mod_pair_lane_t(const ModLane& L, dbl2 c0, dbl2 c1, double qv0, double qv1, double& v0, double& v1) {
+  const double en0 = mod_en_x<CLAMP>(L, fma(L.Ec, c0.x, fma(L.Es, c0.y, L.E0 + qv0)));
+  const double en1 = mod_en_x<CLAMP>(L, fma(L.Ec, c1.x, fma(L.Es, c1.y, L.E0 + qv1)));
+  const double q0 = fma(L.sign, en0, 1.0), q1 = fma(L.sign, en1, 1.0);
+  const double r = rcp1(q0 * q1);
+  const double pds0 = lin(L.D0, L.Dc, L.Ds, c0), pds1 = lin(L.D0, L.Dc, L.Ds, c1);
   const double g0 = pds0 * (en0 * (r * q1)), g1 = pds1 * (en1 * (r * q0));
   v0 = (OUT && pds0 <= 0.0) ? 0.0 : g0;
   v1 = (OUT && pds1 <= 0.0) ? 0.0 : g1;

@@ -15,6 +15,9 @@
 //                 per-(cell,y/eta) factors are built cooperatively in LDS (see
 //                 cf_math.h for the factorisation); no atomics, fixed summation order
 //   k_reduce      sum of the cell-split partial slabs x (2 pi hbarc)^-3 x g
+#ifndef IS3D_LDS_QROW_LIMIT
+#define IS3D_LDS_QROW_LIMIT (80 * 1024)   // above this k_spectra takes the F_LY launch (per-lane y-term rows)
+#endif
 #ifndef IS3D_MAX_SPLITS
 #define IS3D_MAX_SPLITS 64    // cap on k_spectra's cell splits (one output-sized slab each)
 #endif
@@ -651,10 +654,57 @@ static int device_jonah_table(is3d_engine* e, const double* r2, const double* w2
   return IS3D_OK;
 }
 
-// phi points per k_spectra lane for this engine's species / rapidity grid (spectra_kj_fill)
-static int engine_kj(const is3d_engine* e) {
-  const long nq = (e->p.dimension == 3) ? (long)e->y.size() : (long)e->eta.size();
-  return spectra_kj_fill((int)e->phi.size(), (long)e->mass.size() * nq);
+// k_spectra launch shape for this engine's species / grids (shared by the launch and by the {pT cos,
+// pT sin} table finalize_tables builds for KJ-padded phi rows)
+struct SpectraPlan {
+  int KJ, njb, nq, nqmax, tb, ly;
+  size_t shmem;
+};
+static SpectraPlan spectra_plan(const is3d_engine* e) {
+  SpectraPlan P{};
+  const int mode = e->p.df_mode, dim = e->p.dimension;
+  const int np = (int)e->mass.size(), nphi = (int)e->phi.size();
+  const int nk = (dim == 3) ? (int)e->y.size() : 1, nl = (dim == 3) ? 1 : (int)e->eta.size();
+  P.nq = nk * nl;
+  auto shape = [&](int KJ) {
+    P.KJ = KJ;
+    P.njb = (nphi + KJ - 1) / KJ;
+    // rows (r = q + nq jb) one workgroup's 256 consecutive tasks can span: a contiguous range of at most
+    // (kBlock - 1) / np + 2 of the nq njb rows
+    P.nqmax = (int)std::min<long>((long)P.nq * P.njb, (kBlock - 1) / np + 2);
+    // Grad {PD, T1} table (F_TB, sep_quad_tb_t): exact only without baryon terms (R_SCB = R_SSB = 0:
+    // V^mu and alphaB are only packed when include_baryon && include_baryondiff_deltaf (prep_grad_ce), and
+    // df_eval leaves c1 = c3 = 0 without baryons); needs phi blocks of fours and at most kTbQ rows per
+    // workgroup
+    P.tb = (IS3D_GRAD_TB && (mode == GRAD || (mode == CE && IS3D_CE_TB)) && !e->p.include_baryon &&
+            KJ % 4 == 0 && P.nqmax <= kTbQ) ? F_TB : 0;
+  };
+  auto lds_bytes = [&](int qrows) {     // qrows = 0: F_LY layout (one y-term row per lane)
+    const size_t nphp = (size_t)P.njb * P.KJ;
+    return sizeof(double) * (2 * (size_t)kTile * NREC + 2 * (size_t)(kTile + 2) * nphp +
+                             2 * (size_t)kTile * nphp + (size_t)(nk + 2 * nl) +
+                             (qrows ? (size_t)kTile * std::min(qrows, P.nq) : (size_t)kBlock) * kYRow + kExpTabN +
+                             (P.tb ? 2 * (size_t)kTile * qrows * (P.KJ + 1) + 1 : 0) +
+                             (P.tb && mode == CE ? 2 * (size_t)kTile * nphp : 0) +
+                             (mode >= PTM && qrows ? (size_t)kTile * qrows * (P.KJ + 1) + 1 : 0));
+  };
+#ifdef IS3D_FORCE_KJ
+  shape(IS3D_FORCE_KJ);
+#else
+  shape(spectra_kj_fill(nphi, (long)np * P.nq));
+#endif
+  P.ly = 0;
+  P.shmem = lds_bytes(P.nqmax);
+  // grids whose q rows do not fit (large y / eta tables with few species; np >= 86 keeps nqmax <= 4) run
+  // the F_LY launch (KJ = 8, per-lane y-term rows, no q-row tables) instead of failing: the reference has
+  // no grid limit
+  if (P.shmem > IS3D_LDS_QROW_LIMIT && !P.tb) {
+    shape(8);
+    P.tb = 0;
+    P.ly = F_LY;
+    P.shmem = lds_bytes(0);
+  }
+  return P;
 }
 
 static int finalize_tables(is3d_engine* e) {
@@ -737,7 +787,7 @@ static int finalize_tables(is3d_engine* e) {
   // {pT cos phi, pT sin phi} per (pT, padded phi slot) for k_spectra's scalar loads (same products as
   // its LDS copy s_cs); 16-byte aligned
   if (cb.size() & 1) cb.push_back(0.0);
-  const int kj_cs = engine_kj(e);
+  const int kj_cs = spectra_plan(e).KJ;
   const int nphp_cs = (int)((e->phi.size() + kj_cs - 1) / kj_cs) * kj_cs;
   std::vector<double> csv((size_t)e->pT.size() * nphp_cs * 2, 0.0);
   for (size_t i = 0; i < e->pT.size(); i++)
@@ -903,8 +953,9 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   }
   HIPCHK(e, hipEventRecord(e->ev[1], st));
   // --- main integral
-  const int KJ = engine_kj(e);
-  const int njb = (nphi + KJ - 1) / KJ;
+  const SpectraPlan P = spectra_plan(e);
+  const int KJ = P.KJ, njb = P.njb;
+  if (P.shmem > 160 * 1024) return e->fail(IS3D_ERR_ARG, "momentum grid too large for the LDS tile (phi table)");
   const long ntask = (long)np * nk * nl * njb;
   const long bx = (ntask + kBlock - 1) / kBlock;
   const long wgs = bx * npT;
@@ -928,29 +979,11 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   sa.csg = e->d_csg;
   sa.pT = e->d_pT; sa.cphi = e->d_cphi; sa.sphi = e->d_sphi; sa.yv = e->d_y; sa.etav = e->d_eta; sa.etaw = e->d_etaw;
   sa.npart = np; sa.npT = npT; sa.nphi = nphi; sa.ny_out = ny_out; sa.nk = nk; sa.nl = nl; sa.nq = nk * nl; sa.njb = njb;
+  sa.nqmax = P.nqmax;
   sa.ntask = ntask; sa.cells_per_split = cps; sa.nbx = (int)bx; sa.nsplit = (int)nsplit; sa.sstride = sstride;
   sa.regulate = e->p.regulate_deltaf; sa.outflow = e->p.outflow; sa.dim = dim; sa.op = 1;
-  // Grad {PD, T1} table (F_TB, sep_quad_tb_t): exact only without baryon terms (R_SCB = R_SSB = 0);
-  // needs one phi block of fours, and the 256 tasks of a workgroup span at most
-  // (kBlock - 1) / np + 2 <= kTbQ q values
-  // (that span bound holds only when k_spectra builds the y-terms of its lanes' q range, IS3D_YQ_RANGE;
-  // otherwise a workgroup touches all nq rows and the kTbQ-row LDS regions would overflow).
-  // include_baryon = 0 is what makes R_SCB = R_SSB = 0: V^mu and alphaB are only packed when
-  // include_baryon && include_baryondiff_deltaf (prep_grad_ce), and df_eval leaves c1 = c3 = 0 without baryons
-  // q rows one workgroup's 256 consecutive tasks can span: with one phi block they are a contiguous q range
-  // of at most (kBlock - 1) / np + 2 values (IS3D_YQ_RANGE), otherwise every q
-  const int nqmax = (IS3D_YQ_RANGE && njb == 1) ? (int)std::min<long>(sa.nq, (kBlock - 1) / np + 2) : sa.nq;
-  sa.nqmax = nqmax;
-  const int tb = (IS3D_GRAD_TB && IS3D_YQ_RANGE && (mode == GRAD || (mode == CE && IS3D_CE_TB)) && !e->p.include_baryon &&
-                  njb == 1 && KJ % 4 == 0 && nqmax <= kTbQ) ? F_TB : 0;
-  const size_t nphp = (size_t)njb * KJ;
-  const size_t shmem = sizeof(double) * (2 * (size_t)kTile * NREC + 2 * (size_t)(kTile + 2) * nphp +
-                                         2 * (size_t)kTile * nphp + (size_t)(nk + 2 * nl) +
-                                         (size_t)kTile * nqmax * kYRow + kExpTabN +
-                                         (tb ? 2 * (size_t)kTile * nqmax * nphp + 1 : 0) +
-                                         (tb && mode == CE ? 2 * (size_t)kTile * nphp : 0) +
-                                         (mode >= PTM ? (size_t)kTile * nqmax * nphp + 1 : 0));
-  if (shmem > 160 * 1024) return e->fail(IS3D_ERR_ARG, "momentum grid too large for the LDS tile");
+  const size_t shmem = P.shmem;
+  const int tb = P.tb | P.ly;
   const dim3 grid((unsigned)(bx * npT * nsplit));
   const int kflags = (e->p.regulate_deltaf ? F_REG : 0) | (e->p.outflow ? F_OUT : 0) | tb;
   switch (mode) {

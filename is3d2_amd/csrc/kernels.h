@@ -32,6 +32,11 @@ template <int MODE>
 constexpr int spectra_waves() {
   return MODE >= PTM ? IS3D_SPECTRA_WAVES_MOD : MODE == CE ? IS3D_SPECTRA_WAVES_CE : IS3D_SPECTRA_WAVES_SEP;
 }
+#ifndef IS3D_SPECTRA_WAVES_KJ16
+#define IS3D_SPECTRA_WAVES_KJ16 4     // Grad with 16-point phi blocks (acc in 32 VGPRs)
+#endif
+template <int MODE, int KJ>
+constexpr int spectra_waves_kj() { return (KJ == 16 && MODE == GRAD) ? IS3D_SPECTRA_WAVES_KJ16 : spectra_waves<MODE>(); }
 // k_dndx keeps RTA-CE at 2 (its pT loop holds more live state: 215 VGPRs)
 template <int MODE>
 constexpr int dndx_waves() { return MODE == CE ? 2 : spectra_waves<MODE>(); }
@@ -64,7 +69,9 @@ struct SpecArgs {
 // flag bits of the spectra kernel instantiation
 // F_TB (Grad / RTA-CE, include_baryon = 0, one phi block, KJ % 4 == 0): linear delta-f part from the
 // (cell, q, phi) {PD, T1} table (sep_quad_tb_t); a workgroup then uses at most kTbQ q values
-constexpr int F_REG = 1, F_OUT = 2, F_TB = 4;
+// F_LY (grids whose q rows do not fit in LDS: large y / eta tables with few species, KJ = 8 only): every
+// lane builds its own y-term row in LDS and the modified lanes use their linear forms, no q-row tables
+constexpr int F_REG = 1, F_OUT = 2, F_TB = 4, F_LY = 8;
 constexpr int kTbQ = 4;
 
 #ifndef IS3D_SPLIT_BYTES
@@ -93,9 +100,6 @@ constexpr int kTbQ = 4;
 #endif
 #ifndef IS3D_CE_TB
 #define IS3D_CE_TB 1          // RTA-CE without baryon also takes the F_TB launch ({PD, T1} + {TE, T2} tables)
-#endif
-#ifndef IS3D_YQ_RANGE
-#define IS3D_YQ_RANGE 1       // k_spectra builds the y-terms of its lanes' q range only
 #endif
 #ifndef IS3D_TAIL
 #define IS3D_TAIL 1           // Boltzmann-tail lanes skip the per-point reciprocal (kTailX): Grad F_TB 497 -> 481 ms (r2d)
@@ -352,6 +356,19 @@ __device__ __forceinline__ void mod_phi_loop_tab(const ModLane& M, const dbl2* M
   }
 }
 
+// modified lanes without q-row tables (lane_y launches): {pc, ps} and the {PDm, Qv} rows, the lane's
+// linear forms for E_mod^2 and p.dsigma (mod_quad_lane_t), pairs of points per reciprocal
+template <int FLAGS, bool CLAMP, int KJ>
+__device__ __forceinline__ void mod_phi_loop_lane(const ModLane& M, const dbl2* CS, const dbl2* MW, double* acc) {
+  constexpr bool OUT = (FLAGS & F_OUT) != 0;
+#pragma unroll
+  for (int jj = 0; jj < KJ; jj += 2) {
+    double v0, v1;
+    mod_pair_lane_t<OUT, CLAMP>(M, CS[jj], CS[jj + 1], MW[jj].y, MW[jj + 1].y, v0, v1);
+    acc[jj] += v0; acc[jj + 1] += v1;
+  }
+}
+
 template <int FLAGS, bool CLAMP, int KJ>
 __device__ __forceinline__ void mod_phi_loop(const ModLane& M, const dbl2* CS, const dbl2* QV, double* acc) {
   constexpr bool OUT = (FLAGS & F_OUT) != 0;
@@ -422,7 +439,7 @@ __device__ __forceinline__ void wait_fetch() { asm volatile("s_waitcnt vmcnt(0)"
 // (species, q, phi block) with q = (y, eta node): in 2+1D the eta nodes are spread over lanes and
 // summed by k_reduce, so a few species still fill the wavefronts
 template <int MODE, int FLAGS, int KJ>
-__global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_spectra(SpecArgs A) {
+__global__ __launch_bounds__(kBlock, (spectra_waves_kj<MODE, KJ>())) void k_spectra(SpecArgs A) {
   extern __shared__ double smem[];
   const int nphp = A.njb * KJ;                            // phi rows padded to KJ multiples
   double* s_recb = smem;                                  // [2][kTile][NREC] double-buffered
@@ -433,17 +450,22 @@ __global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_spectra(SpecA
   double* s_qv = (double*)(s_bp + kTile * nphp);
   dbl2* s_mw = (dbl2*)s_qv;
   double* s_grid = s_qv + 2 * kTile * nphp;               // y[nk] | eta[nl] | eta_w[nl]
-  const int nqm = A.nqmax;                                // q rows per cell (>= every workgroup's nqw)
-  double* s_y = s_grid + A.nk + 2 * A.nl;                 // [kTile][nqm][kYRow]
+  const int nqm = A.nqmax;                                // rows per cell (>= every workgroup's nqw)
+  double* s_y = s_grid + A.nk + 2 * A.nl;                 // [kTile][min(nqm, nq)][kYRow]
   constexpr bool TB = (MODE == GRAD || MODE == CE) && (FLAGS & F_TB) != 0 && KJ % 4 == 0;
-  // the q-row tables hold nqm <= nq rows: only the lanes' own q range (IS3D_YQ_RANGE) bounds nqw below nq
-  static_assert(!TB || IS3D_YQ_RANGE, "the F_TB launch needs IS3D_YQ_RANGE");
-  double* s_etab = s_y + (long)kTile * nqm * kYRow;       // [kExpTabN] exp_tab's 2^(j/kExpTabN)
-  // TB: [kTile][nqm][nphp] {PD, T1}, 16-byte aligned for ds_read_b128 (s_grid's nk + 2 nl doubles
+  constexpr bool LY = (FLAGS & F_LY) != 0;
+  // LY launches: s_y holds one y-term row per lane instead ([kBlock][kYRow]; odd row stride: no conflicts)
+  // y-term rows per cell: per row, or per q once the rows cover every q (nyr below): min(nqm, nq)
+  double* s_etab = s_y + (LY ? (long)kBlock : (long)kTile * min(nqm, A.nq)) * kYRow;   // [kExpTabN] 2^(j/kExpTabN)
+  // TB: [kTile][nqm][prow] {PD, T1}, 16-byte aligned for ds_read_b128 (s_grid's nk + 2 nl doubles
   // can leave s_etab at an odd double; misaligned dbl2 reads ran the kernel 3.5x slower)
   dbl2* s_pt = (dbl2*)(smem + (((s_etab + kExpTabN) - smem + 1) & ~1L));
-  dbl2* s_pe = s_pt + kTile * nqm * nphp;                 // TB, RTA-CE: [kTile][nphp] {TE, T2}
-  double* s_mt = (double*)s_pt;                           // modified path: [kTile][nqm][nphp] T2 = 2 U_q . W
+  // row tables hold the KJ phi points of their row's phi block plus one padding entry, so two rows read
+  // at the same phi by the two halves of a wavefront that straddles a row boundary land in different
+  // banks (a 512-B row stride is 128 dwords: the same bank, a 2-way conflict in every straddling wave)
+  constexpr int prow = KJ + 1;
+  dbl2* s_pe = s_pt + kTile * nqm * prow;                 // TB, RTA-CE: [kTile][nphp] {TE, T2}
+  double* s_mt = (double*)s_pt;                           // modified path: [kTile][nqm][prow] T2 = 2 U_q . W
 
   const int tid = threadIdx.x;
   for (int i = tid; i < kExpTabN; i += kBlock) s_etab[i] = kExp2Tab[i];
@@ -467,14 +489,23 @@ __global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_spectra(SpecA
     jb = (int)(r / A.nq);
   }
   const int j0 = jb * KJ;
-  // q values this workgroup's lanes use: a contiguous range q0 .. q0 + nqw - 1 when its tasks lie in one
-  // phi block (the y-terms of the other q are not built), all nq otherwise
-  int q0 = 0, nqw = A.nq;
+  // rows r = task / npart = q + nq jb this workgroup's 256 consecutive tasks use: the contiguous range
+  // r0 .. r0 + nqw - 1, at most (kBlock - 1) / npart + 2 of them (the host's nqmax).  The y-terms and
+  // the q tables are built per row (row r holds the (cell, q) y-terms and its own phi block's points),
+  // so a workgroup never builds rows its lanes do not read, whatever the number of phi blocks
+  long r0 = 0;
+  int nqw = 1;
   {
     const long t0 = (long)lane_group * kBlock, t1 = min(A.ntask, t0 + kBlock) - 1;
-    const long r0 = t0 / A.npart, r1 = t1 / A.npart;
-    if (IS3D_YQ_RANGE && r0 / A.nq == r1 / A.nq) { q0 = (int)(r0 % A.nq); nqw = (int)(r1 - r0) + 1; }
+    r0 = t0 / A.npart;
+    nqw = (int)(t1 / A.npart - r0) + 1;
   }
+  const int row = active ? (int)(task / A.npart - r0) : 0;
+  // y-term rows: per row, or per q when the rows cover every q (several phi blocks, few species: the
+  // y-terms depend on q only)
+  const bool allq = nqw >= A.nq;
+  const int nyr = allq ? A.nq : nqw;
+  const int yrow = allq ? q : row;
   const double mass = A.smass[s], m2 = mass * mass, sign = A.ssign[s], baryon = A.sbaryon[s];
   const double mT = sqrt(m2 + pT * pT), mT2 = mT * mT, mTb = mT * baryon;
 
@@ -535,38 +566,41 @@ __global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_spectra(SpecA
         s_pe[t * nphp + j] = e;
       }
     }
-    for (int idx = tid; idx < nt * nqw; idx += kBlock) {
-      const int t = idx / nqw, qq = idx % nqw, q = q0 + qq;
+    for (int idx = tid; idx < (LY ? 0 : nt * nyr); idx += kBlock) {
+      const int t = idx / nyr, qq = idx % nyr, q = allq ? qq : (int)((r0 + qq) % A.nq);
       const double* R = s_rec + t * NREC;
       if (R[R_KIND] != 0.0) {
         const int kk = q / A.nl, l = q % A.nl;
         const double y = s_grid[kk];
         const double eta = (A.dim == 3) ? R[R_ETA] : s_grid[A.nk + l];
         const double w = s_grid[A.nk + A.nl + l];
-        yterms(MODE, A.op, R, y, eta, w, s_y + ((long)t * nqw + qq) * kYRow);
+        yterms(MODE, A.op, R, y, eta, w, s_y + ((long)t * nyr + qq) * kYRow);
       }
     }
     lds_barrier();
-    if constexpr (MODE >= PTM) {
+    if (MODE >= PTM && !LY) {
       // T2 = 2 U_q . W per (cell, q, phi) of the modified cells (mod_quad_tab_t)
-      for (int idx = tid; idx < nt * nqw * nphp; idx += kBlock) {
-        const int j = idx % nphp, r = idx / nphp, qq = r % nqw, t = r / nqw;
+      for (int idx = tid; idx < nt * nqw * KJ; idx += kBlock) {
+        const int jj = idx % KJ, r = idx / KJ, qq = r % nqw, t = r / nqw;
+        const int j = (int)((r0 + qq) / A.nq) * KJ + jj;
         const double* R = s_rec + t * NREC;
         if (R[R_KIND] != 2.0) continue;
-        s_mt[((long)t * nqw + qq) * nphp + j] = modt2(R, s_y + ((long)t * nqw + qq) * kYRow, s_cs[j]);
+        const int yr = allq ? (int)((r0 + qq) % A.nq) : qq;
+        s_mt[((long)t * nqw + qq) * prow + jj] = modt2(R, s_y + ((long)t * nyr + yr) * kYRow, s_cs[j]);
       }
       lds_barrier();
     }
     if constexpr (TB) {
       // {PD, T1 = SC1 pc + SS1 ps} per (cell, q, phi) (rows of skipped cells are never read)
-      for (int idx = tid; idx < nt * nqw * nphp; idx += kBlock) {
-        const int j = idx % nphp, r = idx / nphp, qq = r % nqw, t = r / nqw;
-        const double* Y = s_y + ((long)t * nqw + qq) * kYRow;
+      for (int idx = tid; idx < nt * nqw * KJ; idx += kBlock) {
+        const int jj = idx % KJ, r = idx / KJ, qq = r % nqw, t = r / nqw;
+        const int j = (int)((r0 + qq) / A.nq) * KJ + jj;
+        const double* Y = s_y + ((long)t * nyr + (allq ? (int)((r0 + qq) % A.nq) : qq)) * kYRow;
         const dbl2 c = s_cs[j];
         dbl2 v;
         v.x = s_qv[t * nphp + j];
         v.y = fma(Y[Y_SC1], c.x, Y[Y_SS1] * c.y);
-        s_pt[((long)t * nqw + qq) * nphp + j] = v;
+        s_pt[((long)t * nqw + qq) * prow + jj] = v;
       }
       lds_barrier();
     }
@@ -582,7 +616,13 @@ __global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_spectra(SpecA
           rn_abs = fabs(rn);
         }
         const dbl2* BP = s_bp + t * nphp + j0;
-        const double* Y = s_y + ((long)t * nqw + (q - q0)) * kYRow;
+        const double* Y = s_y + ((long)t * nyr + yrow) * kYRow;
+        if constexpr (LY) {        // this lane's own y-terms, in its LDS row
+          double* Yl = s_y + (long)tid * kYRow;
+          const int kk = q / A.nl, l = q % A.nl;
+          yterms(MODE, A.op, R, s_grid[kk], (A.dim == 3) ? R[R_ETA] : s_grid[A.nk + l], s_grid[A.nk + A.nl + l], Yl);
+          Y = Yl;
+        }
         const bool sep = (MODE <= CE) || kind == 1.0 || Y[Y_NARROW] != 0.0;
         if (sep) {
           SepLane L;
@@ -590,14 +630,14 @@ __global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_spectra(SpecA
                     TB && IS3D_TAIL && (MODE == GRAD || IS3D_TAIL_CE));
           if (L.skip) continue;
           if constexpr (TB) {
-            const dbl2* PT = s_pt + ((long)t * nqw + (q - q0)) * nphp;
+            const dbl2* PT = s_pt + ((long)t * nqw + row) * prow;
             if (IS3D_TAIL && L.tail) {
               if (MODE == GRAD && IS3D_TAIL_PD)
-                sep_phi_loop_pd_tail<FLAGS, KJ>(L, (cs_sptr)A.csg + 2L * ipt * nphp, BP, s_qv + t * nphp, acc);
+                sep_phi_loop_pd_tail<FLAGS, KJ>(L, (cs_sptr)A.csg + 2L * (ipt * nphp + j0), BP, s_qv + t * nphp + j0, acc);
               else
-                sep_phi_loop_tb_tail<MODE, FLAGS, KJ>(L, mT, BP, PT, s_pe + t * nphp, acc);
+                sep_phi_loop_tb_tail<MODE, FLAGS, KJ>(L, mT, BP, PT, s_pe + t * nphp + j0, acc);
             }
-            else if (L.fast) sep_phi_loop_tb<MODE, FLAGS, KJ>(L, mT, BP, PT, s_pe + t * nphp, acc);
+            else if (L.fast) sep_phi_loop_tb<MODE, FLAGS, KJ>(L, mT, BP, PT, s_pe + t * nphp + j0, acc);
             else sep_phi_loop<MODE, FLAGS, false, KJ>(L, s_cs + j0, BP, acc);
           } else if (IS3D_PD_TABLE && IS3D_CS_SCALAR && MODE <= CE && KJ % 4 == 0 && L.fast && A.njb == 1)
             // one phi block: every lane reads the same {pc, ps}, so they come by scalar loads into SGPRs
@@ -613,7 +653,12 @@ __global__ __launch_bounds__(kBlock, spectra_waves<MODE>()) void k_spectra(SpecA
           mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, s_etab, M);
           if (M.skip) continue;
           const dbl2* MW = s_mw + t * nphp + j0;
-          const double* MT = s_mt + ((long)t * nqw + (q - q0)) * nphp + j0;
+          if constexpr (LY) {        // no T2 rows: the lane's linear forms (mod_pair_lane_t)
+            if (M.clamp) mod_phi_loop_lane<FLAGS, true, KJ>(M, s_cs + j0, MW, acc);
+            else mod_phi_loop_lane<FLAGS, false, KJ>(M, s_cs + j0, MW, acc);
+            continue;
+          }
+          const double* MT = s_mt + ((long)t * nqw + row) * prow;
           if (M.clamp) mod_phi_loop_tab<FLAGS, true, KJ>(M, MW, MT, acc);
           else mod_phi_loop_tab<FLAGS, false, KJ>(M, MW, MT, acc);
         }
@@ -828,6 +873,17 @@ __global__ __launch_bounds__(kBlock, dndx_waves<MODE>()) void k_dndx(DndxArgs A)
 
 template <int MODE, int KJ>
 void launch_spectra_kj(dim3 grid, size_t shmem, hipStream_t st, const SpecArgs& a, int flags) {
+  if constexpr (KJ == 8) {
+    if (flags & F_LY) {
+      switch (flags & 3) {
+        case 0: hipLaunchKernelGGL((k_spectra<MODE, 8, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+        case 1: hipLaunchKernelGGL((k_spectra<MODE, 9, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+        case 2: hipLaunchKernelGGL((k_spectra<MODE, 10, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+        default: hipLaunchKernelGGL((k_spectra<MODE, 11, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+      }
+      return;
+    }
+  }
   if constexpr ((MODE == GRAD || MODE == CE) && KJ % 4 == 0) {
     if (flags & F_TB) {
       switch (flags & 3) {
@@ -850,6 +906,9 @@ void launch_spectra_kj(dim3 grid, size_t shmem, hipStream_t st, const SpecArgs& 
 template <int MODE>
 void launch_spectra(dim3 grid, size_t shmem, hipStream_t st, const SpecArgs& a, int flags, int kj) {
   switch (kj) {
+#ifdef IS3D_KJ16
+    case 16: launch_spectra_kj<MODE, 16>(grid, shmem, st, a, flags); break;
+#endif
     case 32: launch_spectra_kj<MODE, 32>(grid, shmem, st, a, flags); break;
     case 24: launch_spectra_kj<MODE, 24>(grid, shmem, st, a, flags); break;
     case 8: launch_spectra_kj<MODE, 8>(grid, shmem, st, a, flags); break;

@@ -112,3 +112,18 @@ def test_table_launch_q_rows(nsp, mode):
     mcids = hrg.chosen_mcids("smash")[:nsp]
     spec = make_spec(hrg_eos=2, chosen=mcids, df_mode=mode, dimension=3, pT="pT24", phi="phi32", y="y21")
     check(spec, s)
+
+
+@pytest.mark.parametrize("dim,mode", [(3, 1), (3, 2), (3, 3), (3, 5), (2, 1), (2, 4)])
+def test_large_rapidity_grids(dim, mode):
+    # y / eta tables whose per-workgroup q rows would not fit in LDS (few species: pikp's 256 lanes span
+    # ~87 q values): the F_LY launch (per-lane y-term rows, no q-row tables); round 1 rejected these
+    # grids ("momentum grid too large for the LDS tile"), the reference has no such limit
+    s = synth.as_read(synth.surface(24, seed=41, dimension=dim, full3d=(dim == 3)))
+    spec = make_spec(hrg_eos=2, chosen="pikp", df_mode=mode, dimension=dim, famod_chains=1)
+    if dim == 3:
+        spec["y"] = np.linspace(-6.0, 6.0, 161)
+    else:
+        x, w = np.polynomial.legendre.leggauss(151)
+        spec["eta"], spec["eta_w"] = 4.0 * x, 4.0 * w
+    check(spec, s)
