@@ -18,6 +18,9 @@
 #ifndef IS3D_LDS_QROW_LIMIT
 #define IS3D_LDS_QROW_LIMIT (80 * 1024)   // above this k_spectra takes the F_LY launch (per-lane y-term rows)
 #endif
+#ifndef IS3D_ANISO_MERGE
+#define IS3D_ANISO_MERGE 1    // PTMA Newton sums over hadrons merged by identical (mass, sign)
+#endif
 #ifndef IS3D_MAX_SPLITS
 #define IS3D_MAX_SPLITS 64    // cap on k_spectra's cell splits (one output-sized slab each)
 #endif
@@ -457,6 +460,8 @@ struct is3d_engine {
   const double *d_pTw = nullptr, *d_phiw = nullptr;
   const double *d_gla = nullptr;
   const double *d_pdg = nullptr;
+  const double* d_aniso_h = nullptr;   // [3][n_aniso_h] merged (mass, sign, degeneracy) of the PTMA hadrons
+  int n_aniso_h = 0;
   int* d_sorig = nullptr;
   double* d_surf = nullptr; bool surf_owned = false; long ncell = 0; long surf_cap = 0;
   double *d_rec = nullptr, *d_aux = nullptr, *d_sol = nullptr, *d_renorm = nullptr, *d_slab = nullptr, *d_out = nullptr;
@@ -657,7 +662,7 @@ static int device_jonah_table(is3d_engine* e, const double* r2, const double* w2
 // k_spectra launch shape for this engine's species / grids (shared by the launch and by the {pT cos,
 // pT sin} table finalize_tables builds for KJ-padded phi rows)
 struct SpectraPlan {
-  int KJ, njb, nq, nqmax, tb, ly;
+  int KJ, njb, nq, nqmax, tb, ly, t8, tile;
   size_t shmem;
 };
 static SpectraPlan spectra_plan(const is3d_engine* e) {
@@ -679,6 +684,7 @@ static SpectraPlan spectra_plan(const is3d_engine* e) {
     P.tb = (IS3D_GRAD_TB && (mode == GRAD || (mode == CE && IS3D_CE_TB)) && !e->p.include_baryon &&
             KJ % 4 == 0 && P.nqmax <= kTbQ) ? F_TB : 0;
   };
+  int kTile = (mode >= PTM) ? IS3D_KTILE_MOD : is3d::kern::kTile;   // spectra_tile<MODE, FLAGS>()
   auto lds_bytes = [&](int qrows) {     // qrows = 0: F_LY layout (one y-term row per lane)
     const size_t nphp = (size_t)P.njb * P.KJ;
     return sizeof(double) * (2 * (size_t)kTile * NREC + 2 * (size_t)(kTile + 2) * nphp +
@@ -695,6 +701,13 @@ static SpectraPlan spectra_plan(const is3d_engine* e) {
 #endif
   P.ly = 0;
   P.shmem = lds_bytes(P.nqmax);
+  // the modified path's 16-cell tiles fall back to 8 (F_T8) before giving up the q-row tables
+  if (P.shmem > IS3D_LDS_QROW_LIMIT && mode >= PTM && kTile != is3d::kern::kTile) {
+    kTile = is3d::kern::kTile;
+    const size_t s8 = lds_bytes(P.nqmax);
+    if (s8 <= IS3D_LDS_QROW_LIMIT) { P.t8 = F_T8; P.shmem = s8; }
+    else kTile = IS3D_KTILE_MOD;
+  }
   // grids whose q rows do not fit (large y / eta tables with few species; np >= 86 keeps nqmax <= 4) run
   // the F_LY launch (KJ = 8, per-lane y-term rows, no q-row tables) instead of failing: the reference has
   // no grid limit
@@ -702,8 +715,10 @@ static SpectraPlan spectra_plan(const is3d_engine* e) {
     shape(8);
     P.tb = 0;
     P.ly = F_LY;
+    kTile = is3d::kern::kTile;     // spectra_tile<MODE, F_LY | ...>
     P.shmem = lds_bytes(0);
   }
+  P.tile = kTile;
   return P;
 }
 
@@ -801,6 +816,28 @@ static int finalize_tables(is3d_engine* e) {
   const size_t opd = cput(e->pdg_mass.data(), e->pdg_mass.size());
   cput(e->pdg_sign.data(), e->pdg_sign.size());
   cput(e->pdg_degen.data(), e->pdg_degen.size());
+  // PTMA Newton solve / famod coefficients: the reference sums its first min(320, N) PDG hadrons
+  // (MomentumSpectra.cpp:1295); the integrands depend on a hadron's (mass, sign) only, times its
+  // degeneracy, so hadrons with identical (mass, sign) are merged with summed degeneracies (SMASH:
+  // 320 -> 92, UrQMD: 320 -> 83; first-occurrence order).  Only the FP summation order changes, as it
+  // already does in the lane-strided sums (the Newton iteration counts still match the oracle's).
+  std::vector<double> am, as, ag;
+  {
+    const int nh = std::min(320, (int)e->pdg_mass.size());
+    for (int i = 0; i < nh; i++) {
+      int k = -1;
+      if (IS3D_ANISO_MERGE)
+        for (size_t u = 0; u < am.size(); u++)
+          if (am[u] == e->pdg_mass[i] && as[u] == e->pdg_sign[i]) { k = (int)u; break; }
+      if (k < 0) { am.push_back(e->pdg_mass[i]); as.push_back(e->pdg_sign[i]); ag.push_back(e->pdg_degen[i]); }
+      else ag[k] += e->pdg_degen[i];
+    }
+    if (am.empty()) { am.push_back(0.0); as.push_back(0.0); ag.push_back(0.0); }
+  }
+  e->n_aniso_h = e->pdg_mass.empty() ? 0 : (int)am.size();
+  const size_t oah = cput(am.data(), am.size());
+  cput(as.data(), as.size());
+  cput(ag.data(), ag.size());
   std::vector<double> sorig(np);
   dfree(e->d_const);
   const size_t nconst = cb.size() + np;   // ints appended as raw space
@@ -814,7 +851,7 @@ static int finalize_tables(is3d_engine* e) {
   e->d_smass = e->d_const + osm; e->d_ssign = e->d_const + oss; e->d_sbaryon = e->d_const + osb; e->d_sdegen = e->d_const + osd;
   e->d_degen_orig = e->d_const + odg; e->d_pT = e->d_const + opt; e->d_cphi = e->d_const + oc; e->d_sphi = e->d_const + os;
   e->d_y = e->d_const + oy; e->d_eta = e->d_const + oe; e->d_etaw = e->d_const + ow;
-  e->d_gla = e->d_const + og; e->d_pdg = e->d_const + opd;
+  e->d_gla = e->d_const + og; e->d_pdg = e->d_const + opd; e->d_aniso_h = e->d_const + oah;
   e->d_pTw = e->d_const + opw; e->d_phiw = e->d_const + ophw;
   e->d_csg = e->d_const + ocs;
   e->tables_dirty = false;
@@ -933,8 +970,8 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
     AnisoArgs aa{};
     aa.rec = e->d_rec; aa.ain = e->d_aux; aa.sol = e->d_sol; aa.n = n;
     aa.chains = (e->p.famod_chains > 0) ? std::min<long>(e->p.famod_chains, n) : n;
-    const int nh = std::min(320, (int)e->pdg_mass.size());
-    aa.h = Hadrons{nh, e->d_pdg, e->d_pdg + e->pdg_mass.size(), e->d_pdg + 2 * e->pdg_mass.size()};
+    const int nh = e->n_aniso_h;
+    aa.h = Hadrons{nh, e->d_aniso_h, e->d_aniso_h + nh, e->d_aniso_h + 2 * nh};
     aa.fp2 = 4.0 * std::pow(M_PI, 2) * std::pow(kHbarC, 3);
     aa.cnt = e->d_cnt;
     hipLaunchKernelGGL(k_aniso, dim3((unsigned)aa.chains), dim3(64), 0, st, aa);
@@ -962,6 +999,7 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   // cell splits: enough workgroups to fill the chip (>= 8k), and each split's records small enough
   // (~2 MB) to stay in one XCD's 4 MB L2 while that XCD's workgroups stream them; a multiple of 8
   // so every XCD owns whole splits; at most IS3D_MAX_SPLITS slabs (each one output-sized)
+  const long kTile = P.tile;                              // cells per tile of this mode's k_spectra
   const long max_split = (n + kTile - 1) / kTile;
   const long by_fill = (8192 + wgs - 1) / wgs;
   const long by_l2 = ((long)NREC * 8 * n + IS3D_SPLIT_BYTES - 1) / IS3D_SPLIT_BYTES;
@@ -983,7 +1021,7 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   sa.ntask = ntask; sa.cells_per_split = cps; sa.nbx = (int)bx; sa.nsplit = (int)nsplit; sa.sstride = sstride;
   sa.regulate = e->p.regulate_deltaf; sa.outflow = e->p.outflow; sa.dim = dim; sa.op = 1;
   const size_t shmem = P.shmem;
-  const int tb = P.tb | P.ly;
+  const int tb = P.tb | P.ly | P.t8;
   const dim3 grid((unsigned)(bx * npT * nsplit));
   const int kflags = (e->p.regulate_deltaf ? F_REG : 0) | (e->p.outflow ? F_OUT : 0) | tb;
   switch (mode) {

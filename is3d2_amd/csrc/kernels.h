@@ -15,6 +15,14 @@ constexpr int kBlock = 256;
 #define IS3D_KTILE 8
 #endif
 constexpr int kTile = IS3D_KTILE;   // cells per LDS tile
+#ifndef IS3D_KTILE_MOD
+#define IS3D_KTILE_MOD 16   // modified path (2 waves/SIMD, LDS allows it): 16 cells per tile, 1279 -> 1245 ms (r2t A/B)
+#endif
+// cells per k_spectra tile of one delta-f mode and launch (8 for Grad / RTA-CE: 16 costs them 18% / 11%,
+// r2t; the modified path's F_T8 and F_LY launches keep 8 where 16 cells' q-row tables would not fit:
+// config 1's shape in F_LY ran 11.2 ms with 8-cell tiles, 13.6 ms with 16)
+template <int MODE, int FLAGS>
+constexpr int spectra_tile() { return (MODE >= PTM && !(FLAGS & (16 | 8))) ? IS3D_KTILE_MOD : kTile; }
 // waves per SIMD the spectra kernel is register-allocated for (measured on MI355X, config2):
 // Grad and RTA-CE run best at 3 (168 VGPRs), the modified-momentum modes at 2
 #ifndef IS3D_SPECTRA_WAVES_SEP
@@ -71,7 +79,8 @@ struct SpecArgs {
 // (cell, q, phi) {PD, T1} table (sep_quad_tb_t); a workgroup then uses at most kTbQ q values
 // F_LY (grids whose q rows do not fit in LDS: large y / eta tables with few species, KJ = 8 only): every
 // lane builds its own y-term row in LDS and the modified lanes use their linear forms, no q-row tables
-constexpr int F_REG = 1, F_OUT = 2, F_TB = 4, F_LY = 8;
+// F_T8 (modified path): 8-cell tiles instead of IS3D_KTILE_MOD (q-row tables of many rows, config 1's shape)
+constexpr int F_REG = 1, F_OUT = 2, F_TB = 4, F_LY = 8, F_T8 = 16;
 constexpr int kTbQ = 4;
 
 #ifndef IS3D_SPLIT_BYTES
@@ -415,15 +424,15 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
-// dbl2 pairs of one record tile (kTile consecutive records of NREC doubles)
-constexpr int kTilePairs = kTile * NREC / 2;
 
 // Async copy of the record tile starting at cell cb into LDS (global_load_lds_dwordx4: no VGPR
 // staging; the LDS destination of a wave-instruction is base + 16 * lane, so the tile lands
 // in the same linear order as the records in HBM).  Completion is tracked by vmcnt.
+template <int KT>
 __device__ __forceinline__ void fetch_tile(const double* rec, long cb, long c_end, double* dst) {
+  constexpr int kTilePairs = KT * NREC / 2;   // dbl2 pairs of one record tile (KT records of NREC doubles)
   const int tid = threadIdx.x;
-  const long lim = (min(c_end, cb + kTile) - cb) * (NREC / 2);
+  const long lim = (min(c_end, cb + KT) - cb) * (NREC / 2);
   for (int base = 0; base < kTilePairs; base += kBlock) {
     const int e = base + tid;
     const int wave0 = base + (tid & ~63);
@@ -440,6 +449,7 @@ __device__ __forceinline__ void wait_fetch() { asm volatile("s_waitcnt vmcnt(0)"
 // summed by k_reduce, so a few species still fill the wavefronts
 template <int MODE, int FLAGS, int KJ>
 __global__ __launch_bounds__(kBlock, (spectra_waves_kj<MODE, KJ>())) void k_spectra(SpecArgs A) {
+  constexpr int kTile = spectra_tile<MODE, FLAGS>();      // cells per LDS tile for this mode / launch
   extern __shared__ double smem[];
   const int nphp = A.njb * KJ;                            // phi rows padded to KJ multiples
   double* s_recb = smem;                                  // [2][kTile][NREC] double-buffered
@@ -533,14 +543,14 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_kj<MODE, KJ>())) void k_spec
   const long c_end = min(A.n, c_begin + A.cells_per_split);
 
   // record tiles: tile i lives in buffer i & 1; tile i + 1 is copied in while tile i is integrated
-  if (c_begin < c_end) fetch_tile(A.rec, c_begin, c_end, s_recb);
+  if (c_begin < c_end) fetch_tile<kTile>(A.rec, c_begin, c_end, s_recb);
   int buf = 0;
   for (long cb = c_begin; cb < c_end; cb += kTile, buf ^= 1) {
     const int nt = (int)min((long)kTile, c_end - cb);
     double* s_rec = s_recb + buf * (kTile * NREC);
     wait_fetch();
     lds_barrier();     // tile cb visible to all waves; everyone is done with the previous tile
-    if (cb + kTile < c_end) fetch_tile(A.rec, cb + kTile, c_end, s_recb + (buf ^ 1) * (kTile * NREC));
+    if (cb + kTile < c_end) fetch_tile<kTile>(A.rec, cb + kTile, c_end, s_recb + (buf ^ 1) * (kTile * NREC));
     for (int idx = tid; idx < nt * nphp; idx += kBlock) {
       const int t = idx / nphp, j = idx % nphp;
       const double* R = s_rec + t * NREC;
@@ -574,7 +584,12 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_kj<MODE, KJ>())) void k_spec
         const double y = s_grid[kk];
         const double eta = (A.dim == 3) ? R[R_ETA] : s_grid[A.nk + l];
         const double w = s_grid[A.nk + A.nl + l];
+#if defined(IS3D_EXPERIMENT_NOLOOP) && IS3D_EXPERIMENT_NOLOOP == 3 || defined(IS3D_EXPERIMENT_NOY)
+        // measurement builds only (wrong results): y-terms replaced by a cheap fill
+        for (int f = 0; f < NYT; f++) s_y[((long)t * nyr + qq) * kYRow + f] = (f == Y_NARROW) ? 0.0 : 0.5 + y + eta + w;
+#else
         yterms(MODE, A.op, R, y, eta, w, s_y + ((long)t * nyr + qq) * kYRow);
+#endif
       }
     }
     lds_barrier();
@@ -624,6 +639,10 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_kj<MODE, KJ>())) void k_spec
           Y = Yl;
         }
         const bool sep = (MODE <= CE) || kind == 1.0 || Y[Y_NARROW] != 0.0;
+#if defined(IS3D_EXPERIMENT_NOLOOP) && IS3D_EXPERIMENT_NOLOOP >= 2
+        acc[0] += Y[Y_AT] + BP[0].x;     // measurement build only: tables and tiles, no lane work
+        continue;
+#endif
         if (sep) {
           SepLane L;
           sep_setup(sep_flavor(MODE), R, Y, mT, mT2, m2, mTb, pT, sign, baryon, s_etab, L,
@@ -631,6 +650,12 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_kj<MODE, KJ>())) void k_spec
           if (L.skip) continue;
           if constexpr (TB) {
             const dbl2* PT = s_pt + ((long)t * nqw + row) * prow;
+#ifdef IS3D_EXPERIMENT_NOLOOP
+            // measurement build only (A/B of the per-lane setup cost): no phi loop
+            acc[0] += L.a + L.D0 + L.escw + L.S0 + PT[0].x;
+            if (L.tail) acc[1] += L.D0;
+            continue;
+#endif
             if (IS3D_TAIL && L.tail) {
               if (MODE == GRAD && IS3D_TAIL_PD)
                 sep_phi_loop_pd_tail<FLAGS, KJ>(L, (cs_sptr)A.csg + 2L * (ipt * nphp + j0), BP, s_qv + t * nphp + j0, acc);
@@ -873,6 +898,17 @@ __global__ __launch_bounds__(kBlock, dndx_waves<MODE>()) void k_dndx(DndxArgs A)
 
 template <int MODE, int KJ>
 void launch_spectra_kj(dim3 grid, size_t shmem, hipStream_t st, const SpecArgs& a, int flags) {
+  if constexpr (MODE >= PTM) {
+    if (flags & F_T8) {
+      switch (flags & 3) {
+        case 0: hipLaunchKernelGGL((k_spectra<MODE, 16, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+        case 1: hipLaunchKernelGGL((k_spectra<MODE, 17, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+        case 2: hipLaunchKernelGGL((k_spectra<MODE, 18, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+        default: hipLaunchKernelGGL((k_spectra<MODE, 19, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+      }
+      return;
+    }
+  }
   if constexpr (KJ == 8) {
     if (flags & F_LY) {
       switch (flags & 3) {
