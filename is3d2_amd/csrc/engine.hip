@@ -685,14 +685,18 @@ static SpectraPlan spectra_plan(const is3d_engine* e) {
             KJ % 4 == 0 && P.nqmax <= kTbQ) ? F_TB : 0;
   };
   int kTile = (mode >= PTM) ? IS3D_KTILE_MOD : is3d::kern::kTile;   // spectra_tile<MODE, FLAGS>()
+  // k_spectra's LDS layout (kernels.h): record tiles x kRecBufs, per-tile tables x kTabBufs
   auto lds_bytes = [&](int qrows) {     // qrows = 0: F_LY layout (one y-term row per lane)
-    const size_t nphp = (size_t)P.njb * P.KJ;
-    return sizeof(double) * (2 * (size_t)kTile * NREC + 2 * (size_t)(kTile + 2) * nphp +
-                             2 * (size_t)kTile * nphp + (size_t)(nk + 2 * nl) +
-                             (qrows ? (size_t)kTile * std::min(qrows, P.nq) : (size_t)kBlock) * kYRow + kExpTabN +
-                             (P.tb ? 2 * (size_t)kTile * qrows * (P.KJ + 1) + 1 : 0) +
-                             (P.tb && mode == CE ? 2 * (size_t)kTile * nphp : 0) +
-                             (mode >= PTM && qrows ? (size_t)kTile * qrows * (P.KJ + 1) + 1 : 0));
+    const size_t nphp = (size_t)P.njb * P.KJ, tile = (size_t)kTile;
+    // pipelined launches (F_TB, the modified path's 16-cell tiles): 3 record tiles, 2 table buffers
+    const bool pipe = IS3D_PIPE && (P.tb || (mode >= PTM && qrows && !P.t8 && !P.ly));
+    const size_t rb = pipe ? 3 : 2, tb = pipe ? 2 : 1, qvf = (mode >= PTM || !pipe) ? 2 : 1;
+    return sizeof(double) * (rb * tile * NREC + 4 * nphp + tb * 2 * tile * nphp + tb * qvf * tile * nphp +
+                             (size_t)(nk + 2 * nl) +
+                             (qrows ? tb * tile * std::min(qrows, P.nq) : (size_t)kBlock) * kYRow + kExpTabN +
+                             (P.tb ? 2 * tile * qrows * (P.KJ + 1) + 1 : 0) +
+                             (P.tb && mode == CE ? tb * 2 * tile * nphp : 0) +
+                             (mode >= PTM && qrows ? tile * qrows * (P.KJ + 1) + 1 : 0));
   };
 #ifdef IS3D_FORCE_KJ
   shape(IS3D_FORCE_KJ);
@@ -704,9 +708,10 @@ static SpectraPlan spectra_plan(const is3d_engine* e) {
   // the modified path's 16-cell tiles fall back to 8 (F_T8) before giving up the q-row tables
   if (P.shmem > IS3D_LDS_QROW_LIMIT && mode >= PTM && kTile != is3d::kern::kTile) {
     kTile = is3d::kern::kTile;
+    P.t8 = F_T8;
     const size_t s8 = lds_bytes(P.nqmax);
-    if (s8 <= IS3D_LDS_QROW_LIMIT) { P.t8 = F_T8; P.shmem = s8; }
-    else kTile = IS3D_KTILE_MOD;
+    if (s8 <= IS3D_LDS_QROW_LIMIT) P.shmem = s8;
+    else { kTile = IS3D_KTILE_MOD; P.t8 = 0; }
   }
   // grids whose q rows do not fit (large y / eta tables with few species; np >= 86 keeps nqmax <= 4) run
   // the F_LY launch (KJ = 8, per-lane y-term rows, no q-row tables) instead of failing: the reference has
@@ -714,6 +719,7 @@ static SpectraPlan spectra_plan(const is3d_engine* e) {
   if (P.shmem > IS3D_LDS_QROW_LIMIT && !P.tb) {
     shape(8);
     P.tb = 0;
+    P.t8 = 0;
     P.ly = F_LY;
     kTile = is3d::kern::kTile;     // spectra_tile<MODE, F_LY | ...>
     P.shmem = lds_bytes(0);

@@ -119,8 +119,9 @@ constexpr int kTbQ = 4;
 #ifndef IS3D_TAIL_CE
 #define IS3D_TAIL_CE 0        // RTA-CE tail lanes (sep_quad_tb_tail_t): 3% slower on MI355X (r2d A/B: 697 vs 675 ms)
 #endif
-#ifndef IS3D_TAIL_MOD
-#define IS3D_TAIL_MOD 0       // modified-path tail loop (mod_quad_tail_t): 2.5% fewer VALU but 11% slower (r2d: 1445 vs 1297 ms)
+// (a modified-path tail loop, mod_quad_tail_t, ran 2.5% fewer VALU ops but 11% slower: r2d, 1445 vs 1297 ms)
+#ifndef IS3D_PIPE
+#define IS3D_PIPE 1           // k_spectra: tables of tile i + 1 built between the lane work of tile i (2 barriers per tile)
 #endif
 #ifndef IS3D_PAIR_RCP
 #define IS3D_PAIR_RCP 1       // fast path: two phi points per reciprocal (sep_pair_t)
@@ -317,20 +318,6 @@ __device__ __forceinline__ void sep_phi_loop_pd_tail(const SepLane& L, CSP CS, c
   }
 }
 
-// Boltzmann-tail modified lanes (M.tail): f = |renorm| en, no reciprocal (mod_quad_tail_t)
-template <int FLAGS, int KJ>
-__device__ __forceinline__ void mod_phi_loop_tail(const ModLane& M, const dbl2* CS, const dbl2* QV, double* acc) {
-  constexpr bool OUT = (FLAGS & F_OUT) != 0;
-  static_assert(KJ % 4 == 0, "tail loop needs phi blocks of fours");
-#pragma unroll
-  for (int jj = 0; jj < KJ; jj += 4) {
-    dbl2 c[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) c[i] = CS[jj + i];
-    mod_quad_tail_t<OUT>(M, c, QV[jj >> 1], QV[(jj >> 1) + 1], acc + jj);
-  }
-}
-
 // modified lanes of k_spectra, table form: {PDm, Qv} (MW) and T2 (MT) rows, four points per reciprocal
 template <int FLAGS, bool CLAMP, int KJ>
 __device__ __forceinline__ void mod_phi_loop_tab(const ModLane& M, const dbl2* MW, const double* MT, double* acc) {
@@ -452,21 +439,32 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_kj<MODE, KJ>())) void k_spec
   constexpr int kTile = spectra_tile<MODE, FLAGS>();      // cells per LDS tile for this mode / launch
   extern __shared__ double smem[];
   const int nphp = A.njb * KJ;                            // phi rows padded to KJ multiples
-  double* s_recb = smem;                                  // [2][kTile][NREC] double-buffered
-  dbl2* s_trig = (dbl2*)(s_recb + 2 * kTile * NREC);      // [nphp]        {cos, sin}
-  dbl2* s_cs = s_trig + nphp;                             // [nphp]        {pT cos, pT sin}
-  dbl2* s_bp = s_cs + nphp;                               // [kTile][nphp] {b', Phi}
-  // Grad / RTA-CE: [kTile][nphp] PD table; modified path: [kTile][nphp] {PDm, Qv} pairs (s_mw)
-  double* s_qv = (double*)(s_bp + kTile * nphp);
-  dbl2* s_mw = (dbl2*)s_qv;
-  double* s_grid = s_qv + 2 * kTile * nphp;               // y[nk] | eta[nl] | eta_w[nl]
-  const int nqm = A.nqmax;                                // rows per cell (>= every workgroup's nqw)
-  double* s_y = s_grid + A.nk + 2 * A.nl;                 // [kTile][min(nqm, nq)][kYRow]
   constexpr bool TB = (MODE == GRAD || MODE == CE) && (FLAGS & F_TB) != 0 && KJ % 4 == 0;
   constexpr bool LY = (FLAGS & F_LY) != 0;
-  // LY launches: s_y holds one y-term row per lane instead ([kBlock][kYRow]; odd row stride: no conflicts)
-  // y-term rows per cell: per row, or per q once the rows cover every q (nyr below): min(nqm, nq)
-  double* s_etab = s_y + (LY ? (long)kBlock : (long)kTile * min(nqm, A.nq)) * kYRow;   // [kExpTabN] 2^(j/kExpTabN)
+  // per-(cell, q, phi) tables built from the per-tile tables (phase C below): Grad / RTA-CE {PD, T1},
+  // modified path T2
+  constexpr bool HAS_C = TB || (MODE >= PTM && !LY);
+  // pipelined tile schedule (see the tile loop): record tiles triple-buffered, per-tile tables
+  // double-buffered.  Only the launches whose tables are small (F_TB: <= kTbQ rows per cell; the modified
+  // path's 16-cell tiles, which fall back to F_T8 when they do not fit): double y-term rows of many q
+  // values would cost a workgroup per CU (config 1's shape: 4.8 -> 5.7 ms, r2z)
+  constexpr bool PIPE = IS3D_PIPE && (TB || (MODE >= PTM && !(FLAGS & (F_LY | F_T8))));
+  constexpr int kRecBufs = PIPE ? 3 : 2, kTabBufs = PIPE ? 2 : 1;
+  constexpr int kQvF = (MODE >= PTM || !PIPE) ? 2 : 1;    // doubles per (cell, phi) of s_qv
+  const int nqm = A.nqmax;                                // rows per cell (>= every workgroup's nqw)
+  const long recsz = (long)kTile * NREC, bpsz = (long)kTile * nphp, qvsz = kQvF * bpsz;
+  // y-term rows per cell: per row, or per q once the rows cover every q (nyr below): min(nqm, nq);
+  // LY launches: one y-term row per lane instead ([kBlock][kYRow], single; odd row stride: no conflicts)
+  const long ysz = (LY ? (long)kBlock : (long)kTile * min(nqm, A.nq)) * kYRow;
+  double* s_recb = smem;                                  // [kRecBufs][kTile][NREC]
+  dbl2* s_trig = (dbl2*)(s_recb + kRecBufs * recsz);      // [nphp]        {cos, sin}
+  dbl2* s_cs = s_trig + nphp;                             // [nphp]        {pT cos, pT sin}
+  dbl2* s_bp = s_cs + nphp;                               // [kTabBufs][kTile][nphp] {b', Phi}
+  // Grad / RTA-CE: [kTabBufs][kTile][nphp] PD table; modified path: {PDm, Qv} pairs (s_mw)
+  double* s_qv = (double*)(s_bp + kTabBufs * bpsz);
+  double* s_grid = s_qv + kTabBufs * qvsz;                // y[nk] | eta[nl] | eta_w[nl]
+  double* s_y = s_grid + A.nk + 2 * A.nl;                 // [kTabBufs (LY: 1)][kTile][min(nqm, nq)][kYRow]
+  double* s_etab = s_y + (LY ? 1 : kTabBufs) * ysz;       // [kExpTabN] 2^(j/kExpTabN)
   // TB: [kTile][nqm][prow] {PD, T1}, 16-byte aligned for ds_read_b128 (s_grid's nk + 2 nl doubles
   // can leave s_etab at an odd double; misaligned dbl2 reads ran the kernel 3.5x slower)
   dbl2* s_pt = (dbl2*)(smem + (((s_etab + kExpTabN) - smem + 1) & ~1L));
@@ -474,7 +472,7 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_kj<MODE, KJ>())) void k_spec
   // at the same phi by the two halves of a wavefront that straddles a row boundary land in different
   // banks (a 512-B row stride is 128 dwords: the same bank, a 2-way conflict in every straddling wave)
   constexpr int prow = KJ + 1;
-  dbl2* s_pe = s_pt + kTile * nqm * prow;                 // TB, RTA-CE: [kTile][nphp] {TE, T2}
+  dbl2* s_pe = s_pt + kTile * nqm * prow;                 // TB, RTA-CE: [kTabBufs][kTile][nphp] {TE, T2}
   double* s_mt = (double*)s_pt;                           // modified path: [kTile][nqm][prow] T2 = 2 U_q . W
 
   const int tid = threadIdx.x;
@@ -542,16 +540,16 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_kj<MODE, KJ>())) void k_spec
   const long c_begin = (long)split * A.cells_per_split;
   const long c_end = min(A.n, c_begin + A.cells_per_split);
 
-  // record tiles: tile i lives in buffer i & 1; tile i + 1 is copied in while tile i is integrated
-  if (c_begin < c_end) fetch_tile<kTile>(A.rec, c_begin, c_end, s_recb);
-  int buf = 0;
-  for (long cb = c_begin; cb < c_end; cb += kTile, buf ^= 1) {
-    const int nt = (int)min((long)kTile, c_end - cb);
-    double* s_rec = s_recb + buf * (kTile * NREC);
-    wait_fetch();
-    lds_barrier();     // tile cb visible to all waves; everyone is done with the previous tile
-    if (cb + kTile < c_end) fetch_tile<kTile>(A.rec, cb + kTile, c_end, s_recb + (buf ^ 1) * (kTile * NREC));
-    for (int idx = tid; idx < nt * nphp; idx += kBlock) {
+  // ---- phase A / B of one tile (records s_rec, ntx cells) into table buffer tb: {b', Phi} and PD (or
+  // the modified path's {PDm, Qv}) per (cell, phi), {TE, T2} for RTA-CE's table launch, y-terms per
+  // (cell, row)
+  auto tables_ab = [&](const double* s_rec, int ntx, int tb) __attribute__((always_inline)) {
+    dbl2* bp = s_bp + tb * bpsz;
+    double* qvt = s_qv + tb * qvsz;
+    dbl2* mw = (dbl2*)qvt;
+    dbl2* pe = s_pe + tb * bpsz;
+    double* yb = s_y + tb * ysz;
+    for (int idx = tid; idx < ntx * nphp; idx += kBlock) {
       const int t = idx / nphp, j = idx % nphp;
       const double* R = s_rec + t * NREC;
       dbl2 v; v.x = 0.0; v.y = 0.0;                        // padding: finite, never written out
@@ -561,77 +559,117 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_kj<MODE, KJ>())) void k_spec
         v = phiterms(MODE, R, pT, tr.x, tr.y, s_etab);
         if (MODE >= PTM && R[R_KIND] == 2.0) qv = modqv(R, s_cs[j]);
       }
-      s_bp[t * nphp + j] = v;
+      bp[t * nphp + j] = v;
       if constexpr (MODE >= PTM) {
-        dbl2 mw; mw.x = modpdm(R, s_cs[j]); mw.y = qv;     // zero rows / padding give 0
-        s_mw[t * nphp + j] = mw;
+        dbl2 m; m.x = modpdm(R, s_cs[j]); m.y = qv;        // zero rows / padding give 0
+        mw[t * nphp + j] = m;
       } else {
-        s_qv[t * nphp + j] = sep_pd(R, s_cs[j], v.x);     // PD table (sep_pd)
+        qvt[t * nphp + j] = sep_pd(R, s_cs[j], v.x);      // PD table (sep_pd)
       }
       if constexpr (TB && MODE == CE) {
         const dbl2 c = s_cs[j];
         dbl2 e;
         e.x = -fma(R[R_UX], c.x, R[R_UY] * c.y);
         e.y = fma(R[R_LC], c.x, R[R_LS] * c.y);
-        s_pe[t * nphp + j] = e;
+        pe[t * nphp + j] = e;
       }
     }
-    for (int idx = tid; idx < (LY ? 0 : nt * nyr); idx += kBlock) {
+    for (int idx = tid; idx < (LY ? 0 : ntx * nyr); idx += kBlock) {
       const int t = idx / nyr, qq = idx % nyr, q = allq ? qq : (int)((r0 + qq) % A.nq);
       const double* R = s_rec + t * NREC;
       if (R[R_KIND] != 0.0) {
         const int kk = q / A.nl, l = q % A.nl;
         const double y = s_grid[kk];
         const double eta = (A.dim == 3) ? R[R_ETA] : s_grid[A.nk + l];
-        const double w = s_grid[A.nk + A.nl + l];
-#if defined(IS3D_EXPERIMENT_NOLOOP) && IS3D_EXPERIMENT_NOLOOP == 3 || defined(IS3D_EXPERIMENT_NOY)
-        // measurement builds only (wrong results): y-terms replaced by a cheap fill
-        for (int f = 0; f < NYT; f++) s_y[((long)t * nyr + qq) * kYRow + f] = (f == Y_NARROW) ? 0.0 : 0.5 + y + eta + w;
-#else
-        yterms(MODE, A.op, R, y, eta, w, s_y + ((long)t * nyr + qq) * kYRow);
-#endif
+        yterms(MODE, A.op, R, y, eta, s_grid[A.nk + A.nl + l], yb + ((long)t * nyr + qq) * kYRow);
       }
     }
-    lds_barrier();
-    if (MODE >= PTM && !LY) {
+  };
+  // ---- phase C: the per-(cell, row, phi) tables of one tile from its buffer-tb tables (single buffer)
+  auto tables_c = [&](const double* s_rec, int ntx, int tb) __attribute__((always_inline)) {
+    const double* qvt = s_qv + tb * qvsz;
+    const double* yb = s_y + tb * ysz;
+    if constexpr (MODE >= PTM && !LY) {
       // T2 = 2 U_q . W per (cell, q, phi) of the modified cells (mod_quad_tab_t)
-      for (int idx = tid; idx < nt * nqw * KJ; idx += kBlock) {
+      for (int idx = tid; idx < ntx * nqw * KJ; idx += kBlock) {
         const int jj = idx % KJ, r = idx / KJ, qq = r % nqw, t = r / nqw;
         const int j = (int)((r0 + qq) / A.nq) * KJ + jj;
         const double* R = s_rec + t * NREC;
         if (R[R_KIND] != 2.0) continue;
         const int yr = allq ? (int)((r0 + qq) % A.nq) : qq;
-        s_mt[((long)t * nqw + qq) * prow + jj] = modt2(R, s_y + ((long)t * nyr + yr) * kYRow, s_cs[j]);
+        s_mt[((long)t * nqw + qq) * prow + jj] = modt2(R, yb + ((long)t * nyr + yr) * kYRow, s_cs[j]);
       }
-      lds_barrier();
     }
     if constexpr (TB) {
       // {PD, T1 = SC1 pc + SS1 ps} per (cell, q, phi) (rows of skipped cells are never read)
-      for (int idx = tid; idx < nt * nqw * KJ; idx += kBlock) {
+      for (int idx = tid; idx < ntx * nqw * KJ; idx += kBlock) {
         const int jj = idx % KJ, r = idx / KJ, qq = r % nqw, t = r / nqw;
         const int j = (int)((r0 + qq) / A.nq) * KJ + jj;
-        const double* Y = s_y + ((long)t * nyr + (allq ? (int)((r0 + qq) % A.nq) : qq)) * kYRow;
+        const double* Y = yb + ((long)t * nyr + (allq ? (int)((r0 + qq) % A.nq) : qq)) * kYRow;
         const dbl2 c = s_cs[j];
         dbl2 v;
-        v.x = s_qv[t * nphp + j];
+        v.x = qvt[t * nphp + j];
         v.y = fma(Y[Y_SC1], c.x, Y[Y_SS1] * c.y);
         s_pt[((long)t * nqw + qq) * prow + jj] = v;
       }
+    }
+  };
+  // Tile schedule.  PIPE: a software pipeline over the split's record tiles (2 workgroup
+  // barriers per tile instead of 3); iteration i:
+  //   [records of tile i + 1 landed]  barrier X
+  //   copy the records of tile i + 2 (buffer (i + 2) % 3, last read by iteration i - 1)
+  //   phase C of tile i (from tables buffer i & 1)                          barrier Y (if phase C)
+  //   phases A / B of tile i + 1 into tables buffer (i + 1) & 1
+  //   lane work of tile i
+  // so the y-term wave's work and the tables of tile i + 1 overlap other waves' lane work of tile i instead
+  // of idling every wave at a barrier, and each record copy has a full tile of lead time.
+  // otherwise: two record buffers, one table buffer, A / B -> barrier -> C -> barrier -> lanes.
+  const int ntiles = (c_begin < c_end) ? (int)((c_end - c_begin + kTile - 1) / kTile) : 0;
+  auto tile_cb = [&](int i) { return c_begin + (long)i * kTile; };
+  auto tile_nt = [&](int i) { return (int)min((long)kTile, c_end - tile_cb(i)); };
+  auto recbuf = [&](int i) { return s_recb + (i % kRecBufs) * recsz; };
+  for (int i = 0; i < min(ntiles, kRecBufs - 1); i++) fetch_tile<kTile>(A.rec, tile_cb(i), c_end, recbuf(i));
+  if (PIPE && ntiles > 0) {
+    wait_fetch();
+    lds_barrier();     // tiles 0 and 1, the trig / grid / exp tables visible
+    tables_ab(recbuf(0), tile_nt(0), 0);
+  }
+  for (int i = 0; i < ntiles; i++) {
+    const double* s_rec = recbuf(i);
+    const long cbx = tile_cb(i);
+    const int ntx = tile_nt(i), tb = PIPE ? (i & 1) : 0;
+    wait_fetch();
+    lds_barrier();     // X: this tile's records (and, pipelined, its A / B tables) visible; the last tile is done
+    if (i + kRecBufs - 1 < ntiles)
+      fetch_tile<kTile>(A.rec, tile_cb(i + kRecBufs - 1), c_end, recbuf(i + kRecBufs - 1));
+    if (!PIPE) {
+      tables_ab(s_rec, ntx, 0);
       lds_barrier();
     }
+    if constexpr (HAS_C) {
+      tables_c(s_rec, ntx, tb);
+      lds_barrier();   // Y
+    }
+    if (PIPE && i + 1 < ntiles) tables_ab(recbuf(i + 1), tile_nt(i + 1), (i + 1) & 1);
     if (active) {
-      for (int t = 0; t < nt; t++) {
+      // the lane's phi points over the ntx cells of tile i
+      const dbl2* bpt = s_bp + tb * bpsz;
+      const double* qvt = s_qv + tb * qvsz;
+      const dbl2* mwt = (const dbl2*)qvt;
+      const dbl2* pet = s_pe + tb * bpsz;
+      const double* yb = s_y + tb * ysz;
+      for (int t = 0; t < ntx; t++) {
         const double* R = s_rec + t * NREC;
         const double kind = R[R_KIND];
         if (kind == 0.0) continue;
         double rn_abs = R[R_RENORM];
         if (MODE == PTM || MODE == PTB) {
-          const double rn = (MODE == PTM) ? A.renorm[(cb + t) * A.npart + s] : R[R_RENORM];
+          const double rn = (MODE == PTM) ? A.renorm[(cbx + t) * A.npart + s] : R[R_RENORM];
           if (!isfinite(rn)) continue;    // species skipped (MomentumSpectra.cpp:828-832)
           rn_abs = fabs(rn);
         }
-        const dbl2* BP = s_bp + t * nphp + j0;
-        const double* Y = s_y + ((long)t * nyr + yrow) * kYRow;
+        const dbl2* BP = bpt + t * nphp + j0;
+        const double* Y = yb + ((long)t * nyr + yrow) * kYRow;
         if constexpr (LY) {        // this lane's own y-terms, in its LDS row
           double* Yl = s_y + (long)tid * kYRow;
           const int kk = q / A.nl, l = q % A.nl;
@@ -639,10 +677,6 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_kj<MODE, KJ>())) void k_spec
           Y = Yl;
         }
         const bool sep = (MODE <= CE) || kind == 1.0 || Y[Y_NARROW] != 0.0;
-#if defined(IS3D_EXPERIMENT_NOLOOP) && IS3D_EXPERIMENT_NOLOOP >= 2
-        acc[0] += Y[Y_AT] + BP[0].x;     // measurement build only: tables and tiles, no lane work
-        continue;
-#endif
         if (sep) {
           SepLane L;
           sep_setup(sep_flavor(MODE), R, Y, mT, mT2, m2, mTb, pT, sign, baryon, s_etab, L,
@@ -650,34 +684,27 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_kj<MODE, KJ>())) void k_spec
           if (L.skip) continue;
           if constexpr (TB) {
             const dbl2* PT = s_pt + ((long)t * nqw + row) * prow;
-#ifdef IS3D_EXPERIMENT_NOLOOP
-            // measurement build only (A/B of the per-lane setup cost): no phi loop
-            acc[0] += L.a + L.D0 + L.escw + L.S0 + PT[0].x;
-            if (L.tail) acc[1] += L.D0;
-            continue;
-#endif
             if (IS3D_TAIL && L.tail) {
               if (MODE == GRAD && IS3D_TAIL_PD)
-                sep_phi_loop_pd_tail<FLAGS, KJ>(L, (cs_sptr)A.csg + 2L * (ipt * nphp + j0), BP, s_qv + t * nphp + j0, acc);
+                sep_phi_loop_pd_tail<FLAGS, KJ>(L, (cs_sptr)A.csg + 2L * (ipt * nphp + j0), BP, qvt + t * nphp + j0, acc);
               else
-                sep_phi_loop_tb_tail<MODE, FLAGS, KJ>(L, mT, BP, PT, s_pe + t * nphp + j0, acc);
+                sep_phi_loop_tb_tail<MODE, FLAGS, KJ>(L, mT, BP, PT, pet + t * nphp + j0, acc);
             }
-            else if (L.fast) sep_phi_loop_tb<MODE, FLAGS, KJ>(L, mT, BP, PT, s_pe + t * nphp + j0, acc);
+            else if (L.fast) sep_phi_loop_tb<MODE, FLAGS, KJ>(L, mT, BP, PT, pet + t * nphp + j0, acc);
             else sep_phi_loop<MODE, FLAGS, false, KJ>(L, s_cs + j0, BP, acc);
           } else if (IS3D_PD_TABLE && IS3D_CS_SCALAR && MODE <= CE && KJ % 4 == 0 && L.fast && A.njb == 1)
             // one phi block: every lane reads the same {pc, ps}, so they come by scalar loads into SGPRs
             // (VALU operands) instead of LDS
-            sep_phi_loop_pd<MODE, FLAGS, KJ, true>(L, (cs_sptr)A.csg + 2L * ipt * nphp,
-                                                   BP, s_qv + t * nphp, acc);
+            sep_phi_loop_pd<MODE, FLAGS, KJ, true>(L, (cs_sptr)A.csg + 2L * ipt * nphp, BP, qvt + t * nphp, acc);
           else if (IS3D_PD_TABLE && MODE <= CE && KJ % 4 == 0 && L.fast)
-            sep_phi_loop_pd<MODE, FLAGS, KJ, true>(L, s_cs + j0, BP, s_qv + t * nphp + j0, acc);
+            sep_phi_loop_pd<MODE, FLAGS, KJ, true>(L, s_cs + j0, BP, qvt + t * nphp + j0, acc);
           else if (L.fast) sep_phi_loop<MODE, FLAGS, true, KJ>(L, s_cs + j0, BP, acc);
           else sep_phi_loop<MODE, FLAGS, false, KJ>(L, s_cs + j0, BP, acc);
         } else if (MODE >= PTM) {
           ModLane M;
           mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, s_etab, M);
           if (M.skip) continue;
-          const dbl2* MW = s_mw + t * nphp + j0;
+          const dbl2* MW = mwt + t * nphp + j0;
           if constexpr (LY) {        // no T2 rows: the lane's linear forms (mod_pair_lane_t)
             if (M.clamp) mod_phi_loop_lane<FLAGS, true, KJ>(M, s_cs + j0, MW, acc);
             else mod_phi_loop_lane<FLAGS, false, KJ>(M, s_cs + j0, MW, acc);
