@@ -235,6 +235,21 @@ IS3D_HD double exp_tab(const ExpTabCoef& E, const double* tab, double xN, int ks
   return ldexp(fma(T, rs * q, T), (ki >> IS3D_EXP_TAB_BITS) - kshift);
 }
 
+// e^(a v ln2 / kExpTabN) for a product a v (|a v| < 2^51) with the range reduction folded into the
+// product: t = fma(a, v, shift) rounds a v to the integer K exactly (one rounding), shift - t = -K
+// exactly, and rs = fma(a, v, -K) is the remainder with a single rounding -- three ops where
+// xN = a v, xN + shift, t - shift, xN - K took four (modified path, mod_en_x)
+IS3D_HD double exp_tab_fma(const ExpTabCoef& E, const double* tab, double a, double v) {
+  const double t = fma(a, v, E.shift);
+  const double rs = fma(a, v, E.shift - t);
+  const int ki = (int)(unsigned)__builtin_bit_cast(unsigned long long, t);
+  double q = E.a[kExpTabDeg - 1];
+#pragma unroll
+  for (int i = kExpTabDeg - 2; i >= 0; i--) q = fma(q, rs, E.a[i]);
+  const double T = tab[ki & (kExpTabN - 1)];
+  return ldexp(fma(T, rs * q, T), ki >> IS3D_EXP_TAB_BITS);
+}
+
 // sinh and cosh of d for the y-terms: |d| < 0.5 by their Taylor series through d^17 / d^16 (truncation
 // < 5e-20 relative), otherwise from e = e^d and 1/e (e -/+ 1/e loses at most a factor coth(0.5) = 2.2 in
 // relative accuracy): ~25 VALU ops instead of the library's double-double sinh / cosh (~100 each)
@@ -530,6 +545,16 @@ IS3D_HD void modified_directions(const double* Asym, double tau, double Xt, doub
   for (int d = 0; d < 4; d++) lu3_solve(LU, perm, dirs[d], rec_u + 3 * d);
 }
 
+// Last step of the modified-path prologues (R_INVTM, R_CHEMM, R_VB and the directions set): Uc, Us, Vc,
+// Vs and R_VB in exp-table units, scaled by sig = (1/T_mod) kExpTabN/ln2, so that every E_mod^2 the
+// lanes build (mod_setup, modqv, modt2) is (sig E_mod)^2 and its square root is exp_tab's argument
+// without a multiply
+IS3D_HD void mod_scale_record(double* R) {
+  const double sig = R[R_INVTM] * kInvLn2xN;
+  for (int f = R_UCX; f <= R_VSZ; f++) R[f] *= sig;
+  R[R_VB] *= sig;
+}
+
 // ---------------------------------------------------------------------------
 // Milne basis / LRF boosts (LocalRestFrame.cpp:12-41, 133-154)
 // ---------------------------------------------------------------------------
@@ -738,6 +763,7 @@ IS3D_HD int prep_feqmod(const PrepConsts& k, const DfTables& tb, const double* s
   modified_directions(A, tau, b.Xt, b.Xx, b.Xy, b.Xn, b.Yx, b.Yy, b.Zt, b.Zn, R + R_UCX);
   R[R_VB] = sqrt(R[R_VCX] * R[R_VCX] + R[R_VCY] * R[R_VCY] + R[R_VCZ] * R[R_VCZ]) +
             sqrt(R[R_VSX] * R[R_VSX] + R[R_VSY] * R[R_VSY] + R[R_VSZ] * R[R_VSZ]);
+  mod_scale_record(R);
   aux[0] = T; aux[1] = T_mod; aux[2] = alphaB; aux[3] = alphaB_mod; aux[4] = F; aux[5] = G; aux[6] = betabulk; aux[7] = bulkPi;
   aux[8] = den;
   R[R_KIND] = breaks ? 1.0 : 2.0;
@@ -934,6 +960,7 @@ IS3D_HD void prep_famod_b(const PrepConsts& k, double* R, const double* ain, con
   R[R_VB] = sqrt(R[R_VCX] * R[R_VCX] + R[R_VCY] * R[R_VCY] + R[R_VCZ] * R[R_VCZ]) +
             sqrt(R[R_VSX] * R[R_VSX] + R[R_VSY] * R[R_VSY] + R[R_VSZ] * R[R_VSZ]);
   R[R_INVTM] = 1.0 / lambda;
+  mod_scale_record(R);
   R[R_ETASCALE] = eta_scale; R[R_DET] = detB;
   R[R_NARROW] = (k.dim == 3 && detB < 0.01) ? 1.0 : 0.0;
   R[R_RENORM] = fabs(renorm);
@@ -1529,17 +1556,20 @@ IS3D_HD double sqrt_nr(double v) {
 // en = exp(chem - E_mod/T_mod): u.p > 0 bounds en by e^chem and, for bosons (no baryon number),
 // below 1, so 1 + sign en lies in ~[1e-3, 2] and two points can share one reciprocal; en -> 0
 // where the reference's exp overflows to 1/inf = 0.  |renorm| is folded into p.dsigma.
+// Exp-table units: the record's directions are scaled by sig = (1/T_mod) kExpTabN/ln2
+// (mod_scale_record), so E0 + Qv + ... = (sig E_mod)^2 and sqrt of it is exp_tab's argument; on the
+// table lanes (!clamp) e^chem is folded out of the exponential into sign and the p.dsigma
+// coefficients (en = e^chem e^-E/T: en / (1 + sign en) = e^chem e / (1 + (sign e^chem) e)), so a point
+// evaluates e^(-sig E_mod) alone.
 struct ModLane {
-  double E0, Ec, Es, D0, Dc, Ds, invTm, chemm, sign;
+  double E0, Ec, Es, D0, Dc, Ds, chemm, sign;   // table lanes: sign = sign e^chem, D = |renorm| e^chem D
   double mT, Dw;               // table form (mod_quad_tab_t): E_mod^2 = E0 + Qv + mT T2, p.dsigma = D0 + Dw PDm
-  double invTmN, chemmN;       // invTm, chemm x 64/ln2 (exp_tab's scaled argument)
   ExpTabCoef et;               // pinned once per lane setup, reused by every phi point
-  const double* etab;          // 2^(j/64) table (LDS on the device)
-  int skip, clamp;   // clamp: some point's exp argument may leave exp_tab's domain (exp_clamped instead)
-  int tail;          // Boltzmann tail: en < 2^-54 at every phi point, so 1 + sign en == 1 (mod_quad_tail_t)
+  const double* etab;          // 2^(j/kExpTabN) table (LDS on the device)
+  int skip, clamp;   // clamp: some point's exp argument may leave the table lanes' domain (exp_clamped instead)
 };
 
-// Qv = |pc Vc + ps Vs|^2 for one (cell, phi)
+// Qv = |pc Vc + ps Vs|^2 for one (cell, phi), exp-table units (sig^2)
 IS3D_HD double modqv(const double* R, dbl2 cs) {
   const double wx = fma(cs.x, R[R_VCX], cs.y * R[R_VSX]);
   const double wy = fma(cs.x, R[R_VCY], cs.y * R[R_VSY]);
@@ -1547,39 +1577,55 @@ IS3D_HD double modqv(const double* R, dbl2 cs) {
   return fma(wx, wx, fma(wy, wy, wz * wz));
 }
 
+// ln2 / kExpTabN: sig E_mod x this = E_mod / T_mod
+static constexpr double kLn2overN = 1.0 / kInvLn2xN;
+// table lanes: E_mod / T_mod below 1e6 (exp_tab's integer part fits the low word; beyond e^-745 en is
+// 0 anyway) and |chem| < 30: where e^(-E/T) underflows (E/T > 745) the reference's exp(E/T - chem)
+// overflows too (E/T - chem > 715), so folding e^chem out loses nothing, and four 1 + sign e^chem e
+// factors multiply without overflow in the quad reciprocal
+static constexpr double kModTabX = 1.0e6, kModTabChem = 30.0;
+#ifndef IS3D_MODQ_ACC
+#define IS3D_MODQ_ACC 1
+#endif
+
 IS3D_HD void mod_setup(const double* R, const double* Y, double mT, double m2, double pT, double sign, double baryon,
                        double renorm_abs, const double* etab, ModLane& L) {
-  const double ux = Y[Y_MUX], uy = Y[Y_MUY], uz = Y[Y_MUZ];
+  const double ux = Y[Y_MUX], uy = Y[Y_MUY], uz = Y[Y_MUZ];   // sig U
   const double u2 = fma(ux, ux, fma(uy, uy, uz * uz));
-  L.E0 = fma(mT * mT, u2, m2);
+  const double sig = R[R_INVTM] * kInvLn2xN, m2s = m2 * (sig * sig);
+  L.E0 = fma(mT * mT, u2, m2s);
   const double tm = 2.0 * mT;
   L.Ec = tm * fma(ux, R[R_VCX], fma(uy, R[R_VCY], uz * R[R_VCZ]));
   L.Es = tm * fma(ux, R[R_VSX], fma(uy, R[R_VSY], uz * R[R_VSZ]));
-  L.D0 = renorm_abs * (mT * Y[Y_MD]); L.Dc = renorm_abs * Y[Y_WDX]; L.Ds = renorm_abs * Y[Y_WDY];
-  L.mT = mT; L.Dw = renorm_abs * Y[Y_W];
-  L.sign = sign;
-  L.invTm = R[R_INVTM]; L.chemm = baryon * R[R_CHEMM];
-  L.invTmN = L.invTm * kInvLn2xN; L.chemmN = L.chemm * kInvLn2xN;
+  L.mT = mT;
+  L.chemm = baryon * R[R_CHEMM];
   L.et = exp_tab_coef();
   L.etab = etab;
-  // | |mT U| - pT |V|max | <= |p_mod| <= |mT U| + pT |V|max: if even the smallest E_mod overflows
-  // exp, every phi point is exactly 0; if the largest could push the exp argument out of
-  // exp_poly's domain the lane takes the clamped exp
+  // | |mT U| - pT |V|max | <= |p_mod| <= |mT U| + pT |V|max (sig units): if even the smallest E_mod
+  // overflows exp, every phi point is exactly 0; if the largest could leave the table lanes' domain
+  // the lane takes the clamped exp
   const double mu = mT * sqrt(u2);
   const double lo = mu - pT * R[R_VB], hi = mu + pT * R[R_VB];
-  const double emin = (lo > 0.0) ? sqrt(m2 + lo * lo) * (1.0 - 1e-12) : 0.0;
-  L.skip = (emin * L.invTm - L.chemm > kExpMax + 1.0) ? 1 : 0;
-  const double xlo = L.chemm - sqrt(m2 + hi * hi) * L.invTm;
-  L.clamp = (xlo > -1.0e6 && L.chemm < 700.0) ? 0 : 1;
-  L.tail = (!L.clamp && emin * L.invTm - L.chemm > kTailX) ? 1 : 0;
+  const double emin = (lo > 0.0) ? sqrt(m2s + lo * lo) * (1.0 - 1e-12) : 0.0;
+  L.skip = (emin * kLn2overN - L.chemm > kExpMax + 1.0) ? 1 : 0;
+  const double emax = sqrt(m2s + hi * hi) * kLn2overN;
+  L.clamp = (emax < kModTabX && fabs(L.chemm) < kModTabChem) ? 0 : 1;
+  // e^chem of the table lanes (1 for mesons and without baryon chemistry: a wave-uniform skip there)
+  double ec = 1.0;
+  if (!L.clamp && L.chemm != 0.0) ec = exp_tab(L.et, etab, L.chemm * kInvLn2xN);
+  const double d = renorm_abs * ec;
+  L.sign = sign * ec;
+  L.D0 = d * (mT * Y[Y_MD]); L.Dc = d * Y[Y_WDX]; L.Ds = d * Y[Y_WDY];
+  L.Dw = d * Y[Y_W];
 }
 
-// en = exp(chem - E_mod / T_mod) at one phi point (qv = modqv of the cell at this phi)
+// en at one phi point (qv = modqv of the cell at this phi): e^(chem - E_mod / T_mod) on clamped lanes,
+// e^(-E_mod / T_mod) on table lanes (e^chem folded into the lane, mod_setup)
 template <bool CLAMP>
 IS3D_HD double mod_en(const ModLane& L, dbl2 cs, double qv) {
-  const double Emod = sqrt_nr(fma(L.Ec, cs.x, fma(L.Es, cs.y, L.E0 + qv)));
-  if (CLAMP) return exp_clamped(exp_coef(), fma(-Emod, L.invTm, L.chemm));
-  return exp_tab(L.et, L.etab, fma(-Emod, L.invTmN, L.chemmN));
+  const double Emod = sqrt_nr(fma(L.Ec, cs.x, fma(L.Es, cs.y, L.E0 + qv)));   // sig E_mod
+  if (CLAMP) return exp_clamped(exp_coef(), fma(-Emod, kLn2overN, L.chemm));
+  return exp_tab(L.et, L.etab, -Emod);
 }
 
 template <bool OUT, bool CLAMP>
@@ -1634,11 +1680,12 @@ IS3D_HD double modt2(const double* R, const double* Y, dbl2 cs) {
   return 2.0 * fma(Y[Y_MUX], wx, fma(Y[Y_MUY], wy, Y[Y_MUZ] * wz));
 }
 
-// en = exp(chem - sqrt(X) / T_mod): one Newton step of the v_rsq_f64 estimate y folded into the exp
-// argument, sqrt(X) = g v with g = X y, v = 1.5 - 0.5 g y (5 ops where sqrt_nr + fma took 6)
+// en from X = (sig E_mod)^2: one Newton step of the v_rsq_f64 estimate y folded into the exp argument,
+// sig E_mod = g v with g = X y, v = 1.5 - 0.5 g y, and the range reduction folded into the product
+// (exp_tab_fma): 6 ops + rsq where sqrt_nr, the 1/T_mod scale, chem and the reduction took 9
 template <bool CLAMP>
 IS3D_HD double mod_en_x(const ModLane& L, double X) {
-  if (CLAMP) return exp_clamped(exp_coef(), fma(-sqrt_nr(X), L.invTm, L.chemm));
+  if (CLAMP) return exp_clamped(exp_coef(), fma(-sqrt_nr(X), kLn2overN, L.chemm));
 #if defined(__HIP_DEVICE_COMPILE__)
   const double y = __builtin_amdgcn_rsq(X);
 #else
@@ -1646,11 +1693,13 @@ IS3D_HD double mod_en_x(const ModLane& L, double X) {
 #endif
   const double g = X * y;
   const double v = fma(-0.5, g * y, 1.5);
-  return exp_tab(L.et, L.etab, fma(-(g * L.invTmN), v, L.chemmN));
+  return exp_tab_fma(L.et, L.etab, -g, v);
 }
 
-template <bool OUT, bool CLAMP>
-IS3D_HD void mod_quad_tab_t(const ModLane& L, const dbl2* mw, const double* mt, double* v) {
+// four points, one reciprocal, accumulated into acc: f_i = en_i / q_i = en_i q_j (1 / q_i q_j) with j the
+// pair partner, so acc_i = fma(pds_i en_i q_j, r_ij, acc_i) -- 4 ops per point after the shared reciprocal
+template <bool OUT, bool CLAMP, typename ACC>
+IS3D_HD void mod_quad_tab_t(const ModLane& L, const dbl2* mw, const double* mt, ACC acc) {
   double en[4], q[4];
 #pragma unroll
   for (int i = 0; i < 4; i++) {
@@ -1659,14 +1708,25 @@ IS3D_HD void mod_quad_tab_t(const ModLane& L, const dbl2* mw, const double* mt, 
   }
   const double q01 = q[0] * q[1], q23 = q[2] * q[3];
   const double r = rcp1(q01 * q23);
+#if IS3D_MODQ_ACC
+  const double rp[4] = {r * q23, r * q23, r * q01, r * q01};
+  const double h[4] = {en[0] * q[1], en[1] * q[0], en[2] * q[3], en[3] * q[2]};
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    double pds = fma(L.Dw, mw[i].x, L.D0);
+    if (OUT) pds = (pds <= 0.0) ? 0.0 : pds;
+    acc[i] = fma(pds * h[i], rp[i], acc[i]);
+  }
+#else
   const double r01 = r * q23, r23 = r * q01;
   const double rq[4] = {r01 * q[1], r01 * q[0], r23 * q[3], r23 * q[2]};
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     const double pds = fma(L.Dw, mw[i].x, L.D0);
     const double g = pds * (en[i] * rq[i]);
-    v[i] = (OUT && pds <= 0.0) ? 0.0 : g;
+    acc[i] += (OUT && pds <= 0.0) ? 0.0 : g;
   }
+#endif
 }
 
 template <bool OUT, bool CLAMP>
@@ -1693,20 +1753,6 @@ IS3D_HD void mod_pair_lane_t(const ModLane& L, dbl2 c0, dbl2 c1, double qv0, dou
   const double g0 = pds0 * (en0 * (r * q1)), g1 = pds1 * (en1 * (r * q0));
   v0 = (OUT && pds0 <= 0.0) ? 0.0 : g0;
   v1 = (OUT && pds1 <= 0.0) ? 0.0 : g1;
-}
-
-// four points of a Boltzmann-tail lane (L.tail): f = |renorm| en exactly (1 + sign en rounds to 1),
-// accumulated straight into acc -- no reciprocal
-template <bool OUT>
-IS3D_HD void mod_quad_tail_t(const ModLane& L, const dbl2* c, dbl2 qa, dbl2 qb, double* acc) {
-  const double qv[4] = {qa.x, qa.y, qb.x, qb.y};
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const double en = mod_en<false>(L, c[i], qv[i]);
-    double pds = lin(L.D0, L.Dc, L.Ds, c[i]);
-    if (OUT) pds = (pds <= 0.0) ? 0.0 : pds;
-    acc[i] = fma(pds, en, acc[i]);
-  }
 }
 
 IS3D_HD void mod_quad(const ModLane& L, const dbl2* c, dbl2 qa, dbl2 qb, int outflow, double* v) {

@@ -173,6 +173,34 @@ __global__ __launch_bounds__(256) void k_renorm(RenormArgs A) {
   A.renorm[idx] = ptm_renorm(A.k, aux, A.mass[s], A.sign[s], A.degen[s], A.baryon[s]);
 }
 
+// Modified modes: the cells whose lanes may take the separable fallback (breakdown: R_KIND == 1; narrow
+// rapidity windows: R_NARROW != 0, MomentumSpectra.cpp:863-871), listed in ascending order for the F_FB
+// launch.  One workgroup: each thread counts a contiguous chunk, an LDS scan gives the offsets, the chunks
+// are written in order -- deterministic, and no host round trip (the count stays on the device).
+__global__ __launch_bounds__(1024) void k_fbscan(const double* rec, long n, int* cells, int* count) {
+  __shared__ int s_off[1024];
+  const int t = threadIdx.x;
+  const long ch = (n + 1023) / 1024, lo = min(n, t * ch), hi = min(n, lo + ch);
+  auto fb = [&](long c) {
+    const double* R = rec + c * NREC;
+    return R[R_KIND] == 1.0 || (R[R_KIND] == 2.0 && R[R_NARROW] != 0.0);
+  };
+  int cnt = 0;
+  for (long c = lo; c < hi; c++) cnt += fb(c) ? 1 : 0;
+  s_off[t] = cnt;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {     // inclusive Hillis-Steele scan
+    const int v = (t >= d) ? s_off[t - d] : 0;
+    __syncthreads();
+    s_off[t] += v;
+    __syncthreads();
+  }
+  int o = s_off[t] - cnt;
+  for (long c = lo; c < hi; c++)
+    if (fb(c)) cells[o++] = (int)c;
+  if (t == 1023) *count = s_off[1023];
+}
+
 struct ReduceArgs {
   const double* slab; long sstride; int nsplit;
   int nbx, npart, npT, nphi, nk, nl, ny_out, kj; long ntask;
@@ -466,6 +494,8 @@ struct is3d_engine {
   double* d_surf = nullptr; bool surf_owned = false; long ncell = 0; long surf_cap = 0;
   double *d_rec = nullptr, *d_aux = nullptr, *d_sol = nullptr, *d_renorm = nullptr, *d_slab = nullptr, *d_out = nullptr;
   long rec_cap = 0, aux_cap = 0, sol_cap = 0, renorm_cap = 0, slab_cap = 0, out_cap = 0;
+  int* d_fb = nullptr;        // modified modes: [0] fallback cell count, [1..] k_fbscan's cell list
+  long fb_cap = 0;
   // operation 0
   double *d_ycell = nullptr, *d_part = nullptr; long ycell_cap = 0, part_cap = 0;
   int *d_keys = nullptr, *d_perm = nullptr; long keys_cap = 0, perm_cap = 0;
@@ -514,6 +544,7 @@ extern "C" void is3d_destroy(is3d_engine* e) {
   dfree(e->d_tables); dfree(e->d_const);
   if (e->surf_owned) dfree(e->d_surf);
   dfree(e->d_rec); dfree(e->d_aux); dfree(e->d_sol); dfree(e->d_renorm); dfree(e->d_slab); dfree(e->d_out);
+  dfree(e->d_fb);
   dfree(e->d_ycell); dfree(e->d_part); dfree(e->d_keys); dfree(e->d_perm); dfree(e->d_offs);
   dfree(e->d_err); dfree(e->d_cnt);
   for (auto& v : e->ev) if (v) (void)hipEventDestroy(v);
@@ -664,6 +695,7 @@ static int device_jonah_table(is3d_engine* e, const double* r2, const double* w2
 struct SpectraPlan {
   int KJ, njb, nq, nqmax, tb, ly, t8, tile;
   size_t shmem;
+  size_t shmem_fb;            // modified modes: the F_FB launch (8-cell tiles, per-lane y-term rows, no q tables)
 };
 static SpectraPlan spectra_plan(const is3d_engine* e) {
   SpectraPlan P{};
@@ -725,6 +757,13 @@ static SpectraPlan spectra_plan(const is3d_engine* e) {
     P.shmem = lds_bytes(0);
   }
   P.tile = kTile;
+  if (mode >= PTM) {
+    const int t = kTile, ly = P.ly, tb = P.tb, t8 = P.t8;
+    kTile = is3d::kern::kTile;
+    P.ly = F_LY; P.tb = 0; P.t8 = 0;
+    P.shmem_fb = lds_bytes(0);
+    kTile = t; P.ly = ly; P.tb = tb; P.t8 = t8;
+  }
   return P;
 }
 
@@ -1016,7 +1055,15 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   cps = ((cps + kTile - 1) / kTile) * kTile;
   nsplit = (n + cps - 1) / cps;
   const long sstride = (long)npT * bx * KJ * kBlock;
-  if (!ensure(e->d_slab, e->slab_cap, nsplit * sstride)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(slabs) failed");
+  // modified modes: the F_FB launch (separable-fallback lanes, cells listed by k_fbscan) writes its own
+  // nsplit_fb slabs after the main ones; k_reduce sums both
+  const long nsplit_fb = (mode >= PTM) ? std::max(1L, std::min(nsplit, 8L)) : 0;
+  if (!ensure(e->d_slab, e->slab_cap, (nsplit + nsplit_fb) * sstride)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(slabs) failed");
+  if (mode >= PTM) {
+    if (!ensure(e->d_fb, e->fb_cap, n + 1)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(fallback list) failed");
+    hipLaunchKernelGGL(k_fbscan, dim3(1), dim3(1024), 0, st, (const double*)e->d_rec, n, e->d_fb + 1, e->d_fb);
+    HIPCHK(e, hipGetLastError());
+  }
   SpecArgs sa{};
   sa.rec = e->d_rec; sa.n = n; sa.renorm = e->d_renorm; sa.slab = e->d_slab; sa.outsize = outsize;
   sa.smass = e->d_smass; sa.ssign = e->d_ssign; sa.sbaryon = e->d_sbaryon; sa.sorig = e->d_sorig;
@@ -1038,15 +1085,28 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
     default: launch_spectra<PTMA>(grid, shmem, st, sa, kflags, KJ); break;
   }
   HIPCHK(e, hipGetLastError());
+  if (mode >= PTM) {
+    SpecArgs fa = sa;
+    fa.slab = e->d_slab + nsplit * sstride; fa.nsplit = (int)nsplit_fb; fa.cells_per_split = 0;
+    fa.fbcells = e->d_fb + 1; fa.fbcount = e->d_fb;
+    const int fflags = (e->p.regulate_deltaf ? F_REG : 0) | (e->p.outflow ? F_OUT : 0) | F_FB;
+    const dim3 gfb((unsigned)(bx * npT * nsplit_fb));
+    switch (mode) {
+      case PTM: launch_spectra<PTM>(gfb, P.shmem_fb, st, fa, fflags, KJ); break;
+      case PTB: launch_spectra<PTB>(gfb, P.shmem_fb, st, fa, fflags, KJ); break;
+      default: launch_spectra<PTMA>(gfb, P.shmem_fb, st, fa, fflags, KJ); break;
+    }
+    HIPCHK(e, hipGetLastError());
+  }
   HIPCHK(e, hipEventRecord(e->ev[2], st));
   ReduceArgs ra{};
-  ra.slab = e->d_slab; ra.sstride = sstride; ra.nsplit = (int)nsplit;
+  ra.slab = e->d_slab; ra.sstride = sstride; ra.nsplit = (int)(nsplit + nsplit_fb);
   ra.nbx = (int)bx; ra.npart = np; ra.npT = npT; ra.nphi = nphi; ra.nk = nk; ra.nl = nl; ra.ny_out = ny_out; ra.kj = KJ;
   ra.ntask = ntask;
   ra.sorig = e->d_sorig; ra.degen_orig = e->d_degen_orig; ra.prefactor = std::pow(2.0 * M_PI * kHbarC, -3);
   ra.out = dev_out;
   // one wavefront per output when each output sums many (eta node, split) terms and there are few outputs
-  if ((long)nl * nsplit >= 128 && sstride / nl < (1L << 20)) {
+  if ((long)nl * ra.nsplit >= 128 && sstride / nl < (1L << 20)) {
     const long nout = (long)np * npT * nphi * ny_out;
     hipLaunchKernelGGL(k_reduce_wave, dim3((unsigned)((nout + 3) / 4)), dim3(256), 0, st, ra);
   } else {

@@ -16,20 +16,21 @@ constexpr int kBlock = 256;
 #endif
 constexpr int kTile = IS3D_KTILE;   // cells per LDS tile
 #ifndef IS3D_KTILE_MOD
-#define IS3D_KTILE_MOD 16   // modified path (2 waves/SIMD, LDS allows it): 16 cells per tile, 1279 -> 1245 ms (r2t A/B)
+#define IS3D_KTILE_MOD 8    // modified path: 8 cells per tile since it runs 3 waves/SIMD (3 workgroups' LDS per CU;
+                            // 16 paid at 2 waves: 1279 -> 1245 ms, r2t A/B)
 #endif
 // cells per k_spectra tile of one delta-f mode and launch (8 for Grad / RTA-CE: 16 costs them 18% / 11%,
 // r2t; the modified path's F_T8 and F_LY launches keep 8 where 16 cells' q-row tables would not fit:
 // config 1's shape in F_LY ran 11.2 ms with 8-cell tiles, 13.6 ms with 16)
 template <int MODE, int FLAGS>
-constexpr int spectra_tile() { return (MODE >= PTM && !(FLAGS & (16 | 8))) ? IS3D_KTILE_MOD : kTile; }
+constexpr int spectra_tile() { return (MODE >= PTM && !(FLAGS & (32 | 16 | 8))) ? IS3D_KTILE_MOD : kTile; }
 // waves per SIMD the spectra kernel is register-allocated for (measured on MI355X, config2):
 // Grad and RTA-CE run best at 3 (168 VGPRs), the modified-momentum modes at 2
 #ifndef IS3D_SPECTRA_WAVES_SEP
 #define IS3D_SPECTRA_WAVES_SEP 3
 #endif
 #ifndef IS3D_SPECTRA_WAVES_MOD
-#define IS3D_SPECTRA_WAVES_MOD 2
+#define IS3D_SPECTRA_WAVES_MOD 3   // without the separable code (F_FB launch): 164 VGPRs; config2 PTM 1242 -> 1044 ms (r3 A/B)
 #endif
 #ifndef IS3D_SPECTRA_WAVES_CE
 #define IS3D_SPECTRA_WAVES_CE 3      // RTA-CE: 3 (16 spilled VGPRs, 3 scratch accesses per 32 points) beat 2 by 4.3% once
@@ -45,9 +46,13 @@ constexpr int spectra_waves() {
 #endif
 template <int MODE, int KJ>
 constexpr int spectra_waves_kj() { return (KJ == 16 && MODE == GRAD) ? IS3D_SPECTRA_WAVES_KJ16 : spectra_waves<MODE>(); }
-// k_dndx keeps RTA-CE at 2 (its pT loop holds more live state: 215 VGPRs)
+// the F_FB launch (separable lanes of a modified mode: per-point exp, RTA-CE-like lane setup) stays at 2
+template <int MODE, int FLAGS, int KJ>
+constexpr int spectra_waves_f() { return (MODE >= PTM && (FLAGS & 32)) ? 2 : spectra_waves_kj<MODE, KJ>(); }
+// k_dndx keeps RTA-CE and the modified modes at 2 (its pT loop holds more live state: 215 VGPRs; it keeps
+// the separable fallback inline)
 template <int MODE>
-constexpr int dndx_waves() { return MODE == CE ? 2 : spectra_waves<MODE>(); }
+constexpr int dndx_waves() { return (MODE == CE || MODE >= PTM) ? 2 : spectra_waves<MODE>(); }
 
 // LDS row stride of the y-terms (doubles): NYT + 1 is odd, so the 8-byte stores of one y-term field
 // by consecutive lanes (rows 136 B apart) spread over the 64 banks instead of hitting two of them
@@ -72,6 +77,8 @@ struct SpecArgs {
   long sstride;               // doubles per slab: npT * nbx * KJ * kBlock
   int regulate, outflow, dim;
   int op;                     // 1 spectra / 0 spacetime (yterms variants)
+  const int* fbcells;         // F_FB launch: ascending indices of the cells with separable-fallback lanes
+  const int* fbcount;         //   (k_fbscan, device-side) and their number
 };
 
 // flag bits of the spectra kernel instantiation
@@ -80,7 +87,11 @@ struct SpecArgs {
 // F_LY (grids whose q rows do not fit in LDS: large y / eta tables with few species, KJ = 8 only): every
 // lane builds its own y-term row in LDS and the modified lanes use their linear forms, no q-row tables
 // F_T8 (modified path): 8-cell tiles instead of IS3D_KTILE_MOD (q-row tables of many rows, config 1's shape)
-constexpr int F_REG = 1, F_OUT = 2, F_TB = 4, F_LY = 8, F_T8 = 16;
+// F_FB (modified path): the separable-fallback launch -- only the lanes the modified launch leaves out (breakdown
+// cells, narrow rapidity windows), over the cells listed by k_fbscan, per-lane y-term rows as F_LY.  Keeping
+// the separable code out of the modified launch takes its k_spectra from 241 to 164 VGPRs (3 waves per SIMD
+// instead of 2) and removes the 32-64 v_mov_b64 per lane and cell that merged two register assignments of acc
+constexpr int F_REG = 1, F_OUT = 2, F_TB = 4, F_LY = 8, F_T8 = 16, F_FB = 32;
 constexpr int kTbQ = 4;
 
 #ifndef IS3D_SPLIT_BYTES
@@ -91,6 +102,10 @@ constexpr int kTbQ = 4;
 #endif
 #ifndef IS3D_QUAD_RCP
 #define IS3D_QUAD_RCP 1       // fast path: four phi points per reciprocal where sep_quads() says so
+#endif
+#ifndef IS3D_MOD_PF
+#define IS3D_MOD_PF 0         // modified table fours: one-quad-ahead prefetch of the {PDm, Qv} / T2 rows (helped at
+                              // 2 waves/SIMD; at 3 it does not fit the 168-VGPR budget)
 #endif
 #ifndef IS3D_MOD_QUAD
 #define IS3D_MOD_QUAD 1       // modified path: four phi points per reciprocal when KJ % 4 == 0
@@ -153,8 +168,8 @@ void launch_dndx(dim3 grid, size_t shmem, hipStream_t st, const DndxArgs& a, int
 namespace {
 // 32 phi points of one lane; the next points' LDS pairs are loaded before the current ones are
 // evaluated so the LDS latency overlaps the FP64 chain
-template <int MODE, int FLAGS, bool FAST, int KJ>
-__device__ __forceinline__ void sep_phi_loop(const SepLane& L, const dbl2* CS, const dbl2* BP, double* acc) {
+template <int MODE, int FLAGS, bool FAST, int KJ, typename ACC>
+__device__ __forceinline__ void sep_phi_loop(const SepLane& L, const dbl2* CS, const dbl2* BP, ACC acc) {
   constexpr int FL = (MODE == GRAD) ? SEP_GRAD : (MODE == CE || MODE == PTM) ? SEP_CE : (MODE == PTB) ? SEP_PTB : SEP_FEQ;
   constexpr bool REG = (FLAGS & F_REG) != 0, OUT = (FLAGS & F_OUT) != 0;
   if (FAST && IS3D_QUAD_RCP && ((IS3D_NOPF_MODES >> MODE) & 1) && sep_quads(MODE, KJ)) {
@@ -319,9 +334,14 @@ __device__ __forceinline__ void sep_phi_loop_pd_tail(const SepLane& L, CSP CS, c
 }
 
 // modified lanes of k_spectra, table form: {PDm, Qv} (MW) and T2 (MT) rows, four points per reciprocal
-template <int FLAGS, bool CLAMP, int KJ>
-__device__ __forceinline__ void mod_phi_loop_tab(const ModLane& M, const dbl2* MW, const double* MT, double* acc) {
+template <int FLAGS, bool CLAMP, int KJ, typename ACC>
+__device__ __forceinline__ void mod_phi_loop_tab(const ModLane& M, const dbl2* MW, const double* MT, ACC acc) {
   constexpr bool OUT = (FLAGS & F_OUT) != 0;
+  if (IS3D_MOD_QUAD && !IS3D_MOD_PF && KJ % 4 == 0) {
+#pragma unroll
+    for (int jj = 0; jj < KJ; jj += 4) mod_quad_tab_t<OUT, CLAMP>(M, MW + jj, MT + jj, acc + jj);
+    return;
+  }
   if (IS3D_MOD_QUAD && KJ % 4 == 0) {
     // the next four points' table rows are loaded before the current four are evaluated (at 2 waves per
     // SIMD the LDS latency is not hidden by other waves)
@@ -332,15 +352,15 @@ __device__ __forceinline__ void mod_phi_loop_tab(const ModLane& M, const dbl2* M
 #pragma unroll
     for (int jj = 0; jj < KJ; jj += 4) {
       dbl2 nw[4];
-      double nt[4], v[4];
+      double nt[4];
 #pragma unroll
       for (int i = 0; i < 4; i++) {
         nw[i] = mw[i]; nt[i] = mt[i];
         if (jj + 4 < KJ) { nw[i] = MW[jj + 4 + i]; nt[i] = MT[jj + 4 + i]; }
       }
-      mod_quad_tab_t<OUT, CLAMP>(M, mw, mt, v);
+      mod_quad_tab_t<OUT, CLAMP>(M, mw, mt, acc + jj);
 #pragma unroll
-      for (int i = 0; i < 4; i++) { acc[jj + i] += v[i]; mw[i] = nw[i]; mt[i] = nt[i]; }
+      for (int i = 0; i < 4; i++) { mw[i] = nw[i]; mt[i] = nt[i]; }
     }
     return;
   }
@@ -354,8 +374,8 @@ __device__ __forceinline__ void mod_phi_loop_tab(const ModLane& M, const dbl2* M
 
 // modified lanes without q-row tables (lane_y launches): {pc, ps} and the {PDm, Qv} rows, the lane's
 // linear forms for E_mod^2 and p.dsigma (mod_quad_lane_t), pairs of points per reciprocal
-template <int FLAGS, bool CLAMP, int KJ>
-__device__ __forceinline__ void mod_phi_loop_lane(const ModLane& M, const dbl2* CS, const dbl2* MW, double* acc) {
+template <int FLAGS, bool CLAMP, int KJ, typename ACC>
+__device__ __forceinline__ void mod_phi_loop_lane(const ModLane& M, const dbl2* CS, const dbl2* MW, ACC acc) {
   constexpr bool OUT = (FLAGS & F_OUT) != 0;
 #pragma unroll
   for (int jj = 0; jj < KJ; jj += 2) {
@@ -415,16 +435,19 @@ __device__ __forceinline__ void lds_barrier() {
 // Async copy of the record tile starting at cell cb into LDS (global_load_lds_dwordx4: no VGPR
 // staging; the LDS destination of a wave-instruction is base + 16 * lane, so the tile lands
 // in the same linear order as the records in HBM).  Completion is tracked by vmcnt.
+// With an index list (F_FB) tile slot k holds the record of cell idx[cb + k]: each lane names its own
+// source pair, so the same LDS-DMA instruction gathers.
 template <int KT>
-__device__ __forceinline__ void fetch_tile(const double* rec, long cb, long c_end, double* dst) {
+__device__ __forceinline__ void fetch_tile(const double* rec, long cb, long c_end, double* dst, const int* idx = nullptr) {
   constexpr int kTilePairs = KT * NREC / 2;   // dbl2 pairs of one record tile (KT records of NREC doubles)
   const int tid = threadIdx.x;
   const long lim = (min(c_end, cb + KT) - cb) * (NREC / 2);
   for (int base = 0; base < kTilePairs; base += kBlock) {
     const int e = base + tid;
     const int wave0 = base + (tid & ~63);
+    const long src = idx ? ((long)idx[cb + e / (NREC / 2)] * (NREC / 2) + e % (NREC / 2)) : cb * (NREC / 2) + e;
     if (e < lim)
-      __builtin_amdgcn_global_load_lds((const void*)(rec + (cb * (NREC / 2) + e) * 2),
+      __builtin_amdgcn_global_load_lds((const void*)(rec + src * 2),
                                        (__attribute__((address_space(3))) void*)(dst + 2 * wave0), 16, 0, 0);
   }
 }
@@ -435,12 +458,14 @@ __device__ __forceinline__ void wait_fetch() { asm volatile("s_waitcnt vmcnt(0)"
 // (species, q, phi block) with q = (y, eta node): in 2+1D the eta nodes are spread over lanes and
 // summed by k_reduce, so a few species still fill the wavefronts
 template <int MODE, int FLAGS, int KJ>
-__global__ __launch_bounds__(kBlock, (spectra_waves_kj<MODE, KJ>())) void k_spectra(SpecArgs A) {
+__global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void k_spectra(SpecArgs A) {
   constexpr int kTile = spectra_tile<MODE, FLAGS>();      // cells per LDS tile for this mode / launch
   extern __shared__ double smem[];
   const int nphp = A.njb * KJ;                            // phi rows padded to KJ multiples
   constexpr bool TB = (MODE == GRAD || MODE == CE) && (FLAGS & F_TB) != 0 && KJ % 4 == 0;
-  constexpr bool LY = (FLAGS & F_LY) != 0;
+  constexpr bool FB = MODE >= PTM && (FLAGS & F_FB) != 0;   // separable-fallback launch of a modified mode
+  constexpr bool MODMAIN = MODE >= PTM && !FB;              // modified launch: separable lanes left to F_FB
+  constexpr bool LY = (FLAGS & F_LY) != 0 || FB;
   // per-(cell, q, phi) tables built from the per-tile tables (phase C below): Grad / RTA-CE {PD, T1},
   // modified path T2
   constexpr bool HAS_C = TB || (MODE >= PTM && !LY);
@@ -448,7 +473,7 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_kj<MODE, KJ>())) void k_spec
   // double-buffered.  Only the launches whose tables are small (F_TB: <= kTbQ rows per cell; the modified
   // path's 16-cell tiles, which fall back to F_T8 when they do not fit): double y-term rows of many q
   // values would cost a workgroup per CU (config 1's shape: 4.8 -> 5.7 ms, r2z)
-  constexpr bool PIPE = IS3D_PIPE && (TB || (MODE >= PTM && !(FLAGS & (F_LY | F_T8))));
+  constexpr bool PIPE = IS3D_PIPE && (TB || (MODE >= PTM && !(FLAGS & (F_LY | F_T8 | F_FB))));
   constexpr int kRecBufs = PIPE ? 3 : 2, kTabBufs = PIPE ? 2 : 1;
   constexpr int kQvF = (MODE >= PTM || !PIPE) ? 2 : 1;    // doubles per (cell, phi) of s_qv
   const int nqm = A.nqmax;                                // rows per cell (>= every workgroup's nqw)
@@ -509,6 +534,9 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_kj<MODE, KJ>())) void k_spec
     nqw = (int)(t1 / A.npart - r0) + 1;
   }
   const int row = active ? (int)(task / A.npart - r0) : 0;
+  // the LDS row tables are sized for nqmax rows (host, spectra_plan): a launch whose workgroup spans more
+  // would write past them, so it computes nothing and returns NaN spectra instead (never on a host plan)
+  const bool rows_ok = LY || nqw <= A.nqmax;
   // y-term rows: per row, or per q when the rows cover every q (several phi blocks, few species: the
   // y-terms depend on q only)
   const bool allq = nqw >= A.nq;
@@ -537,8 +565,19 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_kj<MODE, KJ>())) void k_spec
 #pragma unroll
   for (int jj = 0; jj < KJ; jj++) acc[jj] = 0.0;
 
-  const long c_begin = (long)split * A.cells_per_split;
-  const long c_end = min(A.n, c_begin + A.cells_per_split);
+  // F_FB: positions in the fallback cell list (its length is known on the device only), split evenly
+  long c_begin, c_end;
+  if constexpr (FB) {
+    const long nfb = *A.fbcount, cps = ((nfb + A.nsplit - 1) / A.nsplit + kTile - 1) / kTile * kTile;
+    c_begin = (long)split * cps;
+    c_end = min(nfb, c_begin + cps);
+  } else {
+    c_begin = (long)split * A.cells_per_split;
+    c_end = min(A.n, c_begin + A.cells_per_split);
+  }
+  const int* const fbl = FB ? A.fbcells : nullptr;
+  // this thread's slab entries, layout [split][pT][lane group][phi slot][lane] (see the stores at the end)
+  double* const out = A.slab + (long)split * A.sstride + ((long)ipt * A.nbx + lane_group) * (KJ * kBlock) + tid;
 
   // ---- phase A / B of one tile (records s_rec, ntx cells) into table buffer tb: {b', Phi} and PD (or
   // the modified path's {PDm, Qv}) per (cell, phi), {TE, T2} for RTA-CE's table launch, y-terms per
@@ -624,11 +663,11 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_kj<MODE, KJ>())) void k_spec
   // so the y-term wave's work and the tables of tile i + 1 overlap other waves' lane work of tile i instead
   // of idling every wave at a barrier, and each record copy has a full tile of lead time.
   // otherwise: two record buffers, one table buffer, A / B -> barrier -> C -> barrier -> lanes.
-  const int ntiles = (c_begin < c_end) ? (int)((c_end - c_begin + kTile - 1) / kTile) : 0;
+  const int ntiles = (rows_ok && c_begin < c_end) ? (int)((c_end - c_begin + kTile - 1) / kTile) : 0;
   auto tile_cb = [&](int i) { return c_begin + (long)i * kTile; };
   auto tile_nt = [&](int i) { return (int)min((long)kTile, c_end - tile_cb(i)); };
   auto recbuf = [&](int i) { return s_recb + (i % kRecBufs) * recsz; };
-  for (int i = 0; i < min(ntiles, kRecBufs - 1); i++) fetch_tile<kTile>(A.rec, tile_cb(i), c_end, recbuf(i));
+  for (int i = 0; i < min(ntiles, kRecBufs - 1); i++) fetch_tile<kTile>(A.rec, tile_cb(i), c_end, recbuf(i), fbl);
   if (PIPE && ntiles > 0) {
     wait_fetch();
     lds_barrier();     // tiles 0 and 1, the trig / grid / exp tables visible
@@ -641,7 +680,7 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_kj<MODE, KJ>())) void k_spec
     wait_fetch();
     lds_barrier();     // X: this tile's records (and, pipelined, its A / B tables) visible; the last tile is done
     if (i + kRecBufs - 1 < ntiles)
-      fetch_tile<kTile>(A.rec, tile_cb(i + kRecBufs - 1), c_end, recbuf(i + kRecBufs - 1));
+      fetch_tile<kTile>(A.rec, tile_cb(i + kRecBufs - 1), c_end, recbuf(i + kRecBufs - 1), fbl);
     if (!PIPE) {
       tables_ab(s_rec, ntx, 0);
       lds_barrier();
@@ -664,7 +703,7 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_kj<MODE, KJ>())) void k_spec
         if (kind == 0.0) continue;
         double rn_abs = R[R_RENORM];
         if (MODE == PTM || MODE == PTB) {
-          const double rn = (MODE == PTM) ? A.renorm[(cbx + t) * A.npart + s] : R[R_RENORM];
+          const double rn = (MODE == PTM) ? A.renorm[(FB ? (long)fbl[cbx + t] : cbx + t) * A.npart + s] : R[R_RENORM];
           if (!isfinite(rn)) continue;    // species skipped (MomentumSpectra.cpp:828-832)
           rn_abs = fabs(rn);
         }
@@ -677,7 +716,11 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_kj<MODE, KJ>())) void k_spec
           Y = Yl;
         }
         const bool sep = (MODE <= CE) || kind == 1.0 || Y[Y_NARROW] != 0.0;
-        if (sep) {
+        // the modified launch leaves its separable lanes to the F_FB launch and vice versa (if constexpr:
+        // neither kernel carries the other's code)
+        if (MODMAIN && sep) continue;
+        if (FB && !sep) continue;
+        if constexpr (!MODMAIN) {     // Grad / RTA-CE lanes (sep throughout), the F_FB launch's separable lanes
           SepLane L;
           sep_setup(sep_flavor(MODE), R, Y, mT, mT2, m2, mTb, pT, sign, baryon, s_etab, L,
                     TB && IS3D_TAIL && (MODE == GRAD || IS3D_TAIL_CE));
@@ -700,7 +743,8 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_kj<MODE, KJ>())) void k_spec
             sep_phi_loop_pd<MODE, FLAGS, KJ, true>(L, s_cs + j0, BP, qvt + t * nphp + j0, acc);
           else if (L.fast) sep_phi_loop<MODE, FLAGS, true, KJ>(L, s_cs + j0, BP, acc);
           else sep_phi_loop<MODE, FLAGS, false, KJ>(L, s_cs + j0, BP, acc);
-        } else if (MODE >= PTM) {
+        }
+        if constexpr (MODMAIN) {
           ModLane M;
           mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, s_etab, M);
           if (M.skip) continue;
@@ -720,9 +764,8 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_kj<MODE, KJ>())) void k_spec
   // partial sums, slab layout [split][pT][lane group][phi slot][lane]: every store of the wave is
   // one contiguous 512-byte row; non-temporal so the stream does not evict the cell records the
   // XCD's other workgroups are still reading from L2.  k_reduce scatters into the reference layout.
-  double* out = A.slab + (long)split * A.sstride + ((long)ipt * A.nbx + lane_group) * (KJ * kBlock) + tid;
 #pragma unroll
-  for (int jj = 0; jj < KJ; jj++) __builtin_nontemporal_store(acc[jj], out + jj * kBlock);
+  for (int jj = 0; jj < KJ; jj++) __builtin_nontemporal_store(rows_ok ? acc[jj] : __builtin_nan(""), out + jj * kBlock);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -926,6 +969,15 @@ __global__ __launch_bounds__(kBlock, dndx_waves<MODE>()) void k_dndx(DndxArgs A)
 template <int MODE, int KJ>
 void launch_spectra_kj(dim3 grid, size_t shmem, hipStream_t st, const SpecArgs& a, int flags) {
   if constexpr (MODE >= PTM) {
+    if (flags & F_FB) {
+      switch (flags & 3) {
+        case 0: hipLaunchKernelGGL((k_spectra<MODE, 32, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+        case 1: hipLaunchKernelGGL((k_spectra<MODE, 33, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+        case 2: hipLaunchKernelGGL((k_spectra<MODE, 34, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+        default: hipLaunchKernelGGL((k_spectra<MODE, 35, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+      }
+      return;
+    }
     if (flags & F_T8) {
       switch (flags & 3) {
         case 0: hipLaunchKernelGGL((k_spectra<MODE, 16, KJ>), grid, dim3(kBlock), shmem, st, a); break;

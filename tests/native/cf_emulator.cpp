@@ -62,7 +62,7 @@ struct EmuTables {
 // (sum over pT, phi, y of w_pT w_phi (w_eta p.dsigma f) x prefactor g, as k_dndx)
 // variant bits (k_spectra's launch variants, checked on the CPU): 1 = the F_TB table algebra for Grad /
 // RTA-CE fast lanes without baryon terms (sep_quad_tb_t, phi counts that are multiples of 4), 2 = the
-// Boltzmann-tail lanes (sep_setup allow_tail + sep_quad_tb_tail_t under bit 1; mod_quad_tail_t),
+// Boltzmann-tail lanes (sep_setup allow_tail + sep_quad_tb_tail_t under bit 1),
 // 4 = the modified path's table form (mod_quad_tab_t / mod_pair_tab_t)
 extern "C" int emu_spectra_v(const orc_params* p, const orc_setup* su, const orc_surface* S, int chains, int op,
                              double* out, long* stats, int variant) {
@@ -244,10 +244,8 @@ extern "C" int emu_spectra_v(const orc_params* p, const orc_setup* su, const orc
                 const bool of = p->outflow != 0;
                 if (spectra_kj(nphi) % 4 == 0)
                   for (; j + 3 < nphi; j += 4) {
-                    double v[4];
-                    if (M.clamp) { if (of) mod_quad_tab_t<true, true>(M, &MW[j], &MT[j], v); else mod_quad_tab_t<false, true>(M, &MW[j], &MT[j], v); }
-                    else { if (of) mod_quad_tab_t<true, false>(M, &MW[j], &MT[j], v); else mod_quad_tab_t<false, false>(M, &MW[j], &MT[j], v); }
-                    for (int i = 0; i < 4; i++) a[j + i] += v[i];
+                    if (M.clamp) { if (of) mod_quad_tab_t<true, true>(M, &MW[j], &MT[j], &a[j]); else mod_quad_tab_t<false, true>(M, &MW[j], &MT[j], &a[j]); }
+                    else { if (of) mod_quad_tab_t<true, false>(M, &MW[j], &MT[j], &a[j]); else mod_quad_tab_t<false, false>(M, &MW[j], &MT[j], &a[j]); }
                   }
                 for (; j + 1 < nphi; j += 2) {
                   double v0, v1;
@@ -266,12 +264,6 @@ extern "C" int emu_spectra_v(const orc_params* p, const orc_setup* su, const orc
                   j++;
                 }
               }
-              if (tail && M.tail && spectra_kj(nphi) % 4 == 0)     // k_spectra's tail fours
-                for (; j + 3 < nphi; j += 4) {
-                  dbl2 qa, qb; qa.x = QV[j]; qa.y = QV[j + 1]; qb.x = QV[j + 2]; qb.y = QV[j + 3];
-                  if (p->outflow) mod_quad_tail_t<true>(M, &CS[j], qa, qb, &a[j]);
-                  else mod_quad_tail_t<false>(M, &CS[j], qa, qb, &a[j]);
-                }
               if (op != 0 && spectra_kj(nphi) % 4 == 0)       // k_spectra's fours; k_dndx pairs
                 for (; j + 3 < nphi; j += 4) {
                   double v[4];

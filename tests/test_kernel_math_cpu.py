@@ -130,13 +130,16 @@ def test_table_and_tail_algebra(dim, mode, reg_out):
         assert not np.array_equal(got, base)       # the variant's arithmetic really ran
 
 
-@pytest.mark.parametrize("mode", [3, 4, 5])
-def test_modified_tail_lanes(mode):
-    """mod_quad_tail_t (f = |renorm| en where 1 + sign en == 1) against the oracle on the config-2 grid."""
-    s = synth.as_read(synth.surface(6, seed=23, dimension=3, full3d=True))
-    spec = make_spec(hrg_eos=2, chosen="smash", df_mode=mode, dimension=3, pT="pT24", phi="phi32", famod_chains=1)
+@pytest.mark.parametrize("mode,baryon", [(3, 0), (4, 0), (5, 0), (3, 1), (5, 1)])
+def test_modified_table_lanes(mode, baryon):
+    """k_spectra's modified-path table lanes (variant 4: mod_quad_tab_t in exp-table units -- e^(-E_mod/T_mod)
+    with e^chem folded into the lane's sign and p.dsigma coefficients, four points per reciprocal
+    accumulated by FMA) against the oracle on the config-2 grid, with baryon chemistry (chem != 0) on."""
+    s = synth.as_read(synth.surface(6, seed=23, dimension=3, full3d=True, baryon=bool(baryon)))
+    spec = make_spec(hrg_eos=2, chosen="smash", df_mode=mode, dimension=3, pT="pT24", phi="phi32", famod_chains=1,
+                     include_baryon=baryon)
     ref = O.spectra(spec, s, threads=1)
-    got, _ = emu_spectra(spec, s, chains=1, variant=2)
+    got, _ = emu_spectra(spec, s, chains=1, variant=4)
     rel, zr, zg = parity(got, ref, floor=1e-290)
     assert rel < 1e-8, rel
     assert zr == zg
