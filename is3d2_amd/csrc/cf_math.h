@@ -201,7 +201,17 @@ static constexpr double kInvLn2x256 = 369.3299304675746;   // 256 / ln2
 #ifndef IS3D_EXP_TAB_BITS
 #define IS3D_EXP_TAB_BITS 8
 #endif
-#if IS3D_EXP_TAB_BITS == 8
+#if IS3D_EXP_TAB_BITS == 10
+// 1024-entry table (8 KB of LDS), |c rs| <= ln2/2048, degree-3 Taylor (truncation 5.5e-16, ~2.5 ulp):
+// one FMA fewer per exp than the 256-entry table
+}  // namespace is3d
+#include "exp2_tab1024.h"
+namespace is3d {
+static constexpr int kExpTabN = 1024, kExpTabDeg = 3;
+#define kExp2Tab kExp2Tab1024
+#define kExpTabCoefs kExpTabA1024
+static constexpr double kInvLn2xN = kInvLn2x1024;
+#elif IS3D_EXP_TAB_BITS == 8
 static constexpr int kExpTabN = 256, kExpTabDeg = 4;
 #define kExp2Tab kExp2Tab256
 #define kExpTabCoefs kExpTabA256
@@ -314,9 +324,9 @@ static_assert(NREC % 2 == 0, "records are moved as 16-byte pairs: keep NREC even
 // y-term layout (per cell, q); phi-terms are dbl2 pairs, see phiterms
 // Y_AT = A/T, Y_A = A (u.p = mT A - pT B), Y_D (p.dsigma = mT D + ...), Y_WDX/Y_WDY = w_eta dsigma_{x,y};
 // Y_S2, Y_S1, Y_SC1, Y_SS1, Y_L1: the (cell, y) factors of the separable lane coefficients
-// (sep_setup); Y_MUX..Y_MD, Y_NARROW: modified-momentum path.  Padded to 16 doubles.
+// (sep_setup); Y_MUX..Y_MD, Y_NARROW, Y_MU2 = |sig U|^2, Y_MU = |sig U|: modified-momentum path.
 enum YT : int { Y_AT = 0, Y_A, Y_D, Y_WDX, Y_WDY, Y_S2, Y_S1, Y_SC1, Y_SS1, Y_L1,
-                Y_MUX, Y_MUY, Y_MUZ, Y_MD, Y_NARROW, Y_W, NYT };
+                Y_MUX, Y_MUY, Y_MUZ, Y_MD, Y_NARROW, Y_W, Y_MU2, Y_MU, NYT };
 
 // surface field order (include/is3d_amd.h, is3d_surface)
 enum Surf : int {
@@ -1051,8 +1061,12 @@ IS3D_HD void yterms(int mode, int op, const double* R, double y, double eta, dou
     Y[Y_MUZ] = chm * R[R_UCZ] + shm * R[R_USZ];
     Y[Y_MD] = quirk ? (w * chm * R[R_DAT] + shm * R[R_DANT]) : w * (chm * R[R_DAT] + shm * R[R_DANT]);
     Y[Y_NARROW] = (R[R_NARROW] != 0.0 && fabs(y - eta) < R[R_DET]) ? 1.0 : 0.0;
+    // |sig U|^2 and |sig U| once per (cell, q) instead of once per (cell, lane) in mod_setup
+    const double ux = Y[Y_MUX], uy = Y[Y_MUY], uz = Y[Y_MUZ];
+    Y[Y_MU2] = fma(ux, ux, fma(uy, uy, uz * uz));
+    Y[Y_MU] = sqrt(Y[Y_MU2]);
   } else {
-    Y[Y_MUX] = Y[Y_MUY] = Y[Y_MUZ] = Y[Y_MD] = Y[Y_NARROW] = 0.0;
+    Y[Y_MUX] = Y[Y_MUY] = Y[Y_MUZ] = Y[Y_MD] = Y[Y_NARROW] = Y[Y_MU2] = Y[Y_MU] = 0.0;
   }
   Y[Y_W] = w;                      // w_eta (PD-table scale, sep_setup)
 }
@@ -1587,11 +1601,14 @@ static constexpr double kModTabX = 1.0e6, kModTabChem = 30.0;
 #ifndef IS3D_MODQ_ACC
 #define IS3D_MODQ_ACC 1
 #endif
+#ifndef IS3D_MOD_SQ_BOUNDS
+#define IS3D_MOD_SQ_BOUNDS 1
+#endif
 
 IS3D_HD void mod_setup(const double* R, const double* Y, double mT, double m2, double pT, double sign, double baryon,
                        double renorm_abs, const double* etab, ModLane& L) {
   const double ux = Y[Y_MUX], uy = Y[Y_MUY], uz = Y[Y_MUZ];   // sig U
-  const double u2 = fma(ux, ux, fma(uy, uy, uz * uz));
+  const double u2 = Y[Y_MU2];
   const double sig = R[R_INVTM] * kInvLn2xN, m2s = m2 * (sig * sig);
   L.E0 = fma(mT * mT, u2, m2s);
   const double tm = 2.0 * mT;
@@ -1604,12 +1621,20 @@ IS3D_HD void mod_setup(const double* R, const double* Y, double mT, double m2, d
   // | |mT U| - pT |V|max | <= |p_mod| <= |mT U| + pT |V|max (sig units): if even the smallest E_mod
   // overflows exp, every phi point is exactly 0; if the largest could leave the table lanes' domain
   // the lane takes the clamped exp
-  const double mu = mT * sqrt(u2);
+  const double mu = mT * Y[Y_MU];
   const double lo = mu - pT * R[R_VB], hi = mu + pT * R[R_VB];
+#if IS3D_MOD_SQ_BOUNDS
+  // the same two tests on squares (no sqrt): skip when sig E_min (1 - 1e-12) exceeds
+  // thr = (kExpMax + 1 + chem) N/ln2 -- always when thr < 0, as E_min >= 0
+  const double thr = (kExpMax + 1.0 + L.chemm) * kInvLn2xN, xm = kModTabX * kInvLn2xN;
+  L.skip = (thr < 0.0 || (lo > 0.0 && (m2s + lo * lo) * (1.0 - 2e-12) > thr * thr)) ? 1 : 0;
+  L.clamp = ((m2s + hi * hi) < xm * xm && fabs(L.chemm) < kModTabChem) ? 0 : 1;
+#else
   const double emin = (lo > 0.0) ? sqrt(m2s + lo * lo) * (1.0 - 1e-12) : 0.0;
   L.skip = (emin * kLn2overN - L.chemm > kExpMax + 1.0) ? 1 : 0;
   const double emax = sqrt(m2s + hi * hi) * kLn2overN;
   L.clamp = (emax < kModTabX && fabs(L.chemm) < kModTabChem) ? 0 : 1;
+#endif
   // e^chem of the table lanes (1 for mesons and without baryon chemistry: a wave-uniform skip there)
   double ec = 1.0;
   if (!L.clamp && L.chemm != 0.0) ec = exp_tab(L.et, etab, L.chemm * kInvLn2xN);
@@ -1696,16 +1721,58 @@ IS3D_HD double mod_en_x(const ModLane& L, double X) {
   return exp_tab_fma(L.et, L.etab, -g, v);
 }
 
+// mod_en_x for four points in stages: the four range reductions, then the four table reads issued
+// together, then the four polynomials (independent of the reads), then the products -- so one LDS
+// latency is waited for per four points instead of per one or two (same operations, same results)
+#ifndef IS3D_MOD_STAGED
+#define IS3D_MOD_STAGED 1
+#endif
+template <bool CLAMP>
+IS3D_HD void mod_en4(const ModLane& L, const double* X, double* en) {
+  if (CLAMP || !IS3D_MOD_STAGED) {
+#pragma unroll
+    for (int i = 0; i < 4; i++) en[i] = mod_en_x<CLAMP>(L, X[i]);
+    return;
+  }
+  const ExpTabCoef& E = L.et;
+  double t[4], rs[4], T[4], p[4];
+  int ki[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double y = __builtin_amdgcn_rsq(X[i]);
+#else
+    const double y = 1.0 / sqrt(X[i]);
+#endif
+    const double g = X[i] * y;
+    const double v = fma(-0.5, g * y, 1.5);
+    t[i] = fma(-g, v, E.shift);
+    rs[i] = fma(-g, v, E.shift - t[i]);
+    ki[i] = (int)(unsigned)__builtin_bit_cast(unsigned long long, t[i]);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++) T[i] = L.etab[ki[i] & (kExpTabN - 1)];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    double q = E.a[kExpTabDeg - 1];
+#pragma unroll
+    for (int k = kExpTabDeg - 2; k >= 0; k--) q = fma(q, rs[i], E.a[k]);
+    p[i] = rs[i] * q;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; i++) en[i] = ldexp(fma(T[i], p[i], T[i]), ki[i] >> IS3D_EXP_TAB_BITS);
+}
+
 // four points, one reciprocal, accumulated into acc: f_i = en_i / q_i = en_i q_j (1 / q_i q_j) with j the
 // pair partner, so acc_i = fma(pds_i en_i q_j, r_ij, acc_i) -- 4 ops per point after the shared reciprocal
 template <bool OUT, bool CLAMP, typename ACC>
 IS3D_HD void mod_quad_tab_t(const ModLane& L, const dbl2* mw, const double* mt, ACC acc) {
-  double en[4], q[4];
+  double en[4], q[4], X[4];
 #pragma unroll
-  for (int i = 0; i < 4; i++) {
-    en[i] = mod_en_x<CLAMP>(L, fma(L.mT, mt[i], L.E0 + mw[i].y));
-    q[i] = fma(L.sign, en[i], 1.0);
-  }
+  for (int i = 0; i < 4; i++) X[i] = fma(L.mT, mt[i], L.E0 + mw[i].y);
+  mod_en4<CLAMP>(L, X, en);
+#pragma unroll
+  for (int i = 0; i < 4; i++) q[i] = fma(L.sign, en[i], 1.0);
   const double q01 = q[0] * q[1], q23 = q[2] * q[3];
   const double r = rcp1(q01 * q23);
 #if IS3D_MODQ_ACC

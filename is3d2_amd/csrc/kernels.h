@@ -54,10 +54,10 @@ constexpr int spectra_waves_f() { return (MODE >= PTM && (FLAGS & 32)) ? 2 : spe
 template <int MODE>
 constexpr int dndx_waves() { return (MODE == CE || MODE >= PTM) ? 2 : spectra_waves<MODE>(); }
 
-// LDS row stride of the y-terms (doubles): NYT + 1 is odd, so the 8-byte stores of one y-term field
-// by consecutive lanes (rows 136 B apart) spread over the 64 banks instead of hitting two of them
+// LDS row stride of the y-terms (doubles): NYT | 1 is odd, so the 8-byte stores of one y-term field
+// by consecutive lanes (rows 152 B apart) spread over the 64 banks instead of hitting two of them
 // (a 128-B stride put every lane of a wave on the same bank pair: a 32-way conflict)
-constexpr int kYRow = NYT + 1;
+constexpr int kYRow = NYT | 1;
 
 // ------------------------------------------------------------------------------------------
 // spectra kernel
@@ -481,7 +481,10 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
   // y-term rows per cell: per row, or per q once the rows cover every q (nyr below): min(nqm, nq);
   // LY launches: one y-term row per lane instead ([kBlock][kYRow], single; odd row stride: no conflicts)
   const long ysz = (LY ? (long)kBlock : (long)kTile * min(nqm, A.nq)) * kYRow;
-  double* s_recb = smem;                                  // [kRecBufs][kTile][NREC]
+  // the exp table first: at LDS offset 0 its address is the table index alone (no base register, which
+  // the modified loop otherwise re-read from an SGPR spill lane at every point)
+  double* s_etab = smem;                                  // [kExpTabN] 2^(j/kExpTabN)
+  double* s_recb = smem + kExpTabN;                       // [kRecBufs][kTile][NREC]
   dbl2* s_trig = (dbl2*)(s_recb + kRecBufs * recsz);      // [nphp]        {cos, sin}
   dbl2* s_cs = s_trig + nphp;                             // [nphp]        {pT cos, pT sin}
   dbl2* s_bp = s_cs + nphp;                               // [kTabBufs][kTile][nphp] {b', Phi}
@@ -489,10 +492,9 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
   double* s_qv = (double*)(s_bp + kTabBufs * bpsz);
   double* s_grid = s_qv + kTabBufs * qvsz;                // y[nk] | eta[nl] | eta_w[nl]
   double* s_y = s_grid + A.nk + 2 * A.nl;                 // [kTabBufs (LY: 1)][kTile][min(nqm, nq)][kYRow]
-  double* s_etab = s_y + (LY ? 1 : kTabBufs) * ysz;       // [kExpTabN] 2^(j/kExpTabN)
   // TB: [kTile][nqm][prow] {PD, T1}, 16-byte aligned for ds_read_b128 (s_grid's nk + 2 nl doubles
-  // can leave s_etab at an odd double; misaligned dbl2 reads ran the kernel 3.5x slower)
-  dbl2* s_pt = (dbl2*)(smem + (((s_etab + kExpTabN) - smem + 1) & ~1L));
+  // can leave the y-term rows' end at an odd double; misaligned dbl2 reads ran the kernel 3.5x slower)
+  dbl2* s_pt = (dbl2*)(smem + (((s_y + (LY ? 1 : kTabBufs) * ysz) - smem + 1) & ~1L));
   // row tables hold the KJ phi points of their row's phi block plus one padding entry, so two rows read
   // at the same phi by the two halves of a wavefront that straddles a row boundary land in different
   // banks (a 512-B row stride is 128 dwords: the same bank, a 2-way conflict in every straddling wave)
@@ -697,13 +699,19 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
       const dbl2* mwt = (const dbl2*)qvt;
       const dbl2* pet = s_pe + tb * bpsz;
       const double* yb = s_y + tb * ysz;
+      // PTM: the lane's renormalisation factor of cell t + 1 is loaded while cell t is integrated (a
+      // per-cell load used at once left every cell waiting for the HBM / MALL latency)
+      auto rn_load = [&](int t) { return A.renorm[(FB ? (long)fbl[cbx + t] : cbx + t) * A.npart + s]; };
+      double rn_next = (MODE == PTM && ntx > 0) ? rn_load(0) : 0.0;
       for (int t = 0; t < ntx; t++) {
+        const double rn_cell = rn_next;
+        if (MODE == PTM && t + 1 < ntx) rn_next = rn_load(t + 1);
         const double* R = s_rec + t * NREC;
         const double kind = R[R_KIND];
         if (kind == 0.0) continue;
         double rn_abs = R[R_RENORM];
         if (MODE == PTM || MODE == PTB) {
-          const double rn = (MODE == PTM) ? A.renorm[(FB ? (long)fbl[cbx + t] : cbx + t) * A.npart + s] : R[R_RENORM];
+          const double rn = (MODE == PTM) ? rn_cell : R[R_RENORM];
           if (!isfinite(rn)) continue;    // species skipped (MomentumSpectra.cpp:828-832)
           rn_abs = fabs(rn);
         }

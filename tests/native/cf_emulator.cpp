@@ -334,6 +334,8 @@ extern "C" void emu_jonah_table(const orc_setup* su, double* l2, double* z, doub
 }
 
 // the modified path's table exp (exp_tab) on x: the caller's scaling x 64/ln2 included
+extern "C" int emu_exp_tab_n() { return kExpTabN; }
+
 extern "C" void emu_exp_tab(const double* x, long n, double* out) {
   const ExpTabCoef E = exp_tab_coef();
   for (long i = 0; i < n; i++) out[i] = exp_tab(E, kExp2Tab, x[i] * kInvLn2xN);

@@ -1,4 +1,4 @@
-"""Correctly rounded 2^(j/N), j = 0..N-1 (N = 64 or 256), and the Taylor coefficients of e^(c rs) - 1 in rs
+"""Correctly rounded 2^(j/N), j = 0..N-1 (N = 64, 256 or 1024), and the Taylor coefficients of e^(c rs) - 1 in rs
 (c = ln2/N) for cf_math.h exp_tab.  Decimal arithmetic at 50 digits; float(Decimal) rounds
 correctly, so every table entry is the double nearest the exact value."""
 from decimal import Decimal, getcontext
@@ -9,8 +9,8 @@ LN2 = Decimal(2).ln()
 
 def main():
     import sys
-    n = int(sys.argv[1]) if len(sys.argv) > 1 else 64          # 64 (degree 5) or 256 (degree 4)
-    deg = 5 if n == 64 else 4
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 64          # 64 (degree 5), 256 (degree 4), 1024 (degree 3)
+    deg = {64: 5, 256: 4, 1024: 3}[n]
     tab = [float((Decimal(j) / n * LN2).exp()) for j in range(n)]
     c = LN2 / n
     coef = [c ** k / Decimal(__import__("math").factorial(k)) for k in range(1, deg + 1)]
