@@ -16,7 +16,7 @@ size-independent properties in test_gpu_parity.py / test_gpu_properties.py."""
 import numpy as np
 import pytest
 
-from helpers import parity
+from helpers import emu_spectra, parity
 from is3d2_amd import build_engine, hrg, make_spec, synth
 from oracle import oracle as O
 
@@ -144,11 +144,20 @@ def test_modified_fallback_launch(dim, mode):
     assert rst[0] > 0 and st["breakdown"] == rst[0]
     assert np.array_equal(np.isnan(got), np.isnan(ref))      # 2+1D PTB: the reference's NaN rows
     rel, zr, zg = parity(np.nan_to_num(got), np.nan_to_num(ref))
-    # PTMA: on this surface the warm-started Newton chain (tolerance 1e-4, AnisoVariables.cpp) takes a different
-    # number of steps in the device math than in the oracle (894 vs 751 over the chain; the host emulator of
-    # the same math agrees with the GPU), so the converged (lambda, aT, aL) agree to the solver's tolerance,
-    # not to rounding: measured 1.7e-7 -- the north_star bar (1e-6) applies
-    assert rel < (1e-6 if mode == 5 else TOL), rel
+    if mode != 5:
+        assert rel < TOL, rel
+        return
+    # PTMA: on this surface (bulk x10) the warm-started Newton chain (tolerance 1e-4, AnisoVariables.cpp) is
+    # sensitive to last-bit differences: the device math sums the hadrons merged by (mass, sign) and the host
+    # libm's exp / pow differ between CPUs, so the step count over the chain differs from the oracle's (894
+    # vs 751 here) and the converged (lambda, aT, aL) agree to the solver's tolerance, not to rounding
+    # (measured 1.7e-7 on an EPYC host, 2.6e-6 on a Xeon host; unchained solves 3.4e-6).  So: the GPU must
+    # equal the host build of the same device math (tests/native/cf_emulator.cpp: same Newton path, same
+    # step count) to rounding, and the oracle to the solver's tolerance.
+    emu, est = emu_spectra(spec, s, chains=1, variant=4)
+    assert st["iterations"] == est[3], (st["iterations"], est[3])
+    assert parity(np.nan_to_num(got), np.nan_to_num(emu))[0] < TOL
+    assert rel < 1e-5, rel
 
 
 def test_modified_fallback_launch_smash_grid():
