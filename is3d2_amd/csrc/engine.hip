@@ -27,6 +27,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
+#include <cstdint>
+#include <map>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -156,16 +159,17 @@ __global__ __launch_bounds__(256) void k_famod_b(PrepArgs A, const double* sol) 
 
 struct RenormArgs {
   PrepConsts k;
-  const double* rec; const double* aux; double* renorm;   // renorm[c][s_sorted]
+  const double* rec; const double* aux; double* renorm;   // renorm[c][class]
   const double *mass, *sign, *degen, *baryon;              // sorted species
-  long n; int npart;
+  const int* rrep;                                         // representative sorted species of each class
+  long n; int npart;                                       // npart = number of classes
 };
 
 __global__ __launch_bounds__(256) void k_renorm(RenormArgs A) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= A.n * A.npart) return;
   const long c = idx / A.npart;
-  const int s = (int)(idx % A.npart);
+  const int s = A.rrep[(int)(idx % A.npart)];
   if (A.rec[c * NREC + R_KIND] == 0.0) { A.renorm[idx] = 0.0; return; }
   double aux[9];
 #pragma unroll
@@ -491,6 +495,12 @@ struct is3d_engine {
   const double* d_aniso_h = nullptr;   // [3][n_aniso_h] merged (mass, sign, degeneracy) of the PTMA hadrons
   int n_aniso_h = 0;
   int* d_sorig = nullptr;
+  // PTM renormalisation classes: sorted species with identical (mass, sign, degeneracy, baryon) share one
+  // n_linear / n_mod per cell (ptm_renorm depends on nothing else): d_rcls[s] = class of sorted species s,
+  // d_rrep[k] = a representative sorted species of class k (SMASH 444 -> nrcls classes)
+  int* d_rcls = nullptr;
+  int* d_rrep = nullptr;
+  int nrcls = 0;
   double* d_surf = nullptr; bool surf_owned = false; long ncell = 0; long surf_cap = 0;
   double *d_rec = nullptr, *d_aux = nullptr, *d_sol = nullptr, *d_renorm = nullptr, *d_slab = nullptr, *d_out = nullptr;
   long rec_cap = 0, aux_cap = 0, sol_cap = 0, renorm_cap = 0, slab_cap = 0, out_cap = 0;
@@ -883,9 +893,21 @@ static int finalize_tables(is3d_engine* e) {
   const size_t oah = cput(am.data(), am.size());
   cput(as.data(), as.size());
   cput(ag.data(), ag.size());
+  std::vector<int> rcls(np), rrep;
+  {
+    std::map<std::array<uint64_t, 4>, int> cls;
+    for (int i = 0; i < np; i++) {
+      const std::array<uint64_t, 4> key{__builtin_bit_cast(uint64_t, sm[i]), __builtin_bit_cast(uint64_t, ss[i]),
+                                        __builtin_bit_cast(uint64_t, sd[i]), __builtin_bit_cast(uint64_t, sb[i])};
+      auto it = cls.find(key);
+      if (it == cls.end()) { it = cls.emplace(key, (int)rrep.size()).first; rrep.push_back(i); }
+      rcls[i] = it->second;
+    }
+  }
+  e->nrcls = (int)rrep.size();
   std::vector<double> sorig(np);
   dfree(e->d_const);
-  const size_t nconst = cb.size() + np;   // ints appended as raw space
+  const size_t nconst = cb.size() + 3 * (size_t)np;   // ints appended as raw space: sorig, rcls, rrep
   e->d_const = dalloc<double>(nconst);
   if (!e->d_const) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(constants) failed");
   HIPCHK(e, hipMemcpy(e->d_const, cb.data(), cb.size() * sizeof(double), hipMemcpyHostToDevice));
@@ -893,6 +915,10 @@ static int finalize_tables(is3d_engine* e) {
   for (int i = 0; i < np; i++) so[i] = e->order[i];
   e->d_sorig = (int*)(e->d_const + cb.size());
   HIPCHK(e, hipMemcpy(e->d_sorig, so.data(), np * sizeof(int), hipMemcpyHostToDevice));
+  e->d_rcls = (int*)(e->d_const + cb.size() + np);
+  e->d_rrep = (int*)(e->d_const + cb.size() + 2 * (size_t)np);
+  HIPCHK(e, hipMemcpy(e->d_rcls, rcls.data(), np * sizeof(int), hipMemcpyHostToDevice));
+  if (!rrep.empty()) HIPCHK(e, hipMemcpy(e->d_rrep, rrep.data(), rrep.size() * sizeof(int), hipMemcpyHostToDevice));
   e->d_smass = e->d_const + osm; e->d_ssign = e->d_const + oss; e->d_sbaryon = e->d_const + osb; e->d_sdegen = e->d_const + osd;
   e->d_degen_orig = e->d_const + odg; e->d_pT = e->d_const + opt; e->d_cphi = e->d_const + oc; e->d_sphi = e->d_const + os;
   e->d_y = e->d_const + oy; e->d_eta = e->d_const + oe; e->d_etaw = e->d_const + ow;
@@ -1025,11 +1051,12 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
     HIPCHK(e, hipGetLastError());
   }
   if (mode == PTM) {
-    if (!ensure(e->d_renorm, e->renorm_cap, n * (long)np)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(renorm) failed");
+    if (!ensure(e->d_renorm, e->renorm_cap, n * (long)e->nrcls)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(renorm) failed");
     RenormArgs ra{};
     ra.k = pa.k; ra.rec = e->d_rec; ra.aux = e->d_aux; ra.renorm = e->d_renorm;
-    ra.mass = e->d_smass; ra.sign = e->d_ssign; ra.degen = e->d_sdegen; ra.baryon = e->d_sbaryon; ra.n = n; ra.npart = np;
-    const long tot = n * (long)np;
+    ra.mass = e->d_smass; ra.sign = e->d_ssign; ra.degen = e->d_sdegen; ra.baryon = e->d_sbaryon; ra.n = n;
+    ra.npart = e->nrcls; ra.rrep = e->d_rrep;
+    const long tot = n * (long)e->nrcls;
     hipLaunchKernelGGL(k_renorm, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, ra);
     HIPCHK(e, hipGetLastError());
   }
@@ -1065,7 +1092,7 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
     HIPCHK(e, hipGetLastError());
   }
   SpecArgs sa{};
-  sa.rec = e->d_rec; sa.n = n; sa.renorm = e->d_renorm; sa.slab = e->d_slab; sa.outsize = outsize;
+  sa.rec = e->d_rec; sa.n = n; sa.renorm = e->d_renorm; sa.rcls = e->d_rcls; sa.nrcls = e->nrcls; sa.slab = e->d_slab; sa.outsize = outsize;
   sa.smass = e->d_smass; sa.ssign = e->d_ssign; sa.sbaryon = e->d_sbaryon; sa.sorig = e->d_sorig;
   sa.csg = e->d_csg;
   sa.pT = e->d_pT; sa.cphi = e->d_cphi; sa.sphi = e->d_sphi; sa.yv = e->d_y; sa.etav = e->d_eta; sa.etaw = e->d_etaw;
@@ -1201,11 +1228,12 @@ extern "C" int is3d_calculate_dN_dX(is3d_engine* e, double* dN_taudtaudy, double
     }
     HIPCHK(e, hipGetLastError());
     if (mode == PTM) {
-      if (!ensure(e->d_renorm, e->renorm_cap, n * (long)np)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(renorm) failed");
+      if (!ensure(e->d_renorm, e->renorm_cap, n * (long)e->nrcls)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(renorm) failed");
       RenormArgs ra{};
       ra.k = pa.k; ra.rec = e->d_rec; ra.aux = e->d_aux; ra.renorm = e->d_renorm;
-      ra.mass = e->d_smass; ra.sign = e->d_ssign; ra.degen = e->d_sdegen; ra.baryon = e->d_sbaryon; ra.n = n; ra.npart = np;
-      const long tot = n * (long)np;
+      ra.mass = e->d_smass; ra.sign = e->d_ssign; ra.degen = e->d_sdegen; ra.baryon = e->d_sbaryon; ra.n = n;
+    ra.npart = e->nrcls; ra.rrep = e->d_rrep;
+      const long tot = n * (long)e->nrcls;
       hipLaunchKernelGGL(k_renorm, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, ra);
       HIPCHK(e, hipGetLastError());
     }
@@ -1225,7 +1253,7 @@ extern "C" int is3d_calculate_dN_dX(is3d_engine* e, double* dN_taudtaudy, double
     da.cells_per_wg = cpw;
     da.nchunk = (n + cpw - 1) / cpw;
     if (!ensure(e->d_ycell, e->ycell_cap, (long)np * n)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(cell yields) failed");
-    da.rec = e->d_rec; da.n = n; da.renorm = e->d_renorm; da.ycell = e->d_ycell;
+    da.rec = e->d_rec; da.n = n; da.renorm = e->d_renorm; da.rcls = e->d_rcls; da.nrcls = e->nrcls; da.ycell = e->d_ycell;
     da.smass = e->d_smass; da.ssign = e->d_ssign; da.sbaryon = e->d_sbaryon;
     da.pT = e->d_pT; da.pTw = e->d_pTw; da.cphi = e->d_cphi; da.sphi = e->d_sphi; da.phiw = e->d_phiw;
     da.yv = e->d_y; da.etav = e->d_eta; da.etaw = e->d_etaw;

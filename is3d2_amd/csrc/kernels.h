@@ -64,7 +64,8 @@ constexpr int kYRow = NYT | 1;
 // ------------------------------------------------------------------------------------------
 struct SpecArgs {
   const double* rec; long n;
-  const double* renorm;       // PTM: [c][s_sorted]
+  const double* renorm;       // PTM: [c][renorm class]
+  const int* rcls; int nrcls; // renorm class of each sorted species (engine.hip), number of classes
   double* slab; long outsize;
   const double *smass, *ssign, *sbaryon; const int* sorig;
   const double *pT, *cphi, *sphi, *yv, *etav, *etaw;
@@ -145,7 +146,8 @@ constexpr int kTbQ = 4;
 
 struct DndxArgs {
   const double* rec; long n;
-  const double* renorm;       // PTM: [c][s_sorted]
+  const double* renorm;       // PTM: [c][renorm class]
+  const int* rcls; int nrcls; // renorm class of each sorted species (engine.hip), number of classes
   double* ycell;              // [npart (sorted)][n]: sum over (pT, phi, y, eta) of w_pT w_phi w_eta p.dsigma f
   const double *smass, *ssign, *sbaryon;
   const double *pT, *pTw, *cphi, *sphi, *phiw, *yv, *etav, *etaw;
@@ -701,7 +703,8 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
       const double* yb = s_y + tb * ysz;
       // PTM: the lane's renormalisation factor of cell t + 1 is loaded while cell t is integrated (a
       // per-cell load used at once left every cell waiting for the HBM / MALL latency)
-      auto rn_load = [&](int t) { return A.renorm[(FB ? (long)fbl[cbx + t] : cbx + t) * A.npart + s]; };
+      const int rc = (MODE == PTM) ? A.rcls[s] : 0;
+      auto rn_load = [&](int t) { return A.renorm[(FB ? (long)fbl[cbx + t] : cbx + t) * A.nrcls + rc]; };
       double rn_next = (MODE == PTM && ntx > 0) ? rn_load(0) : 0.0;
       for (int t = 0; t < ntx; t++) {
         const double rn_cell = rn_next;
@@ -928,7 +931,7 @@ __global__ __launch_bounds__(kBlock, dndx_waves<MODE>()) void k_dndx(DndxArgs A)
         if (kind == 0.0) continue;
         double rn_abs = R[R_RENORM];
         if (MODE == PTM || MODE == PTB) {
-          const double rn = (MODE == PTM) ? A.renorm[(cb + t) * A.npart + s] : R[R_RENORM];
+          const double rn = (MODE == PTM) ? A.renorm[(cb + t) * A.nrcls + A.rcls[s]] : R[R_RENORM];
           if (!isfinite(rn)) continue;    // cell skipped for this species (SpacetimeDistribution.cpp:972-976)
           rn_abs = fabs(rn);
         }
