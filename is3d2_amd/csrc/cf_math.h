@@ -1019,7 +1019,9 @@ IS3D_HD void sep_cell_consts(int mode, double* R) {
 //   Q1 = pi^tt ch^2 + tau^2 pi^ee sh^2 - 2 tau pi^te ch sh,  W = V^t ch - tau V^e sh
 // and the separable delta-f coefficients factor as  S0 = mT^2 S2 + mT b S1 + m^2 R_S0M2,
 // Sc = mT SC1 + b R_SCB,  Ss = mT SS1 + b R_SSB,  L0 = mT L1 + b R_L0B  (see sep_setup).
-IS3D_HD void yterms(int mode, int op, const double* R, double y, double eta, double w, double* Y) {
+// mu_slots = false: rows of kYRowLY doubles (k_spectra's per-lane rows), without Y_MU2 / Y_MU (mod_setup
+// then takes |sig U| itself, ymu = false)
+IS3D_HD void yterms(int mode, int op, const double* R, double y, double eta, double w, double* Y, bool mu_slots = true) {
   const int quirk = quirk_pds(mode, op);
   // separable part: p^tau = mT cosh(y-eta) (spectra Grad/CE: sqrt(1+sinh^2), MomentumSpectra.cpp:307-308;
   // the spacetime path uses cosh, SpacetimeDistribution.cpp:313)
@@ -1062,11 +1064,14 @@ IS3D_HD void yterms(int mode, int op, const double* R, double y, double eta, dou
     Y[Y_MD] = quirk ? (w * chm * R[R_DAT] + shm * R[R_DANT]) : w * (chm * R[R_DAT] + shm * R[R_DANT]);
     Y[Y_NARROW] = (R[R_NARROW] != 0.0 && fabs(y - eta) < R[R_DET]) ? 1.0 : 0.0;
     // |sig U|^2 and |sig U| once per (cell, q) instead of once per (cell, lane) in mod_setup
-    const double ux = Y[Y_MUX], uy = Y[Y_MUY], uz = Y[Y_MUZ];
-    Y[Y_MU2] = fma(ux, ux, fma(uy, uy, uz * uz));
-    Y[Y_MU] = sqrt(Y[Y_MU2]);
+    if (mu_slots) {
+      const double ux = Y[Y_MUX], uy = Y[Y_MUY], uz = Y[Y_MUZ];
+      Y[Y_MU2] = fma(ux, ux, fma(uy, uy, uz * uz));
+      Y[Y_MU] = sqrt(Y[Y_MU2]);
+    }
   } else {
-    Y[Y_MUX] = Y[Y_MUY] = Y[Y_MUZ] = Y[Y_MD] = Y[Y_NARROW] = Y[Y_MU2] = Y[Y_MU] = 0.0;
+    Y[Y_MUX] = Y[Y_MUY] = Y[Y_MUZ] = Y[Y_MD] = Y[Y_NARROW] = 0.0;
+    if (mu_slots) Y[Y_MU2] = Y[Y_MU] = 0.0;
   }
   Y[Y_W] = w;                      // w_eta (PD-table scale, sep_setup)
 }
@@ -1606,9 +1611,9 @@ static constexpr double kModTabX = 1.0e6, kModTabChem = 30.0;
 #endif
 
 IS3D_HD void mod_setup(const double* R, const double* Y, double mT, double m2, double pT, double sign, double baryon,
-                       double renorm_abs, const double* etab, ModLane& L) {
+                       double renorm_abs, const double* etab, ModLane& L, bool ymu = true) {
   const double ux = Y[Y_MUX], uy = Y[Y_MUY], uz = Y[Y_MUZ];   // sig U
-  const double u2 = Y[Y_MU2];
+  const double u2 = ymu ? Y[Y_MU2] : fma(ux, ux, fma(uy, uy, uz * uz));
   const double sig = R[R_INVTM] * kInvLn2xN, m2s = m2 * (sig * sig);
   L.E0 = fma(mT * mT, u2, m2s);
   const double tm = 2.0 * mT;
@@ -1621,7 +1626,7 @@ IS3D_HD void mod_setup(const double* R, const double* Y, double mT, double m2, d
   // | |mT U| - pT |V|max | <= |p_mod| <= |mT U| + pT |V|max (sig units): if even the smallest E_mod
   // overflows exp, every phi point is exactly 0; if the largest could leave the table lanes' domain
   // the lane takes the clamped exp
-  const double mu = mT * Y[Y_MU];
+  const double mu = mT * (ymu ? Y[Y_MU] : sqrt(u2));
   const double lo = mu - pT * R[R_VB], hi = mu + pT * R[R_VB];
 #if IS3D_MOD_SQ_BOUNDS
   // the same two tests on squares (no sqrt): skip when sig E_min (1 - 1e-12) exceeds

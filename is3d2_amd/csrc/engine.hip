@@ -735,7 +735,7 @@ static SpectraPlan spectra_plan(const is3d_engine* e) {
     const size_t rb = pipe ? 3 : 2, tb = pipe ? 2 : 1, qvf = (mode >= PTM || !pipe) ? 2 : 1;
     return sizeof(double) * (rb * tile * NREC + 4 * nphp + tb * 2 * tile * nphp + tb * qvf * tile * nphp +
                              (size_t)(nk + 2 * nl) +
-                             (qrows ? tb * tile * std::min(qrows, P.nq) : (size_t)kBlock) * kYRow + kExpTabN +
+                             (qrows ? tb * tile * std::min(qrows, P.nq) * kYRow : (size_t)kBlock * kYRowLY) + kExpTabN +
                              (P.tb ? 2 * tile * qrows * (P.KJ + 1) + 1 : 0) +
                              (P.tb && mode == CE ? tb * 2 * tile * nphp : 0) +
                              (mode >= PTM && qrows ? tile * qrows * (P.KJ + 1) + 1 : 0));

@@ -58,6 +58,9 @@ constexpr int dndx_waves() { return (MODE == CE || MODE >= PTM) ? 2 : spectra_wa
 // by consecutive lanes (rows 152 B apart) spread over the 64 banks instead of hitting two of them
 // (a 128-B stride put every lane of a wave on the same bank pair: a 32-way conflict)
 constexpr int kYRow = NYT | 1;
+// per-lane y-term rows of the F_LY / F_FB launches: without the Y_MU2 / Y_MU slots (17 doubles, odd): the
+// 256 rows are LDS the launch's occupancy depends on, and each lane's row serves one lane only
+constexpr int kYRowLY = Y_MU2 | 1;
 
 // ------------------------------------------------------------------------------------------
 // spectra kernel
@@ -481,8 +484,8 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
   const int nqm = A.nqmax;                                // rows per cell (>= every workgroup's nqw)
   const long recsz = (long)kTile * NREC, bpsz = (long)kTile * nphp, qvsz = kQvF * bpsz;
   // y-term rows per cell: per row, or per q once the rows cover every q (nyr below): min(nqm, nq);
-  // LY launches: one y-term row per lane instead ([kBlock][kYRow], single; odd row stride: no conflicts)
-  const long ysz = (LY ? (long)kBlock : (long)kTile * min(nqm, A.nq)) * kYRow;
+  // LY launches: one y-term row per lane instead ([kBlock][kYRowLY], single; odd row stride: no conflicts)
+  const long ysz = LY ? (long)kBlock * kYRowLY : (long)kTile * min(nqm, A.nq) * kYRow;
   // the exp table first: at LDS offset 0 its address is the table index alone (no base register, which
   // the modified loop otherwise re-read from an SGPR spill lane at every point)
   double* s_etab = smem;                                  // [kExpTabN] 2^(j/kExpTabN)
@@ -721,9 +724,9 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
         const dbl2* BP = bpt + t * nphp + j0;
         const double* Y = yb + ((long)t * nyr + yrow) * kYRow;
         if constexpr (LY) {        // this lane's own y-terms, in its LDS row
-          double* Yl = s_y + (long)tid * kYRow;
+          double* Yl = s_y + (long)tid * kYRowLY;
           const int kk = q / A.nl, l = q % A.nl;
-          yterms(MODE, A.op, R, s_grid[kk], (A.dim == 3) ? R[R_ETA] : s_grid[A.nk + l], s_grid[A.nk + A.nl + l], Yl);
+          yterms(MODE, A.op, R, s_grid[kk], (A.dim == 3) ? R[R_ETA] : s_grid[A.nk + l], s_grid[A.nk + A.nl + l], Yl, false);
           Y = Yl;
         }
         const bool sep = (MODE <= CE) || kind == 1.0 || Y[Y_NARROW] != 0.0;
@@ -757,7 +760,7 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
         }
         if constexpr (MODMAIN) {
           ModLane M;
-          mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, s_etab, M);
+          mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, s_etab, M, !LY);
           if (M.skip) continue;
           const dbl2* MW = mwt + t * nphp + j0;
           if constexpr (LY) {        // no T2 rows: the lane's linear forms (mod_pair_lane_t)
