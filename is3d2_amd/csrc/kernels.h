@@ -853,8 +853,10 @@ __global__ __launch_bounds__(kBlock, dndx_waves<MODE>()) void k_dndx(DndxArgs A)
   double* s_qv = (double*)(s_bp + kTile * nphp);         // [kTile][nphp] Qv of the current pT (modified path)
   double* s_red = s_qv + kTile * nphp;                    // [kTile][kBlock] per-lane cell sums
   double* s_grid = s_red + kTile * kBlock;                // y[nk] | eta[nl] | eta_w[nl]
-  double* s_y = s_grid + A.nk + 2 * A.nl;                 // [kTile][nq][kYRow]
-  double* s_etab = s_y + (long)kTile * A.nq * kYRow;      // [kExpTabN] exp_tab's 2^(j/kExpTabN)
+  // y-term rows without the Y_MU2 / Y_MU slots (kYRowLY): two more doubles per row took config 2's Grad
+  // launch past the LDS of three workgroups per CU (k_dndx 647 -> 784 ms)
+  double* s_y = s_grid + A.nk + 2 * A.nl;                 // [kTile][nq][kYRowLY]
+  double* s_etab = s_y + (long)kTile * A.nq * kYRowLY;    // [kExpTabN] exp_tab's 2^(j/kExpTabN)
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   for (int i = tid; i < kExpTabN; i += kBlock) s_etab[i] = kExp2Tab[i];
@@ -898,7 +900,7 @@ __global__ __launch_bounds__(kBlock, dndx_waves<MODE>()) void k_dndx(DndxArgs A)
         const double y = s_grid[ky];
         const double eta = (A.dim == 3) ? R[R_ETA] : s_grid[A.nk + l];
         const double w = s_grid[A.nk + A.nl + l];
-        yterms(MODE, 0, R, y, eta, w, s_y + ((long)t * A.nq + q) * kYRow);
+        yterms(MODE, 0, R, y, eta, w, s_y + ((long)t * A.nq + q) * kYRowLY, false);
       }
     }
     for (int ipt = 0; ipt < A.npT; ipt++) {
@@ -928,13 +930,14 @@ __global__ __launch_bounds__(kBlock, dndx_waves<MODE>()) void k_dndx(DndxArgs A)
       }
       __syncthreads();
       if (!active) continue;
+      const int rc = (MODE == PTM) ? A.rcls[s] : 0;      // the lane's renormalisation class
       for (int t = 0; t < nt; t++) {
         const double* R = s_rec + t * NREC;
         const double kind = R[R_KIND];
         if (kind == 0.0) continue;
         double rn_abs = R[R_RENORM];
         if (MODE == PTM || MODE == PTB) {
-          const double rn = (MODE == PTM) ? A.renorm[(cb + t) * A.nrcls + A.rcls[s]] : R[R_RENORM];
+          const double rn = (MODE == PTM) ? A.renorm[(cb + t) * A.nrcls + rc] : R[R_RENORM];
           if (!isfinite(rn)) continue;    // cell skipped for this species (SpacetimeDistribution.cpp:972-976)
           rn_abs = fabs(rn);
         }
@@ -942,7 +945,7 @@ __global__ __launch_bounds__(kBlock, dndx_waves<MODE>()) void k_dndx(DndxArgs A)
         for (int task = slot; task < A.ntask; task += nslot) {
           const int kk = task / A.nl, l = task % A.nl;
           const int k = kk % A.nk, jb = kk / A.nk, j0 = jb * KJ;
-          const double* Y = s_y + ((long)t * A.nq + k * A.nl + l) * kYRow;
+          const double* Y = s_y + ((long)t * A.nq + k * A.nl + l) * kYRowLY;
           const dbl2* BP = s_bp + t * nphp + j0;
           const dbl2* W = (const dbl2*)(s_w + j0);
           const bool sep = (MODE <= CE) || kind == 1.0 || Y[Y_NARROW] != 0.0;
@@ -954,7 +957,7 @@ __global__ __launch_bounds__(kBlock, dndx_waves<MODE>()) void k_dndx(DndxArgs A)
                            : sep_phi_wsum<MODE, FLAGS, false, KJ>(L, s_cs + j0, BP, W);
           } else if (MODE >= PTM) {
             ModLane M;
-            mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, s_etab, M);
+            mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, s_etab, M, false);
             if (M.skip) continue;
             const dbl2* QV = (const dbl2*)(s_qv + t * nphp + j0);
             cell += M.clamp ? mod_phi_wsum<FLAGS, true, KJ>(M, s_cs + j0, QV, W)
