@@ -48,15 +48,18 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def make_surface(cfg, rank, world, dim, baryon):
-    from is3d2_amd import synth
+def make_surface(cfg, rank, world, dim, baryon, whole=False):
+    """This rank's cells: weak scaling -- its own surface (seed 7 + rank); strong scaling -- its cost-balanced
+    contiguous range of the one surface (dist.shard_bounds), or the whole surface and the range (whole=True,
+    PTMA warm-start chains: every rank walks the chain, integrates its range)."""
+    from is3d2_amd import dist as D, synth
     if cfg["scaling"] == "strong":
-        total = cfg["cells"]
-        lo = rank * total // world
-        hi = (rank + 1) * total // world
-        s = synth.as_read(synth.surface(total, seed=7, dimension=dim, baryon=baryon, full3d=(dim == 3)))
-        return {k: np.ascontiguousarray(v[lo:hi]) for k, v in s.items()}
-    return synth.as_read(synth.surface(cfg["cells"], seed=7 + rank, dimension=dim, baryon=baryon, full3d=(dim == 3)))
+        s = synth.as_read(synth.surface(cfg["cells"], seed=7, dimension=dim, baryon=baryon, full3d=(dim == 3)))
+        lo, hi = D.shard_bounds(s, rank, world)
+        if whole:
+            return s, (lo, hi)
+        return {k: np.ascontiguousarray(v[lo:hi]) for k, v in s.items()}, None
+    return synth.as_read(synth.surface(cfg["cells"], seed=7 + rank, dimension=dim, baryon=baryon, full3d=(dim == 3))), None
 
 
 def _host_cpu():
@@ -138,7 +141,24 @@ def executed_roofline(args, mode, ms_spectra, ms_total, neta, units_local, n_loc
     for name in ("pmc_traffic", "pmc_valu"):
         path = os.path.join(ROOT, "profiles", name + ".json")
         pmc[name] = json.load(open(path)).get(key) if os.path.exists(path) else None
+    from is3d2_amd import _lib
+    bid = _lib.build_id()
     traffic, ex = pmc["pmc_traffic"], pmc["pmc_valu"]
+    stale = []
+    # counter summaries count only for the identical build (is3d_build_id: hash of the sources and flags):
+    # a profile of an older kernel would price this run's time against another kernel's instruction counts
+    if isinstance(traffic, dict):
+        if traffic.get("build_id") != bid:
+            stale.append("traffic: %s (build %s)" % (traffic.get("tag"), traffic.get("build_id")))
+            traffic = None
+        else:
+            traffic = traffic["hbm_bytes_per_launch"]
+    elif traffic is not None:
+        stale.append("traffic: untagged")
+        traffic = None
+    if ex is not None and ex.get("build_id") != bid:
+        stale.append("executed: %s (build %s)" % (ex.get("tag"), ex.get("build_id")))
+        ex = None
     t = ms_spectra * 1e-3
     ref_flops = FLOPS_PER_NODE[mode] * neta * units_local
     algo_bytes = 200.0 * n_local + 8.0 * outsize           # surface read once + spectra written once
@@ -149,7 +169,10 @@ def executed_roofline(args, mode, ms_spectra, ms_total, neta, units_local, n_loc
          "algorithmic_bytes": algo_bytes,
          "traffic_over_algorithmic": None if traffic is None else traffic / algo_bytes,
          "hbm_gbs": None if traffic is None else traffic / t / 1e9,
-         "hbm_frac": None if traffic is None else traffic / t / HBM_PEAK_BPS}
+         "hbm_frac": None if traffic is None else traffic / t / HBM_PEAK_BPS,
+         "build_id": bid}
+    if stale:
+        r["stale_profiles"] = "counter summaries of another build, not used: " + "; ".join(stale)
     if ex is not None:
         if "fp64_flops_per_launch" in ex:
             r["achieved"] = ex["fp64_flops_per_launch"] / t / 1e12
@@ -180,12 +203,16 @@ def run_workload(args, cfg_name, mode, steps, warmup, rank, world, local_rank, d
         flags.pop("include_baryon", None); flags.pop("include_baryondiff_deltaf", None)
     spec = make_spec(hrg_eos=cfg["hrg"], chosen=cfg["chosen"], pT=cfg["pT"], phi=cfg["phi"], y="y21", eta="eta24",
                      dimension=cfg["dim"], df_mode=mode, gla_points=cfg.get("gla", 32), **flags)
-    surf = make_surface(cfg, rank, world, cfg["dim"], bool(flags.get("include_baryon", 0)))
-    n_local = len(surf["tau"])
+    chained = mode == 5 and spec["params"]["famod_chains"] > 0 and world > 1
+    surf, window = make_surface(cfg, rank, world, cfg["dim"], bool(flags.get("include_baryon", 0)), whole=chained)
+    n_local = len(surf["tau"]) if window is None else window[1] - window[0]
     reduce = D.torch_all_reduce(dist, dev) if world > 1 else (lambda a: a)
-    T_avg = D.global_averages(D.average_sums(surf, flags.get("include_baryon", 0)), reduce)[0]
+    mine = surf if window is None else {k: v[window[0]:window[1]] for k, v in surf.items()}
+    T_avg = D.global_averages(D.average_sums(mine, flags.get("include_baryon", 0)), reduce)[0]
 
     eng = build_engine(spec, surf, T_avg=T_avg, device=local_rank)
+    if window is not None:
+        eng.set_cell_window(*window)
     outsize = eng.output_size()
     out = torch.zeros(outsize, dtype=torch.float64, device=dev)
     stream = torch.cuda.current_stream(dev).cuda_stream
@@ -246,6 +273,7 @@ def run_workload(args, cfg_name, mode, steps, warmup, rank, world, local_rank, d
                        "" if neta == 1 else " x %d eta" % neta),
         "operation": operation,
         "cells_per_gpu": n_local, "species": nsp, "grid": [npT, nphi, ny, neta], "df_mode": mode,
+        "famod_chains": spec["params"]["famod_chains"] if mode == 5 else None,
         "parallelism": "dp%d (cell shards + RCCL all-reduce of spectra)" % world if world > 1 else "1 GPU",
     }
     return dict(value=total_units / elapsed, elapsed=elapsed, steps=steps, warmup=warmup, cfg=cfg, config=config,
@@ -284,6 +312,8 @@ def main():
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
 
+    from is3d2_amd import _lib
+    log("build_id %s" % _lib.build_id())
     m = run_workload(args, args.config, args.df_mode, args.steps, args.warmup, rank, world, local_rank, dev, dist)
     ns = None
     if args.north_star_steps > 0 and args.config != "config4" and args.operation == 1:

@@ -107,7 +107,21 @@ typedef struct {
 } is3d_stats;
 
 int is3d_abi_version(void);
+/* Build identity: a hash of the sources and compiler flags this library was built from (Makefile SRC_ID).
+ * The committed rocprofv3 counter summaries (profiles/pmc_*.json) record it; bench.py reports their
+ * roofline figures only for the identical build. */
+const char *is3d_build_id(void);
 is3d_engine *is3d_create(int device);
+/* One engine over several GPUs of this process (the multi-GPU fan-out inside the compute
+ * call).  Every setter goes to one engine per listed device; is3d_set_surface splits the cells into
+ * contiguous windows of ~equal estimated cost (cells with u.dsigma <= 0 are nearly free); one
+ * is3d_calculate_spectra / is3d_launch runs all devices concurrently and sums their spectra with one
+ * RCCL ncclAllReduce (float64, sum) of the device-resident outputs -- or, when the list repeats a device,
+ * with peer copies and a fixed-order add on devices[0].  is3d_launch's dev_out and stream belong to
+ * devices[0].  PTMA with warm-start chains (famod_chains > 0): every device holds the whole surface and
+ * walks the chains (set the params before the surface).  Replaces the reference's OpenMP fan-out
+ * (MomentumSpectra.cpp:98-107) and its thread reduction (:383-411). */
+is3d_engine *is3d_create_devices(int n_devices, const int *devices);
 void is3d_destroy(is3d_engine *e);
 const char *is3d_last_error(const is3d_engine *e);
 
@@ -131,6 +145,12 @@ int is3d_set_surface(is3d_engine *e, long n_cells, const is3d_surface *s);
 /* Same, but the 25 field arrays are already in device memory on the engine's GPU
  * (field-major: dev[f * n_cells + c], f in is3d_surface order).  Not copied. */
 int is3d_set_surface_device(is3d_engine *e, long n_cells, const double *dev_fields);
+
+/* Integrate only cells [lo, hi) of the surface set last (lo = hi = -1: every cell; setting a surface clears
+ * it).  For one process per GPU: every rank holds the whole surface and integrates its window; the PTMA
+ * warm-start chains (famod_chains > 0) still walk every cell, so each window sees the serial chain's
+ * solutions (MomentumSpectra.cpp:1308-1364), which cell shards could not. */
+int is3d_set_cell_window(is3d_engine *e, long lo, long hi);
 
 /* Full call: kernels + device->host copy of dN/(pT dpT dphi dy) into dN_out. */
 int is3d_calculate_spectra(is3d_engine *e, double *dN_out);

@@ -21,6 +21,9 @@
 #ifndef IS3D_ANISO_MERGE
 #define IS3D_ANISO_MERGE 1    // PTMA Newton sums over hadrons merged by identical (mass, sign)
 #endif
+#ifndef IS3D_TB2
+#define IS3D_TB2 0            // Grad table launch with two species per lane (F_S2), A/B variant
+#endif
 #ifndef IS3D_MAX_SPLITS
 #define IS3D_MAX_SPLITS 64    // cap on k_spectra's cell splits (one output-sized slab each)
 #endif
@@ -41,6 +44,7 @@
 #include "cf_math.h"
 #include "spline_host.h"
 #include "kernels.h"
+#include "group.h"
 
 using namespace is3d;
 using namespace is3d::kern;
@@ -60,15 +64,16 @@ struct PrepArgs {
   const double* surf;   // [NSURF][n]
   double* rec;          // [n][NREC]
   double* aux;          // PTM/PTB: [9][n]; PTMA: [9][n] Newton inputs
-  long n;
+  long n;               // cells held (the field stride of surf / aux)
+  long c0, c1;          // cells [c0, c1) prepared by this launch
   int* err;
   unsigned long long* cnt;  // [0] breakdown [1] pl<0 [2] recon fail [3] iterations
 };
 
 template <int MODE>
 __global__ __launch_bounds__(256) void k_prep(PrepArgs A) {
-  const long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= A.n) return;
+  const long c = A.c0 + (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= A.c1) return;
   double s[NSURF];
 #pragma unroll
   for (int f = 0; f < NSURF; f++) s[f] = A.surf[(long)f * A.n + c];
@@ -107,8 +112,9 @@ struct WaveSum {
 };
 
 struct AnisoArgs {
-  const double* rec; const double* ain; double* sol;   // rec [n][NREC], sol [6][n]
-  long n, chains;
+  const double* rec; const double* ain; double* sol;   // rec [n][NREC], ain [9][stride], sol [6][stride]
+  long c0, n, chains;   // cells [c0, c0 + n) in `chains` warm-start chains
+  long stride;          // cells held
   Hadrons h;
   double fp2;
   unsigned long long* cnt;
@@ -120,16 +126,16 @@ __global__ __launch_bounds__(64) void k_aniso(AnisoArgs A) {
   const int lane = threadIdx.x;
   double state[4] = {0.0, 0.0, 0.0, 0.0};
   long cnt[3] = {0, 0, 0};
-  for (long c = chain; c < A.n; c += A.chains) {
+  for (long c = A.c0 + chain; c < A.c0 + A.n; c += A.chains) {
     if (A.rec[c * NREC + R_KIND] == 0.0) continue;
     double ain[4];
 #pragma unroll
-    for (int f = 0; f < 4; f++) ain[f] = A.ain[(long)f * A.n + c];
+    for (int f = 0; f < 4; f++) ain[f] = A.ain[(long)f * A.stride + c];
     double out[6];
     aniso_cell(ain, A.h, lane, 64, WaveSum(), A.fp2, state, out, cnt);
     if (lane == 0) {
 #pragma unroll
-      for (int f = 0; f < 6; f++) A.sol[(long)f * A.n + c] = out[f];
+      for (int f = 0; f < 6; f++) A.sol[(long)f * A.stride + c] = out[f];
     }
   }
   if (lane == 0) {
@@ -139,9 +145,181 @@ __global__ __launch_bounds__(64) void k_aniso(AnisoArgs A) {
   }
 }
 
+// ---- PTMA warm-start chains (MomentumSpectra.cpp:1308-1364) in parallel segments -----------------------
+// The reference warm-starts each cell's Newton solve from the chain state the previous cell of its OpenMP
+// thread left (chain c = cells c, c + C, c + 2C, ...; the shipped serial build is one chain).  That state
+// recurrence is serial, and a lone wavefront walking it is latency-bound (354 us per cell on MI355X:
+// 1e5 cells took 35 s).  The chain is instead cut into segments of L positions, one wavefront each:
+//   pass 0      every segment runs its cells from a cold start (exact for each chain's first segment);
+//   pass j >= 1 a segment whose incoming state (the end state the previous segment left in pass j - 1)
+//               differs bitwise from the start its stored run used re-runs from the new start, and stops
+//               at the first cell whose new chain state equals the stored one: from there on the stored
+//               cells were computed from that same state, so they stand.  A segment that reaches its end
+//               without re-synchronising publishes a new end state and flags pass j as changed.
+// The passes stop once a pass changes nothing; then every segment's stored run starts from its
+// predecessor's true end state, i.e. the stored states and solutions are the serial chain's, bit for bit.
+// A chain state differs from a cold-start guess for ~10 cells on average before the Newton solves forget it
+// (CPU sweep study, tests/native/cf_emulator.cpp emu_chain_sweeps), so a pass re-runs little.  After
+// kChainPasses passes a single-wavefront finisher completes any remaining ripple serially (exact).
+constexpr int kChainPasses = 24;
+
+struct ChainArgs {
+  const double* rec; const double* ain; double* sol;   // ain [9][n], sol [6][n]
+  double* sta;           // [4][n] chain state after each cell (prev_ok, lambda, aT, aL)
+  int* info;             // [n] Newton iterations | pl/pt < 0 << 16 | reconstruction failure << 17
+  double* send;          // [2][4][nseg] segment end states, by pass parity
+  double* sstart;        // [4][nseg] the start state of each segment's stored run
+  int* changed;          // [kChainPasses] pass j changed some segment's end state
+  long n, C, L, nspc;    // cells, chains, positions per segment, segments per chain
+  Hadrons h;
+  double fp2;
+};
+
+__device__ __forceinline__ bool state_eq(const double* a, const double* b) {
+  bool eq = true;
+#pragma unroll
+  for (int f = 0; f < 4; f++) eq = eq && (__double_as_longlong(a[f]) == __double_as_longlong(b[f]));
+  return eq;
+}
+
+// Run segment `seg` from `state` (its start): re-run mode (sync) stops at the first cell whose new state equals
+// the stored one and returns true (end state unchanged); otherwise the state after the last cell is in `state`.
+__device__ bool chain_segment_run(const ChainArgs& A, long seg, double* state, bool sync) {
+  const int lane = threadIdx.x;
+  const long c = seg / A.nspc, s = seg % A.nspc;
+  const long P = (A.n - c + A.C - 1) / A.C;                 // positions of chain c
+  const long p0 = s * A.L, p1 = min(P, p0 + A.L);
+  for (long pos = p0; pos < p1; pos++) {
+    const long cell = c + pos * A.C;
+    if (A.rec[cell * NREC + R_KIND] == 0.0) continue;       // u.dsigma <= 0: not in the chain (:1146)
+    double ain[4];
+#pragma unroll
+    for (int f = 0; f < 4; f++) ain[f] = A.ain[(long)f * A.n + cell];
+    double out[6];
+    long cnt[3] = {0, 0, 0};
+    aniso_cell(ain, A.h, lane, 64, WaveSum(), A.fp2, state, out, cnt);
+    double old[4];
+#pragma unroll
+    for (int f = 0; f < 4; f++) old[f] = A.sta[(long)f * A.n + cell];
+    const bool same = sync && state_eq(state, old);
+    if (lane == 0) {
+#pragma unroll
+      for (int f = 0; f < 6; f++) A.sol[(long)f * A.n + cell] = out[f];
+#pragma unroll
+      for (int f = 0; f < 4; f++) A.sta[(long)f * A.n + cell] = state[f];
+      A.info[cell] = (int)cnt[2] | ((int)cnt[0] << 16) | ((int)cnt[1] << 17);
+    }
+    if (same) return true;
+  }
+  return false;
+}
+
+__global__ __launch_bounds__(64) void k_chain_pass(ChainArgs A, int pass) {
+  const long seg = blockIdx.x, nseg = A.C * A.nspc;
+  const int lane = threadIdx.x;
+  if (pass > 0 && A.changed[pass - 1] == 0) return;         // converged: the remaining passes are no-ops
+  const double* prev = A.send + (long)((pass + 1) & 1) * 4 * nseg;
+  double* cur = A.send + (long)(pass & 1) * 4 * nseg;
+  double state[4] = {0.0, 0.0, 0.0, 0.0};                   // cold: no previous success in this chain
+  if (pass > 0) {
+    double st0[4], used[4];
+#pragma unroll
+    for (int f = 0; f < 4; f++) used[f] = A.sstart[f * nseg + seg];
+    if (seg % A.nspc == 0) {
+#pragma unroll
+      for (int f = 0; f < 4; f++) st0[f] = 0.0;
+    } else {
+#pragma unroll
+      for (int f = 0; f < 4; f++) st0[f] = prev[f * nseg + seg - 1];
+    }
+    if (state_eq(st0, used)) {                              // same start: the stored run stands
+      if (lane == 0) for (int f = 0; f < 4; f++) cur[f * nseg + seg] = prev[f * nseg + seg];
+      return;
+    }
+#pragma unroll
+    for (int f = 0; f < 4; f++) state[f] = st0[f];
+  }
+  if (lane == 0) for (int f = 0; f < 4; f++) A.sstart[f * nseg + seg] = state[f];
+  const bool synced = chain_segment_run(A, seg, state, pass > 0);
+  if (lane == 0) {
+    if (synced) {
+      for (int f = 0; f < 4; f++) cur[f * nseg + seg] = prev[f * nseg + seg];
+    } else {
+      bool moved = pass == 0;
+      for (int f = 0; f < 4; f++) {
+        moved = moved || __double_as_longlong(state[f]) != __double_as_longlong(prev[f * nseg + seg]);
+        cur[f * nseg + seg] = state[f];
+      }
+      if (moved && pass > 0) atomicOr(&A.changed[pass], 1);
+    }
+  }
+  if (pass == 0 && lane == 0 && A.nspc > 1) atomicOr(&A.changed[0], 1);
+}
+
+// Serial completion after kChainPasses passes (one wavefront; normally returns at once): segments in chain
+// order, each from its predecessor's current end state -- exact by induction.
+__global__ __launch_bounds__(64) void k_chain_finish(ChainArgs A) {
+  if (A.changed[kChainPasses - 1] == 0) return;
+  const long nseg = A.C * A.nspc;
+  double* cur = A.send + (long)((kChainPasses - 1) & 1) * 4 * nseg;
+  const int lane = threadIdx.x;
+  // the running end state stays in registers (uniform over the wavefront): no memory round trip between
+  // segments, and every array element this kernel reads was written by an earlier launch or not at all
+  double carry[4] = {0.0, 0.0, 0.0, 0.0};
+  for (long seg = 0; seg < nseg; seg++) {
+    if (seg % A.nspc == 0) {
+#pragma unroll
+      for (int f = 0; f < 4; f++) carry[f] = cur[f * nseg + seg];
+      continue;
+    }
+    double used[4];
+#pragma unroll
+    for (int f = 0; f < 4; f++) used[f] = A.sstart[f * nseg + seg];
+    if (state_eq(carry, used)) {
+#pragma unroll
+      for (int f = 0; f < 4; f++) carry[f] = cur[f * nseg + seg];
+      continue;
+    }
+    if (lane == 0) for (int f = 0; f < 4; f++) A.sstart[f * nseg + seg] = carry[f];
+    double state[4] = {carry[0], carry[1], carry[2], carry[3]};
+    if (chain_segment_run(A, seg, state, true)) {
+#pragma unroll
+      for (int f = 0; f < 4; f++) carry[f] = cur[f * nseg + seg];
+    } else {
+#pragma unroll
+      for (int f = 0; f < 4; f++) carry[f] = state[f];
+      if (lane == 0) for (int f = 0; f < 4; f++) cur[f * nseg + seg] = state[f];
+    }
+  }
+}
+
+// the serial chain's counters from the per-cell records: [1] pl/pt < 0, [2] reconstruction failures,
+// [3] Newton iterations
+__global__ __launch_bounds__(256) void k_chain_count(const double* rec, const int* info, long n, unsigned long long* cnt) {
+  __shared__ unsigned long long s[3][256];
+  unsigned long long a = 0, b = 0, it = 0;
+  for (long c = (long)blockIdx.x * 256 + threadIdx.x; c < n; c += (long)gridDim.x * 256) {
+    if (rec[c * NREC + R_KIND] == 0.0) continue;
+    const int v = info[c];
+    it += (unsigned)(v & 0xffff); a += (v >> 16) & 1; b += (v >> 17) & 1;
+  }
+  s[0][threadIdx.x] = a; s[1][threadIdx.x] = b; s[2][threadIdx.x] = it;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o)
+      for (int k = 0; k < 3; k++) s[k][threadIdx.x] += s[k][threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    if (s[0][0]) atomicAdd(&cnt[1], s[0][0]);
+    if (s[1][0]) atomicAdd(&cnt[2], s[1][0]);
+    if (s[2][0]) atomicAdd(&cnt[3], s[2][0]);
+  }
+}
+
 __global__ __launch_bounds__(256) void k_famod_b(PrepArgs A, const double* sol) {
-  const long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= A.n) return;
+  const long c = A.c0 + (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= A.c1) return;
   if (A.rec[c * NREC + R_KIND] == 0.0) return;
   double R[NREC], ain[9], so[6];
 #pragma unroll
@@ -159,21 +337,21 @@ __global__ __launch_bounds__(256) void k_famod_b(PrepArgs A, const double* sol) 
 
 struct RenormArgs {
   PrepConsts k;
-  const double* rec; const double* aux; double* renorm;   // renorm[c][class]
+  const double* rec; const double* aux; double* renorm;   // renorm[c - c0][class]
   const double *mass, *sign, *degen, *baryon;              // sorted species
   const int* rrep;                                         // representative sorted species of each class
-  long n; int npart;                                       // npart = number of classes
+  long c0, n, stride; int npart;                           // cells [c0, c0 + n) of stride held; npart = classes
 };
 
 __global__ __launch_bounds__(256) void k_renorm(RenormArgs A) {
   const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= A.n * A.npart) return;
-  const long c = idx / A.npart;
+  const long c = A.c0 + idx / A.npart;
   const int s = A.rrep[(int)(idx % A.npart)];
   if (A.rec[c * NREC + R_KIND] == 0.0) { A.renorm[idx] = 0.0; return; }
   double aux[9];
 #pragma unroll
-  for (int f = 0; f < 9; f++) aux[f] = A.aux[(long)f * A.n + c];
+  for (int f = 0; f < 9; f++) aux[f] = A.aux[(long)f * A.stride + c];
   A.renorm[idx] = ptm_renorm(A.k, aux, A.mass[s], A.sign[s], A.degen[s], A.baryon[s]);
 }
 
@@ -208,6 +386,7 @@ __global__ __launch_bounds__(1024) void k_fbscan(const double* rec, long n, int*
 struct ReduceArgs {
   const double* slab; long sstride; int nsplit;
   int nbx, npart, npT, nphi, nk, nl, ny_out, kj; long ntask;
+  int spl, npl;               // species per lane (F_S2: 2), species slots per row
   const int* sorig; const double* degen_orig; double prefactor;
   double* out;
 };
@@ -218,15 +397,16 @@ struct ReduceArgs {
 __global__ __launch_bounds__(256) void k_reduce(ReduceArgs A) {
   const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= A.sstride) return;
-  const int KJ = A.kj;
+  const int KJ = A.kj, SK = A.spl * KJ;
   const int lane = (int)(e % kBlock);
-  const int jj = (int)((e / kBlock) % KJ);
-  const long rest = e / ((long)kBlock * KJ);
+  const int slot = (int)((e / kBlock) % SK), jj = slot % KJ;
+  const long rest = e / ((long)kBlock * SK);
   const int lane_group = (int)(rest % A.nbx), ipt = (int)(rest / A.nbx);
   const long task = (long)lane_group * kBlock + lane;
   if (task >= A.ntask) return;
-  const int s = (int)(task % A.npart);
-  const long r = task / A.npart;
+  const int s = A.spl * (int)(task % A.npl) + slot / KJ;
+  if (s >= A.npart) return;
+  const long r = task / A.npl;
   const long nq = (long)A.nk * A.nl;
   const int q = (int)(r % nq);
   if (q % A.nl != 0) return;
@@ -234,8 +414,8 @@ __global__ __launch_bounds__(256) void k_reduce(ReduceArgs A) {
   if (j >= A.nphi) return;
   double acc = 0.0;
   for (int l = 0; l < A.nl; l++) {
-    const long tl = task + (long)l * A.npart;
-    const long el = ((long)ipt * A.nbx + tl / kBlock) * ((long)KJ * kBlock) + (long)jj * kBlock + tl % kBlock;
+    const long tl = task + (long)l * A.npl;
+    const long el = ((long)ipt * A.nbx + tl / kBlock) * ((long)SK * kBlock) + (long)slot * kBlock + tl % kBlock;
     for (int z = 0; z < A.nsplit; z++) acc += A.slab[(long)z * A.sstride + el];
   }
   const int so = A.sorig[s];
@@ -256,15 +436,15 @@ __global__ __launch_bounds__(256) void k_reduce_wave(ReduceArgs A) {
   const int j = (int)(r1 % A.nphi);
   const long r2 = r1 / A.nphi;
   const int ipt = (int)(r2 % A.npT), s = (int)(r2 / A.npT);
-  const int KJ = A.kj, jb = j / KJ, jj = j % KJ;
+  const int KJ = A.kj, jb = j / KJ, jj = j % KJ, SK = A.spl * KJ, slot = (s % A.spl) * KJ + jj;
   const long nq = (long)A.nk * A.nl;
-  const long task0 = s + (long)A.npart * (k * A.nl + nq * jb);
+  const long task0 = s / A.spl + (long)A.npl * (k * A.nl + nq * jb);
   const long nterm = (long)A.nl * A.nsplit;
   double acc = 0.0;
   for (long m = lane; m < nterm; m += 64) {
     const int l = (int)(m / A.nsplit), z = (int)(m % A.nsplit);
-    const long tl = task0 + (long)l * A.npart;
-    const long el = ((long)ipt * A.nbx + tl / kBlock) * ((long)KJ * kBlock) + (long)jj * kBlock + tl % kBlock;
+    const long tl = task0 + (long)l * A.npl;
+    const long el = ((long)ipt * A.nbx + tl / kBlock) * ((long)SK * kBlock) + (long)slot * kBlock + tl % kBlock;
     acc += A.slab[(long)z * A.sstride + el];
   }
 #pragma unroll
@@ -463,6 +643,11 @@ T* dalloc(size_t count) {
 struct is3d_engine {
   int device = 0;
   std::string err;
+  // is3d_create_devices: the shard engines and their reduction (group.hip); every entry point forwards
+  is3d::Group* grp = nullptr;
+  // cell window [win_lo, win_hi) of the held surface that k_spectra integrates (-1: every cell); set by a
+  // group whose shards hold the whole surface for the PTMA warm-start chains
+  long win_lo = -1, win_hi = -1;
   bool have_params = false, have_species = false, have_pdg = false, have_grid = false, have_gla = false, have_df = false;
   is3d_params p{};
   // species (original order) and mass-sorted permutation
@@ -502,6 +687,7 @@ struct is3d_engine {
   int* d_rrep = nullptr;
   int nrcls = 0;
   double* d_surf = nullptr; bool surf_owned = false; long ncell = 0; long surf_cap = 0;
+  double* d_chain = nullptr; long chain_cap = 0;   // PTMA warm-start chain segments (k_chain_pass)
   double *d_rec = nullptr, *d_aux = nullptr, *d_sol = nullptr, *d_renorm = nullptr, *d_slab = nullptr, *d_out = nullptr;
   long rec_cap = 0, aux_cap = 0, sol_cap = 0, renorm_cap = 0, slab_cap = 0, out_cap = 0;
   int* d_fb = nullptr;        // modified modes: [0] fallback cell count, [1..] k_fbscan's cell list
@@ -533,6 +719,11 @@ static void dfree(void* p) { if (p) (void)hipFree(p); }
 
 extern "C" int is3d_abi_version(void) { return IS3D_ABI_VERSION; }
 
+#ifndef IS3D_BUILD_ID
+#define IS3D_BUILD_ID "unknown"
+#endif
+extern "C" const char* is3d_build_id(void) { return IS3D_BUILD_ID; }
+
 extern "C" is3d_engine* is3d_create(int device) {
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0 || device < 0 || device >= ndev) return nullptr;
@@ -549,10 +740,16 @@ extern "C" is3d_engine* is3d_create(int device) {
 
 extern "C" void is3d_destroy(is3d_engine* e) {
   if (!e) return;
+  if (e->grp) {
+    is3d::group_destroy(e->grp);
+    delete e;
+    return;
+  }
   (void)hipSetDevice(e->device);
   (void)hipDeviceSynchronize();
   dfree(e->d_tables); dfree(e->d_const);
   if (e->surf_owned) dfree(e->d_surf);
+  dfree(e->d_chain);
   dfree(e->d_rec); dfree(e->d_aux); dfree(e->d_sol); dfree(e->d_renorm); dfree(e->d_slab); dfree(e->d_out);
   dfree(e->d_fb);
   dfree(e->d_ycell); dfree(e->d_part); dfree(e->d_keys); dfree(e->d_perm); dfree(e->d_offs);
@@ -561,9 +758,32 @@ extern "C" void is3d_destroy(is3d_engine* e) {
   delete e;
 }
 
-extern "C" const char* is3d_last_error(const is3d_engine* e) { return e ? e->err.c_str() : "null engine"; }
+extern "C" const char* is3d_last_error(const is3d_engine* e) {
+  if (!e) return "null engine";
+  return e->grp ? is3d::group_error(e->grp) : e->err.c_str();
+}
+
+extern "C" is3d_engine* is3d_create_devices(int n, const int* devices) {
+  std::string err;
+  is3d::Group* g = is3d::group_create(n, devices, err);
+  if (!g) return nullptr;
+  is3d_engine* e = new is3d_engine();
+  e->device = devices[0];
+  e->grp = g;
+  return e;
+}
+
+extern "C" int is3d_set_cell_window(is3d_engine* e, long lo, long hi) {
+  if (!e) return IS3D_ERR_ARG;
+  if (e->grp) return e->fail(IS3D_ERR_UNSUPPORTED, "a device-list engine places its own windows");
+  if (lo < 0 || hi < 0) { e->win_lo = e->win_hi = -1; return IS3D_OK; }
+  if (lo > hi || hi > e->ncell) return e->fail(IS3D_ERR_ARG, "cell window outside the surface");
+  e->win_lo = lo; e->win_hi = hi;
+  return IS3D_OK;
+}
 
 extern "C" int is3d_set_params(is3d_engine* e, const is3d_params* p) {
+  if (e && e->grp) return p ? is3d::group_set_params(e->grp, p) : IS3D_ERR_ARG;
   if (!e || !p) return IS3D_ERR_ARG;
   // operation 2 is accepted for its oversampling estimate (is3d_total_yield); the sampler itself is not on this path
   if (p->operation < 0 || p->operation > 2)
@@ -580,6 +800,7 @@ extern "C" int is3d_set_params(is3d_engine* e, const is3d_params* p) {
 
 extern "C" int is3d_set_species(is3d_engine* e, int n, const double* mass, const double* sign, const double* degeneracy,
                                 const double* baryon) {
+  if (e && e->grp) return is3d::group_set_species(e->grp, n, mass, sign, degeneracy, baryon);
   if (!e || n <= 0 || !mass || !sign || !degeneracy || !baryon) return e ? e->fail(IS3D_ERR_ARG, "bad species arrays") : IS3D_ERR_ARG;
   e->mass.assign(mass, mass + n); e->sign.assign(sign, sign + n); e->degen.assign(degeneracy, degeneracy + n);
   e->baryon.assign(baryon, baryon + n);
@@ -595,6 +816,7 @@ extern "C" int is3d_set_species(is3d_engine* e, int n, const double* mass, const
 
 extern "C" int is3d_set_pdg(is3d_engine* e, int n, const double* mass, const double* sign, const double* degeneracy,
                             const double* baryon) {
+  if (e && e->grp) return is3d::group_set_pdg(e->grp, n, mass, sign, degeneracy, baryon);
   if (!e || n <= 0 || !mass || !sign || !degeneracy || !baryon) return e ? e->fail(IS3D_ERR_ARG, "bad pdg arrays") : IS3D_ERR_ARG;
   e->pdg_mass.assign(mass, mass + n); e->pdg_sign.assign(sign, sign + n); e->pdg_degen.assign(degeneracy, degeneracy + n);
   e->pdg_baryon.assign(baryon, baryon + n);
@@ -605,6 +827,7 @@ extern "C" int is3d_set_pdg(is3d_engine* e, int n, const double* mass, const dou
 
 extern "C" int is3d_set_momentum_grid(is3d_engine* e, int npT, const double* pT, int nphi, const double* phi, int ny,
                                       const double* y, int neta, const double* eta, const double* eta_weight) {
+  if (e && e->grp) return is3d::group_set_momentum_grid(e->grp, npT, pT, nphi, phi, ny, y, neta, eta, eta_weight);
   if (!e) return IS3D_ERR_ARG;
   if (npT <= 0 || nphi <= 0 || !pT || !phi) return e->fail(IS3D_ERR_ARG, "empty pT/phi table");
   e->pT.assign(pT, pT + npT); e->phi.assign(phi, phi + nphi);
@@ -617,6 +840,7 @@ extern "C" int is3d_set_momentum_grid(is3d_engine* e, int npT, const double* pT,
 }
 
 extern "C" int is3d_set_momentum_weights(is3d_engine* e, const double* pT_weight, const double* phi_weight) {
+  if (e && e->grp) return is3d::group_set_momentum_weights(e->grp, pT_weight, phi_weight);
   if (!e) return IS3D_ERR_ARG;
   if (!e->have_grid) return e->fail(IS3D_ERR_STATE, "is3d_set_momentum_grid not called");
   if (!pT_weight || !phi_weight) return e->fail(IS3D_ERR_ARG, "null pT/phi weights");
@@ -628,6 +852,7 @@ extern "C" int is3d_set_momentum_weights(is3d_engine* e, const double* pT_weight
 }
 
 extern "C" int is3d_set_spacetime_bins(is3d_engine* e, const is3d_spacetime_bins* b) {
+  if (e && e->grp) return b ? is3d::group_set_spacetime_bins(e->grp, b) : IS3D_ERR_ARG;
   if (!e || !b) return IS3D_ERR_ARG;
   if (b->tau_bins <= 0 || b->r_bins <= 0 || b->phip_bins <= 0) return e->fail(IS3D_ERR_ARG, "spacetime bins must be positive");
   if (!(b->tau_max > b->tau_min) || !(b->r_max > b->r_min)) return e->fail(IS3D_ERR_ARG, "spacetime bin ranges must be increasing");
@@ -638,6 +863,7 @@ extern "C" int is3d_set_spacetime_bins(is3d_engine* e, const is3d_spacetime_bins
 }
 
 extern "C" int is3d_set_gauss_laguerre(is3d_engine* e, int alpha, int points, const double* roots, const double* weights) {
+  if (e && e->grp) return is3d::group_set_gauss_laguerre(e->grp, alpha, points, roots, weights);
   if (!e) return IS3D_ERR_ARG;
   if (alpha < 3 || points <= 0 || !roots || !weights) return e->fail(IS3D_ERR_ARG, "Gauss-Laguerre table needs alpha >= 3");
   e->gla_alpha = alpha; e->gla_pts = points;
@@ -650,6 +876,7 @@ extern "C" int is3d_set_gauss_laguerre(is3d_engine* e, int alpha, int points, co
 
 extern "C" int is3d_set_df_tables(is3d_engine* e, int nT, int nmuB, const double* T, const double* muB,
                                   const double* tables, double T_avg) {
+  if (e && e->grp) return is3d::group_set_df_tables(e->grp, nT, nmuB, T, muB, tables, T_avg);
   if (!e) return IS3D_ERR_ARG;
   if (nT < 3 || nmuB < 1 || !T || !muB || !tables) return e->fail(IS3D_ERR_ARG, "bad df coefficient tables");
   e->nT = nT; e->nmuB = nmuB;
@@ -704,6 +931,7 @@ static int device_jonah_table(is3d_engine* e, const double* r2, const double* w2
 // pT sin} table finalize_tables builds for KJ-padded phi rows)
 struct SpectraPlan {
   int KJ, njb, nq, nqmax, tb, ly, t8, tile;
+  int s2, spl, npl;           // F_S2 (two species per lane), species per lane, species slots per row
   size_t shmem;
   size_t shmem_fb;            // modified modes: the F_FB launch (8-cell tiles, per-lane y-term rows, no q tables)
 };
@@ -713,12 +941,13 @@ static SpectraPlan spectra_plan(const is3d_engine* e) {
   const int np = (int)e->mass.size(), nphi = (int)e->phi.size();
   const int nk = (dim == 3) ? (int)e->y.size() : 1, nl = (dim == 3) ? 1 : (int)e->eta.size();
   P.nq = nk * nl;
+  P.spl = 1; P.npl = np; P.s2 = 0;
   auto shape = [&](int KJ) {
     P.KJ = KJ;
     P.njb = (nphi + KJ - 1) / KJ;
     // rows (r = q + nq jb) one workgroup's 256 consecutive tasks can span: a contiguous range of at most
-    // (kBlock - 1) / np + 2 of the nq njb rows
-    P.nqmax = (int)std::min<long>((long)P.nq * P.njb, (kBlock - 1) / np + 2);
+    // (kBlock - 1) / npl + 2 of the nq njb rows
+    P.nqmax = (int)std::min<long>((long)P.nq * P.njb, (kBlock - 1) / P.npl + 2);
     // Grad {PD, T1} table (F_TB, sep_quad_tb_t): exact only without baryon terms (R_SCB = R_SSB = 0:
     // V^mu and alphaB are only packed when include_baryon && include_baryondiff_deltaf (prep_grad_ce), and
     // df_eval leaves c1 = c3 = 0 without baryons); needs phi blocks of fours and at most kTbQ rows per
@@ -745,6 +974,14 @@ static SpectraPlan spectra_plan(const is3d_engine* e) {
 #else
   shape(spectra_kj_fill(nphi, (long)np * P.nq));
 #endif
+  // Grad table launch with two species per lane (F_S2, KJ = 16): phi tables in blocks of 16 and >= 86 species
+  // pairs, so a workgroup still spans <= kTbQ q rows
+  if (IS3D_TB2 && mode == GRAD && P.tb && nphi % 16 == 0 && (np + 1) / 2 >= 86) {
+    P.spl = 2; P.npl = (np + 1) / 2;
+    shape(16);
+    if (P.tb) P.s2 = F_S2;
+    else { P.spl = 1; P.npl = np; shape(spectra_kj_fill(nphi, (long)np * P.nq)); }
+  }
   P.ly = 0;
   P.shmem = lds_bytes(P.nqmax);
   // the modified path's 16-cell tiles fall back to 8 (F_T8) before giving up the q-row tables
@@ -875,7 +1112,10 @@ static int finalize_tables(is3d_engine* e) {
   // (MomentumSpectra.cpp:1295); the integrands depend on a hadron's (mass, sign) only, times its
   // degeneracy, so hadrons with identical (mass, sign) are merged with summed degeneracies (SMASH:
   // 320 -> 92, UrQMD: 320 -> 83; first-occurrence order).  Only the FP summation order changes, as it
-  // already does in the lane-strided sums (the Newton iteration counts still match the oracle's).
+  // already does in the lane-strided sums.  Checked on the breakdown-heavy chain (bulk x10, one chain,
+  // tests/test_gpu_configs.py::test_modified_fallback_launch): the merged GPU solve and the unmerged
+  // oracle take the same 894 Newton steps and agree to 3e-13; tests/test_kernel_math_cpu.py compares
+  // merged and per-hadron sums of the same device math directly (cf_emulator variant bit 8).
   std::vector<double> am, as, ag;
   {
     const int nh = std::min(320, (int)e->pdg_mass.size());
@@ -930,6 +1170,7 @@ static int finalize_tables(is3d_engine* e) {
 }
 
 extern "C" int is3d_set_surface(is3d_engine* e, long n, const is3d_surface* s) {
+  if (e && e->grp) return is3d::group_set_surface(e->grp, n, s);
   if (!e || !s || n < 0) return e ? e->fail(IS3D_ERR_ARG, "bad surface") : IS3D_ERR_ARG;
   HIPCHK(e, hipSetDevice(e->device));
   const double* fields[NSURF] = {s->tau, s->x, s->y, s->eta, s->dat, s->dax, s->day, s->dan, s->ux, s->uy, s->un,
@@ -945,6 +1186,7 @@ extern "C" int is3d_set_surface(is3d_engine* e, long n, const is3d_surface* s) {
     e->surf_cap = n;
   }
   e->ncell = n;
+  e->win_lo = e->win_hi = -1;
   if (n == 0) return IS3D_OK;
   for (int f = 0; f < NSURF; f++) {
     double* dst = e->d_surf + (size_t)f * n;
@@ -955,16 +1197,36 @@ extern "C" int is3d_set_surface(is3d_engine* e, long n, const is3d_surface* s) {
 }
 
 extern "C" int is3d_set_surface_device(is3d_engine* e, long n, const double* dev_fields) {
+  if (e && e->grp) return is3d::group_set_surface_device(e->grp, n, dev_fields);
   if (!e || n < 0 || (!dev_fields && n > 0)) return e ? e->fail(IS3D_ERR_ARG, "bad device surface") : IS3D_ERR_ARG;
   if (e->surf_owned) dfree(e->d_surf);
   e->surf_owned = false;
   e->surf_cap = 0;
   e->d_surf = const_cast<double*>(dev_fields);
   e->ncell = n;
+  e->win_lo = e->win_hi = -1;
+  return IS3D_OK;
+}
+
+extern "C" int is3d_internal_copy_surface(is3d_engine* e, long n, const double* src, long src_n, int src_device, long lo) {
+  if (!e || e->grp || n < 0 || lo < 0 || lo + n > src_n || (!src && n > 0)) return e ? e->fail(IS3D_ERR_ARG, "bad surface copy") : IS3D_ERR_ARG;
+  HIPCHK(e, hipSetDevice(e->device));
+  if (!e->surf_owned || e->surf_cap < n) {
+    if (e->surf_owned) dfree(e->d_surf);
+    e->d_surf = dalloc<double>((size_t)NSURF * std::max(n, 1L));
+    if (!e->d_surf) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(surface) failed");
+    e->surf_owned = true;
+    e->surf_cap = n;
+  }
+  e->ncell = n;
+  e->win_lo = e->win_hi = -1;
+  for (int f = 0; f < NSURF && n > 0; f++)
+    HIPCHK(e, hipMemcpyPeer(e->d_surf + (size_t)f * n, e->device, src + (size_t)f * src_n + lo, src_device, n * sizeof(double)));
   return IS3D_OK;
 }
 
 extern "C" long is3d_output_size(const is3d_engine* e) {
+  if (e && e->grp) return is3d::group_output_size(e->grp);
   if (!e || !e->have_species || !e->have_grid || !e->have_params) return -1;
   const long ny = (e->p.dimension == 3) ? (long)e->y.size() : 1;
   return (long)e->mass.size() * (long)e->pT.size() * (long)e->phi.size() * ny;
@@ -997,6 +1259,7 @@ static PrepConsts make_consts(const is3d_engine* e) {
 }
 
 extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
+  if (e && e->grp) return is3d::group_launch(e->grp, dev_out, stream);
   if (!e) return IS3D_ERR_ARG;
   int rc = finalize_tables(e);
   if (rc) return rc;
@@ -1009,12 +1272,17 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   const int np = (int)e->mass.size(), npT = (int)e->pT.size(), nphi = (int)e->phi.size();
   const int ny_out = (dim == 3) ? (int)e->y.size() : 1;
   const int nk = ny_out, nl = (dim == 3) ? 1 : (int)e->eta.size();
+  // cell window (group shards holding the whole surface): k_spectra integrates [wlo, whi); the prepass covers
+  // the window too, except for PTMA's warm-start chains, which walk every cell (MomentumSpectra.cpp:1308-1364)
+  const long wlo = e->win_hi >= 0 ? e->win_lo : 0, whi = e->win_hi >= 0 ? e->win_hi : n, nw = whi - wlo;
+  const bool chained = mode == PTMA && e->p.famod_chains > 0;
+  const long p0 = chained ? 0 : wlo, p1 = chained ? n : whi;
   e->st = is3d_stats{};
-  e->st.cells = n;
+  e->st.cells = nw;
   HIPCHK(e, hipMemsetAsync(e->d_err, 0, sizeof(int), st));
   HIPCHK(e, hipMemsetAsync(e->d_cnt, 0, 8 * sizeof(unsigned long long), st));
   HIPCHK(e, hipEventRecord(e->ev[0], st));
-  if (n == 0) {
+  if (nw == 0) {
     HIPCHK(e, hipMemsetAsync(dev_out, 0, outsize * sizeof(double), st));
     HIPCHK(e, hipEventRecord(e->ev[1], st));
     HIPCHK(e, hipEventRecord(e->ev[2], st));
@@ -1027,8 +1295,9 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   if (mode == PTMA && !ensure(e->d_sol, e->sol_cap, 6L * n)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(sol) failed");
   PrepArgs pa{};
   pa.k = make_consts(e); pa.tb = e->dtb; pa.surf = e->d_surf; pa.rec = e->d_rec; pa.aux = e->d_aux; pa.n = n;
+  pa.c0 = p0; pa.c1 = p1;
   pa.err = e->d_err; pa.cnt = e->d_cnt;
-  const dim3 g1((unsigned)((n + 255) / 256)), b1(256);
+  const dim3 g1((unsigned)std::max(1L, (p1 - p0 + 255) / 256)), b1(256);
   switch (mode) {
     case GRAD: hipLaunchKernelGGL(k_prep<GRAD>, g1, b1, 0, st, pa); break;
     case CE: hipLaunchKernelGGL(k_prep<CE>, g1, b1, 0, st, pa); break;
@@ -1039,69 +1308,108 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   HIPCHK(e, hipGetLastError());
   if (mode == PTMA) {
     AnisoArgs aa{};
-    aa.rec = e->d_rec; aa.ain = e->d_aux; aa.sol = e->d_sol; aa.n = n;
-    aa.chains = (e->p.famod_chains > 0) ? std::min<long>(e->p.famod_chains, n) : n;
+    aa.rec = e->d_rec; aa.ain = e->d_aux; aa.sol = e->d_sol; aa.stride = n;
+    aa.c0 = p0; aa.n = p1 - p0;
+    aa.chains = chained ? std::min<long>(e->p.famod_chains, n) : std::max(1L, p1 - p0);
     const int nh = e->n_aniso_h;
     aa.h = Hadrons{nh, e->d_aniso_h, e->d_aniso_h + nh, e->d_aniso_h + 2 * nh};
     aa.fp2 = 4.0 * std::pow(M_PI, 2) * std::pow(kHbarC, 3);
     aa.cnt = e->d_cnt;
-    hipLaunchKernelGGL(k_aniso, dim3((unsigned)aa.chains), dim3(64), 0, st, aa);
-    HIPCHK(e, hipGetLastError());
+    if (!chained) {
+      hipLaunchKernelGGL(k_aniso, dim3((unsigned)aa.chains), dim3(64), 0, st, aa);
+      HIPCHK(e, hipGetLastError());
+    } else {
+      // warm-start chains in parallel segments (k_chain_pass): ~16k segments keep the GPU full
+      ChainArgs ca{};
+      ca.rec = e->d_rec; ca.ain = e->d_aux; ca.sol = e->d_sol; ca.n = n; ca.C = aa.chains; ca.h = aa.h; ca.fp2 = aa.fp2;
+      const long P = (n + ca.C - 1) / ca.C;
+      ca.L = std::max(32L, (n + 16383) / 16384);
+      ca.nspc = (P + ca.L - 1) / ca.L;
+      const long nseg = ca.C * ca.nspc;
+      const long need = 4 * n + (n + 1) / 2 + 12 * nseg + kChainPasses;
+      if (!ensure(e->d_chain, e->chain_cap, need)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(chain state) failed");
+      ca.sta = e->d_chain; ca.info = (int*)(e->d_chain + 4 * n);
+      ca.send = e->d_chain + 4 * n + (n + 1) / 2; ca.sstart = ca.send + 8 * nseg;
+      ca.changed = (int*)(ca.sstart + 4 * nseg);
+      HIPCHK(e, hipMemsetAsync(ca.changed, 0, kChainPasses * sizeof(int), st));
+      for (int pass = 0; pass < kChainPasses; pass++)
+        hipLaunchKernelGGL(k_chain_pass, dim3((unsigned)nseg), dim3(64), 0, st, ca, pass);
+      hipLaunchKernelGGL(k_chain_finish, dim3(1), dim3(64), 0, st, ca);
+      hipLaunchKernelGGL(k_chain_count, dim3((unsigned)std::min(1024L, (n + 255) / 256)), dim3(256), 0, st,
+                         (const double*)e->d_rec, (const int*)ca.info, n, e->d_cnt);
+      HIPCHK(e, hipGetLastError());
+    }
     hipLaunchKernelGGL(k_famod_b, g1, b1, 0, st, pa, (const double*)e->d_sol);
     HIPCHK(e, hipGetLastError());
   }
   if (mode == PTM) {
-    if (!ensure(e->d_renorm, e->renorm_cap, n * (long)e->nrcls)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(renorm) failed");
+    if (!ensure(e->d_renorm, e->renorm_cap, nw * (long)e->nrcls)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(renorm) failed");
     RenormArgs ra{};
     ra.k = pa.k; ra.rec = e->d_rec; ra.aux = e->d_aux; ra.renorm = e->d_renorm;
-    ra.mass = e->d_smass; ra.sign = e->d_ssign; ra.degen = e->d_sdegen; ra.baryon = e->d_sbaryon; ra.n = n;
+    ra.mass = e->d_smass; ra.sign = e->d_ssign; ra.degen = e->d_sdegen; ra.baryon = e->d_sbaryon;
+    ra.c0 = wlo; ra.n = nw; ra.stride = n;
     ra.npart = e->nrcls; ra.rrep = e->d_rrep;
-    const long tot = n * (long)e->nrcls;
-    hipLaunchKernelGGL(k_renorm, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, ra);
+    const long tot = nw * (long)e->nrcls;
+    hipLaunchKernelGGL(k_renorm, dim3((unsigned)std::max(1L, (tot + 255) / 256)), dim3(256), 0, st, ra);
     HIPCHK(e, hipGetLastError());
   }
   HIPCHK(e, hipEventRecord(e->ev[1], st));
+  // the integral and the reduction see the window only: records from wlo on, nw cells
+  const double* rec_w = e->d_rec + wlo * (long)NREC;
   // --- main integral
   const SpectraPlan P = spectra_plan(e);
   const int KJ = P.KJ, njb = P.njb;
+  if (!spectra_kj_supported(KJ) && !(P.s2 && KJ == 16))
+    return e->fail(IS3D_ERR_ARG, "internal: no k_spectra instantiation for this phi block");
+  const int spl = P.spl, npl = P.npl;
   if (P.shmem > 160 * 1024) return e->fail(IS3D_ERR_ARG, "momentum grid too large for the LDS tile (phi table)");
-  const long ntask = (long)np * nk * nl * njb;
+  const long ntask = (long)npl * nk * nl * njb;
   const long bx = (ntask + kBlock - 1) / kBlock;
+  if (!P.ly) {
+    // k_spectra's LDS row tables hold nqmax rows per cell; a lane group spanning more would compute nothing
+    // (its slab is NaN-filled, rows_ok), so refuse the launch here instead of returning NaN spectra
+    for (long g = 0; g < bx; g++) {
+      const long t0 = g * kBlock, t1 = std::min(ntask, t0 + kBlock) - 1;
+      if (t1 / npl - t0 / npl + 1 > P.nqmax)
+        return e->fail(IS3D_ERR_ARG, "internal: k_spectra lane group spans more q rows than the LDS plan");
+    }
+  }
   const long wgs = bx * npT;
   // cell splits: enough workgroups to fill the chip (>= 8k), and each split's records small enough
   // (~2 MB) to stay in one XCD's 4 MB L2 while that XCD's workgroups stream them; a multiple of 8
   // so every XCD owns whole splits; at most IS3D_MAX_SPLITS slabs (each one output-sized)
   const long kTile = P.tile;                              // cells per tile of this mode's k_spectra
-  const long max_split = (n + kTile - 1) / kTile;
+  const long max_split = std::max(1L, (nw + kTile - 1) / kTile);
   const long by_fill = (8192 + wgs - 1) / wgs;
-  const long by_l2 = ((long)NREC * 8 * n + IS3D_SPLIT_BYTES - 1) / IS3D_SPLIT_BYTES;
+  const long by_l2 = ((long)NREC * 8 * nw + IS3D_SPLIT_BYTES - 1) / IS3D_SPLIT_BYTES;
   long nsplit = std::max(by_fill, std::min(by_l2, (long)IS3D_MAX_SPLITS));
   if (nsplit >= 8) nsplit = (nsplit + 7) / 8 * 8;
   nsplit = std::max(1L, std::min(nsplit, max_split));
-  long cps = (n + nsplit - 1) / nsplit;
+  long cps = std::max(1L, (nw + nsplit - 1) / nsplit);
   cps = ((cps + kTile - 1) / kTile) * kTile;
-  nsplit = (n + cps - 1) / cps;
-  const long sstride = (long)npT * bx * KJ * kBlock;
+  nsplit = std::max(1L, (nw + cps - 1) / cps);
+  const long sstride = (long)npT * bx * spl * KJ * kBlock;
   // modified modes: the F_FB launch (separable-fallback lanes, cells listed by k_fbscan) writes its own
   // nsplit_fb slabs after the main ones; k_reduce sums both
   const long nsplit_fb = (mode >= PTM) ? std::max(1L, std::min(nsplit, 8L)) : 0;
   if (!ensure(e->d_slab, e->slab_cap, (nsplit + nsplit_fb) * sstride)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(slabs) failed");
   if (mode >= PTM) {
-    if (!ensure(e->d_fb, e->fb_cap, n + 1)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(fallback list) failed");
-    hipLaunchKernelGGL(k_fbscan, dim3(1), dim3(1024), 0, st, (const double*)e->d_rec, n, e->d_fb + 1, e->d_fb);
+    if (!ensure(e->d_fb, e->fb_cap, nw + 1)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(fallback list) failed");
+    hipLaunchKernelGGL(k_fbscan, dim3(1), dim3(1024), 0, st, rec_w, nw, e->d_fb + 1, e->d_fb);
     HIPCHK(e, hipGetLastError());
   }
   SpecArgs sa{};
-  sa.rec = e->d_rec; sa.n = n; sa.renorm = e->d_renorm; sa.rcls = e->d_rcls; sa.nrcls = e->nrcls; sa.slab = e->d_slab; sa.outsize = outsize;
+  sa.rec = rec_w; sa.n = nw; sa.renorm = e->d_renorm; sa.rcls = e->d_rcls; sa.nrcls = e->nrcls; sa.slab = e->d_slab; sa.outsize = outsize;
   sa.smass = e->d_smass; sa.ssign = e->d_ssign; sa.sbaryon = e->d_sbaryon; sa.sorig = e->d_sorig;
   sa.csg = e->d_csg;
   sa.pT = e->d_pT; sa.cphi = e->d_cphi; sa.sphi = e->d_sphi; sa.yv = e->d_y; sa.etav = e->d_eta; sa.etaw = e->d_etaw;
   sa.npart = np; sa.npT = npT; sa.nphi = nphi; sa.ny_out = ny_out; sa.nk = nk; sa.nl = nl; sa.nq = nk * nl; sa.njb = njb;
+  sa.npl = npl;
   sa.nqmax = P.nqmax;
   sa.ntask = ntask; sa.cells_per_split = cps; sa.nbx = (int)bx; sa.nsplit = (int)nsplit; sa.sstride = sstride;
   sa.regulate = e->p.regulate_deltaf; sa.outflow = e->p.outflow; sa.dim = dim; sa.op = 1;
   const size_t shmem = P.shmem;
-  const int tb = P.tb | P.ly | P.t8;
+  const int tb = P.tb | P.ly | P.t8 | P.s2;
   const dim3 grid((unsigned)(bx * npT * nsplit));
   const int kflags = (e->p.regulate_deltaf ? F_REG : 0) | (e->p.outflow ? F_OUT : 0) | tb;
   switch (mode) {
@@ -1129,6 +1437,7 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   ReduceArgs ra{};
   ra.slab = e->d_slab; ra.sstride = sstride; ra.nsplit = (int)(nsplit + nsplit_fb);
   ra.nbx = (int)bx; ra.npart = np; ra.npT = npT; ra.nphi = nphi; ra.nk = nk; ra.nl = nl; ra.ny_out = ny_out; ra.kj = KJ;
+  ra.spl = spl; ra.npl = npl;
   ra.ntask = ntask;
   ra.sorig = e->d_sorig; ra.degen_orig = e->d_degen_orig; ra.prefactor = std::pow(2.0 * M_PI * kHbarC, -3);
   ra.out = dev_out;
@@ -1146,6 +1455,7 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
 }
 
 extern "C" int is3d_finish(is3d_engine* e) {
+  if (e && e->grp) return is3d::group_finish(e->grp);
   if (!e) return IS3D_ERR_ARG;
   if (!e->launched) return e->fail(IS3D_ERR_STATE, "nothing launched");
   HIPCHK(e, hipSetDevice(e->device));
@@ -1170,6 +1480,7 @@ extern "C" int is3d_finish(is3d_engine* e) {
 }
 
 extern "C" int is3d_calculate_spectra(is3d_engine* e, double* dN_out) {
+  if (e && e->grp) return is3d::group_calculate_spectra(e->grp, dN_out);
   if (!e || !dN_out) return e ? e->fail(IS3D_ERR_ARG, "null output") : IS3D_ERR_ARG;
   int rc = finalize_tables(e);
   if (rc) return rc;
@@ -1187,6 +1498,7 @@ extern "C" int is3d_calculate_spectra(is3d_engine* e, double* dN_out) {
 // into thread slices; the host then applies the reference's per-species reset (byte-count memset,
 // :165-167 / :628-630) and writes the bin-normalised distributions (:407-440).
 extern "C" int is3d_calculate_dN_dX(is3d_engine* e, double* dN_taudtaudy, double* dN_2pirdrdy, double* dN_dphidy) {
+  if (e && e->grp) return is3d::group_calculate_dN_dX(e->grp, dN_taudtaudy, dN_2pirdrdy, dN_dphidy);
   if (!e) return IS3D_ERR_ARG;
   if (!dN_taudtaudy || !dN_2pirdrdy || !dN_dphidy) return e->fail(IS3D_ERR_ARG, "null output");
   if (!e->have_params) return e->fail(IS3D_ERR_STATE, "is3d_set_params not called");
@@ -1218,6 +1530,7 @@ extern "C" int is3d_calculate_dN_dX(is3d_engine* e, double* dN_taudtaudy, double
     PrepArgs pa{};
     pa.k = make_consts(e); pa.k.operation = 0;
     pa.tb = e->dtb; pa.surf = e->d_surf; pa.rec = e->d_rec; pa.aux = e->d_aux; pa.n = n;
+    pa.c0 = 0; pa.c1 = n;
     pa.err = e->d_err; pa.cnt = e->d_cnt;
     const dim3 g1((unsigned)((n + 255) / 256)), b1(256);
     switch (mode) {
@@ -1231,8 +1544,9 @@ extern "C" int is3d_calculate_dN_dX(is3d_engine* e, double* dN_taudtaudy, double
       if (!ensure(e->d_renorm, e->renorm_cap, n * (long)e->nrcls)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(renorm) failed");
       RenormArgs ra{};
       ra.k = pa.k; ra.rec = e->d_rec; ra.aux = e->d_aux; ra.renorm = e->d_renorm;
-      ra.mass = e->d_smass; ra.sign = e->d_ssign; ra.degen = e->d_sdegen; ra.baryon = e->d_sbaryon; ra.n = n;
-    ra.npart = e->nrcls; ra.rrep = e->d_rrep;
+      ra.mass = e->d_smass; ra.sign = e->d_ssign; ra.degen = e->d_sdegen; ra.baryon = e->d_sbaryon;
+      ra.c0 = 0; ra.n = n; ra.stride = n;
+      ra.npart = e->nrcls; ra.rrep = e->d_rrep;
       const long tot = n * (long)e->nrcls;
       hipLaunchKernelGGL(k_renorm, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, st, ra);
       HIPCHK(e, hipGetLastError());
@@ -1365,6 +1679,7 @@ extern "C" int is3d_calculate_dN_dX(is3d_engine* e, double* dN_taudtaudy, double
 }
 
 extern "C" int is3d_get_cell_yields(const is3d_engine* e, double* dN_dy_cell) {
+  if (e && e->grp) return is3d::group_get_cell_yields(e->grp, dN_dy_cell);
   if (!e || !dN_dy_cell) return IS3D_ERR_ARG;
   if (e->ycell_n < 0) return IS3D_ERR_STATE;
   const long n = e->ycell_n;
@@ -1382,6 +1697,7 @@ extern "C" int is3d_get_cell_yields(const is3d_engine* e, double* dN_dy_cell) {
 }
 
 extern "C" int is3d_get_stats(const is3d_engine* e, is3d_stats* out) {
+  if (e && e->grp) return out ? is3d::group_get_stats(e->grp, out) : IS3D_ERR_ARG;
   if (!e || !out) return IS3D_ERR_ARG;
   *out = e->st;
   return IS3D_OK;
@@ -1389,6 +1705,7 @@ extern "C" int is3d_get_stats(const is3d_engine* e, is3d_stats* out) {
 
 extern "C" int is3d_evaluate_df_coefficients(is3d_engine* e, double T, double muB, double E, double P, double bulkPi,
                                              double* out15) {
+  if (e && e->grp) return out15 ? is3d::group_evaluate_df_coefficients(e->grp, T, muB, E, P, bulkPi, out15) : IS3D_ERR_ARG;
   if (!e || !out15) return IS3D_ERR_ARG;
   int rc = finalize_tables(e);
   if (rc) return rc;
@@ -1409,6 +1726,7 @@ extern "C" int is3d_evaluate_df_coefficients(is3d_engine* e, double T, double mu
 
 extern "C" int is3d_total_yield(is3d_engine* e, const double* plasma, double y_cut, double* n_total,
                                 double* densities) {
+  if (e && e->grp) return is3d::group_total_yield(e->grp, plasma, y_cut, n_total, densities);
   if (!e || !plasma || !n_total) return IS3D_ERR_ARG;
   int rc = finalize_tables(e);
   if (rc) return rc;
@@ -1456,6 +1774,7 @@ extern "C" int is3d_total_yield(is3d_engine* e, const double* plasma, double y_c
 }
 
 extern "C" int is3d_get_jonah_table(const is3d_engine* e, double* l2, double* z, double* bp, double* bpmax) {
+  if (e && e->grp) return is3d::group_get_jonah_table(e->grp, l2, z, bp, bpmax);
   if (!e || e->jx.size() != 301) return IS3D_ERR_STATE;
   std::copy(e->jl2.begin(), e->jl2.end(), l2);
   std::copy(e->jz.begin(), e->jz.end(), z);

@@ -7,7 +7,6 @@
 #include <cstdio>
 #include <cstring>
 #include <stdexcept>
-#include <thread>
 
 #include "../../../include/is3d_amd.h"
 #include "../../../include/is3d_host.h"
@@ -73,7 +72,10 @@ static is3d_params engine_params(const ParameterReader& p, int operation, int di
   prm.outflow = (int)p.get("outflow");
   prm.deta_min = p.get("deta_min");
   prm.mass_pion0 = p.get("mass_pion0");
-  prm.famod_chains = (int)p.get("famod_chains", 0.0);
+  // PTMA warm-start chains: the reference as shipped is serial (CORES = 1, EmissionFunction.cpp:131-135), one
+  // chain over every cell (MomentumSpectra.cpp:1308-1364); iS3D_parameters.dat has no such key, so the drop-in
+  // default is 1.  famod_chains = C reproduces an OpenMP build with C threads, 0 solves every cell cold.
+  prm.famod_chains = (int)p.get("famod_chains", 1.0);
   return prm;
 }
 
@@ -88,84 +90,58 @@ static is3d_spacetime_bins spacetime_bins(const ParameterReader& p) {
   return b;
 }
 
+// One engine over every requested device (is3d_create_devices): the library splits the cells into
+// cost-balanced windows, runs the devices concurrently and sums their spectra on the devices (RCCL
+// all-reduce over distinct GPUs), replacing the reference's OpenMP fan-out and thread reduction
+// (MomentumSpectra.cpp:98-107, 383-411).
 void EmissionFunctionArray::run_sharded(const RunOptions& opt, int operation) {
   const is3d_params prm = engine_params(p_, operation, dimension_);
   const is3d_spacetime_bins bins = spacetime_bins(p_);
   const int ndev = opt.devices.empty() ? std::max(1, opt.num_devices) : (int)opt.devices.size();
-  auto dev_of = [&](int k) { return opt.devices.empty() ? opt.device + k : opt.devices[k]; };
+  std::vector<int> devs(ndev);
+  for (int k = 0; k < ndev; k++) devs[k] = opt.devices.empty() ? opt.device + k : opt.devices[k];
   std::vector<double> pTv(pT_.cols[0]), phiv(phi_.cols[0]), yv(y_.cols[0]), etav(eta_.cols[0]), etaw(eta_.cols[1]);
   std::vector<double> pTw(pT_.ncols() > 1 ? pT_.cols[1] : std::vector<double>(pTv.size(), 0.0));
   std::vector<double> phiw(phi_.ncols() > 1 ? phi_.cols[1] : std::vector<double>(phiv.size(), 0.0));
   const long n = surf_.size();
   const int np = (int)mass_.size();
-  std::vector<std::vector<double>> parts(ndev);
-  std::vector<std::string> errs(ndev);
-  std::vector<int> codes(ndev, IS3D_ERR_ARG);
   auto t0 = std::chrono::steady_clock::now();
-  auto work = [&](int k) {
-    is3d_engine* e = is3d_create(dev_of(k));
-    if (!e) { errs[k] = "is3d_create(" + std::to_string(dev_of(k)) + ") failed"; codes[k] = IS3D_ERR_DEVICE; return; }
-    try {
-      set_or_throw(e, is3d_set_params(e, &prm));
-      set_or_throw(e, is3d_set_species(e, np, mass_.data(), sign_.data(), degen_.data(), baryon_.data()));
-      set_or_throw(e, is3d_set_pdg(e, (int)pdg_mass_.size(), pdg_mass_.data(), pdg_sign_.data(), pdg_degen_.data(), pdg_baryon_.data()));
-      set_or_throw(e, is3d_set_momentum_grid(e, (int)pTv.size(), pTv.data(), (int)phiv.size(), phiv.data(), (int)yv.size(),
-                                             yv.data(), (int)etav.size(), etav.data(), etaw.data()));
-      set_or_throw(e, is3d_set_gauss_laguerre(e, galpha_, gpts_, gr_.data(), gw_.data()));
-      set_or_throw(e, is3d_set_df_tables(e, df_.nT, df_.nmuB, df_.T.data(), df_.muB.data(), df_.tab.data(), plasma_.T));
-      // contiguous cell shard k (PTMA warm-start chains and the dN/dX thread emulation need the whole surface)
-      const long lo = n * k / ndev, hi = n * (k + 1) / ndev;
-      auto sl = [&](const std::vector<double>& v) { return v.empty() ? nullptr : v.data() + lo; };
-      is3d_surface s{sl(surf_.tau), sl(surf_.x), sl(surf_.y), sl(surf_.eta), sl(surf_.dat), sl(surf_.dax), sl(surf_.day),
-                     sl(surf_.dan), sl(surf_.ux), sl(surf_.uy), sl(surf_.un), sl(surf_.E), sl(surf_.T), sl(surf_.P),
-                     sl(surf_.pixx), sl(surf_.pixy), sl(surf_.pixn), sl(surf_.piyy), sl(surf_.piyn), sl(surf_.bulkPi),
-                     sl(surf_.muB), sl(surf_.nB), sl(surf_.Vx), sl(surf_.Vy), sl(surf_.Vn)};
-      set_or_throw(e, is3d_set_surface(e, hi - lo, &s));
-      if (operation == 1) {
-        parts[k].assign(is3d_output_size(e), 0.0);
-        set_or_throw(e, is3d_calculate_spectra(e, parts[k].data()));
-      } else if (operation == 2) {
-        // the estimate is a sum over cells: per-shard partial Ntotal (the Plasma averages stay global)
-        const double plasma[5] = {plasma_.T, plasma_.E, plasma_.P, plasma_.muB, plasma_.nB};
-        parts[k].assign(1, 0.0);
-        set_or_throw(e, is3d_total_yield(e, plasma, p_.get("y_cut", 0.5), parts[k].data(), nullptr));
-      } else {
-        set_or_throw(e, is3d_set_momentum_weights(e, pTw.data(), phiw.data()));
-        set_or_throw(e, is3d_set_spacetime_bins(e, &bins));
-        const long nt = (long)np * bins.tau_bins, nr = (long)np * bins.r_bins;
-        parts[k].assign(nt + nr + (long)np * bins.phip_bins, 0.0);
-        set_or_throw(e, is3d_calculate_dN_dX(e, parts[k].data(), parts[k].data() + nt, parts[k].data() + nt + nr));
-      }
-    } catch (const EngineError& ex) {
-      errs[k] = ex.what();
-      codes[k] = ex.code;
-    } catch (const std::exception& ex) {
-      errs[k] = ex.what();
+  is3d_engine* e = ndev == 1 ? is3d_create(devs[0]) : is3d_create_devices(ndev, devs.data());
+  if (!e) throw EngineError(IS3D_ERR_DEVICE, "is3d_create on device " + std::to_string(devs[0]) + " failed");
+  try {
+    set_or_throw(e, is3d_set_params(e, &prm));
+    set_or_throw(e, is3d_set_species(e, np, mass_.data(), sign_.data(), degen_.data(), baryon_.data()));
+    set_or_throw(e, is3d_set_pdg(e, (int)pdg_mass_.size(), pdg_mass_.data(), pdg_sign_.data(), pdg_degen_.data(), pdg_baryon_.data()));
+    set_or_throw(e, is3d_set_momentum_grid(e, (int)pTv.size(), pTv.data(), (int)phiv.size(), phiv.data(), (int)yv.size(),
+                                           yv.data(), (int)etav.size(), etav.data(), etaw.data()));
+    set_or_throw(e, is3d_set_gauss_laguerre(e, galpha_, gpts_, gr_.data(), gw_.data()));
+    set_or_throw(e, is3d_set_df_tables(e, df_.nT, df_.nmuB, df_.T.data(), df_.muB.data(), df_.tab.data(), plasma_.T));
+    auto fp = [&](const std::vector<double>& v) { return v.empty() ? nullptr : v.data(); };
+    is3d_surface s{fp(surf_.tau), fp(surf_.x), fp(surf_.y), fp(surf_.eta), fp(surf_.dat), fp(surf_.dax), fp(surf_.day),
+                   fp(surf_.dan), fp(surf_.ux), fp(surf_.uy), fp(surf_.un), fp(surf_.E), fp(surf_.T), fp(surf_.P),
+                   fp(surf_.pixx), fp(surf_.pixy), fp(surf_.pixn), fp(surf_.piyy), fp(surf_.piyn), fp(surf_.bulkPi),
+                   fp(surf_.muB), fp(surf_.nB), fp(surf_.Vx), fp(surf_.Vy), fp(surf_.Vn)};
+    set_or_throw(e, is3d_set_surface(e, n, &s));
+    if (operation == 1) {
+      dN_.assign(is3d_output_size(e), 0.0);
+      set_or_throw(e, is3d_calculate_spectra(e, dN_.data()));
+    } else if (operation == 2) {
+      const double plasma[5] = {plasma_.T, plasma_.E, plasma_.P, plasma_.muB, plasma_.nB};
+      set_or_throw(e, is3d_total_yield(e, plasma, p_.get("y_cut", 0.5), &ntotal_, nullptr));
+    } else {
+      set_or_throw(e, is3d_set_momentum_weights(e, pTw.data(), phiw.data()));
+      set_or_throw(e, is3d_set_spacetime_bins(e, &bins));
+      bins_ = bins;
+      dNtau_.assign((size_t)np * bins.tau_bins, 0.0);
+      dNr_.assign((size_t)np * bins.r_bins, 0.0);
+      dNphi_.assign((size_t)np * bins.phip_bins, 0.0);
+      set_or_throw(e, is3d_calculate_dN_dX(e, dNtau_.data(), dNr_.data(), dNphi_.data()));
     }
+  } catch (...) {
     is3d_destroy(e);
-  };
-  if (prm.df_mode == 5 && prm.famod_chains > 0 && ndev > 1)
-    throw std::runtime_error("famod_chains > 0 (reference warm-start emulation) runs on one device");
-  if (operation == 0 && bins.threads > 0 && ndev > 1)
-    throw std::runtime_error("spacetime_threads > 0 (reference thread-slice emulation) runs on one device");
-  std::vector<std::thread> th;
-  for (int k = 0; k < ndev; k++) th.emplace_back(work, k);
-  for (auto& t : th) t.join();
-  for (int k = 0; k < ndev; k++) if (!errs[k].empty()) throw EngineError(codes[k], errs[k]);
-  std::vector<double> sum(parts[0].size(), 0.0);
-  for (int k = 0; k < ndev; k++)
-    for (size_t i = 0; i < sum.size(); i++) sum[i] += parts[k][i];
-  if (operation == 1) {
-    dN_ = std::move(sum);
-  } else if (operation == 2) {
-    ntotal_ = sum[0];
-  } else {
-    const long nt = (long)np * bins.tau_bins, nr = (long)np * bins.r_bins;
-    bins_ = bins;
-    dNtau_.assign(sum.begin(), sum.begin() + nt);
-    dNr_.assign(sum.begin() + nt, sum.begin() + nt + nr);
-    dNphi_.assign(sum.begin() + nt + nr, sum.end());
+    throw;
   }
+  is3d_destroy(e);
   seconds_ = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
 }
 

@@ -6,15 +6,45 @@ the end: each rank integrates its contiguous cell range and one all-reduce (sum,
 over torch.distributed ('nccl' = RCCL over xGMI on MI355X, 'gloo' in CPU tests) combines
 the [species][pT][phi][y] accumulators.  The only other collective is the tiny
 ds_max-weighted Plasma average (5 sums) the PTB table needs (readindata.cpp:316-366).
-PTMA with reference warm-start chains (famod_chains > 0) does not shard (it is a serial
-recurrence per chain) and runs on one rank.
+Shards are contiguous cell ranges balanced by estimated cost: a cell with
+u.dsigma <= 0 is skipped by every kernel (MomentumSpectra.cpp:132) and costs only its record prep.
+PTMA with the reference's warm-start chains (famod_chains > 0) is a serial recurrence over the whole
+surface: every rank then holds the whole surface, walks the chains itself and integrates its range
+only (Engine.set_cell_window), so each rank sees the serial chain's solutions.
 """
 import numpy as np
 
+SKIP_COST = 0.02     # a u.dsigma <= 0 cell relative to a live one (record prep only); group.hip kSkipCost
+
 
 def shard_range(n, rank, world):
-    """Contiguous cell range [lo, hi) of `rank` (balanced to within one cell)."""
+    """Contiguous cell range [lo, hi) of `rank` (equal counts, to within one cell)."""
     return n * rank // world, n * (rank + 1) // world
+
+
+def cell_costs(surf):
+    """Estimated integration cost per cell: 1 for a live cell, SKIP_COST for u.dsigma <= 0."""
+    tau = surf["tau"]
+    ut = np.sqrt(1. + surf["ux"] ** 2 + surf["uy"] ** 2 + tau * tau * surf["un"] ** 2)
+    uds = ut * surf["dat"] + surf["ux"] * surf["dax"] + surf["uy"] * surf["day"] + surf["un"] * surf["dan"]
+    return np.where(uds > 0.0, 1.0, SKIP_COST)
+
+
+def balanced_ranges(costs, world):
+    """Contiguous [lo, hi) per rank with ~equal summed cost (the rule group.hip applies in-library)."""
+    n = len(costs)
+    pre = np.concatenate([[0.0], np.cumsum(costs)])
+    bounds = [0]
+    for k in range(1, world):
+        c = int(np.searchsorted(pre, pre[-1] * k / world, side="left"))
+        bounds.append(min(max(c, bounds[-1]), n))
+    bounds.append(n)
+    return [(bounds[k], bounds[k + 1]) for k in range(world)]
+
+
+def shard_bounds(surf, rank, world):
+    """This rank's cost-balanced contiguous cell range of `surf`."""
+    return balanced_ranges(cell_costs(surf), world)[rank]
 
 
 def average_sums(surf, include_baryon=0):

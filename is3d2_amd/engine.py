@@ -15,9 +15,13 @@ from . import _lib
 from . import data as _data
 from . import hrg as _hrg
 
+# famod_chains = 1: PTMA's Newton solves warm-start along one chain over every cell, as the reference does as
+# shipped (serial: CORES = 1, EmissionFunction.cpp:131-135; MomentumSpectra.cpp:1308-1364); C > 1 reproduces
+# a reference run with OMP_NUM_THREADS = C, 0 solves every cell from (T, 1, 1) -- differently converged
+# solutions, measured 3.6e-6 from the one-chain spectra (tests/test_gpu_chains.py)
 _DEFAULTS = dict(operation=1, dimension=2, df_mode=1, include_baryon=0, include_bulk_deltaf=1,
                  include_shear_deltaf=1, include_baryondiff_deltaf=0, regulate_deltaf=0, outflow=0,
-                 famod_chains=0, deta_min=1.e-5, mass_pion0=0.138)
+                 famod_chains=1, deta_min=1.e-5, mass_pion0=0.138)
 
 
 # operation = 0 binning (iS3D_parameters.dat defaults; EmissionFunction.cpp:232-247).  `threads` is the
@@ -42,11 +46,19 @@ class IS3DError(RuntimeError):
 
 
 class Engine:
-    """One engine per GPU (device index in the current process's visible devices)."""
+    """One engine per GPU (device index in the current process's visible devices), or -- devices = [d0, d1,
+    ...] -- one engine over several GPUs of this process (is3d_create_devices: cells sharded by estimated cost,
+    spectra summed with one RCCL all-reduce inside the compute call)."""
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, devices=None):
         self.lib = _lib.load()
-        self._e = self.lib.is3d_create(int(device))
+        if devices is not None:
+            dv = (C.c_int * len(devices))(*[int(d) for d in devices])
+            self._e = self.lib.is3d_create_devices(len(devices), dv)
+            if not self._e:
+                raise IS3DError(_lib.IS3D_ERR_DEVICE, "is3d_create_devices(%s) failed" % list(devices))
+        else:
+            self._e = self.lib.is3d_create(int(device))
         if not self._e:
             raise IS3DError(_lib.IS3D_ERR_DEVICE, "is3d_create(%d) failed (no HIP device?)" % device)
         self._keep = []
@@ -114,6 +126,10 @@ class Engine:
     def set_surface_device(self, ptr, n):
         self._chk(self.lib.is3d_set_surface_device(self._e, int(n), C.c_void_p(ptr)))
         self.ncell = n
+
+    def set_cell_window(self, lo, hi):
+        """Integrate only cells [lo, hi) of the surface (-1, -1: all); PTMA chains still walk every cell."""
+        self._chk(self.lib.is3d_set_cell_window(self._e, int(lo), int(hi)))
 
     # --- compute -----------------------------------------------------------------------
     def output_size(self):
@@ -207,8 +223,8 @@ def make_spec(hrg_eos=2, chosen="pikp", pT="pT24", phi="phi24", y="y21", eta="et
                 pT_w=pTw, phi_w=phiw, bins=bins, gla=(roots, weights), df=(T, muB, tab), hrg_eos=hrg_eos)
 
 
-def build_engine(spec, surf, T_avg=None, device=0):
-    e = Engine(device)
+def build_engine(spec, surf, T_avg=None, device=0, devices=None):
+    e = Engine(device, devices)
     p = spec["params"]
     e.set_params(**p)
     sp = spec["species"]

@@ -63,7 +63,9 @@ struct EmuTables {
 // variant bits (k_spectra's launch variants, checked on the CPU): 1 = the F_TB table algebra for Grad /
 // RTA-CE fast lanes without baryon terms (sep_quad_tb_t, phi counts that are multiples of 4), 2 = the
 // Boltzmann-tail lanes (sep_setup allow_tail + sep_quad_tb_tail_t under bit 1),
-// 4 = the modified path's table form (mod_quad_tab_t / mod_pair_tab_t)
+// 4 = the modified path's table form (mod_quad_tab_t / mod_pair_tab_t), 8 = PTMA Newton sums over hadrons
+// merged by identical (mass, sign) with summed degeneracies, first-occurrence order (engine.hip
+// finalize_tables, IS3D_ANISO_MERGE); without it the sums run per hadron in PDG order as the reference
 extern "C" int emu_spectra_v(const orc_params* p, const orc_setup* su, const orc_surface* S, int chains, int op,
                              double* out, long* stats, int variant) {
   const int mode = p->df_mode, dim = p->dimension;
@@ -95,7 +97,16 @@ extern "C" int emu_spectra_v(const orc_params* p, const orc_setup* su, const orc
   }
   if (mode == PTMA) {
     const int nh = su->npdg < 320 ? su->npdg : 320;
-    Hadrons h{nh, su->pdg_mass, su->pdg_sign, su->pdg_degen};
+    std::vector<double> am, as, ag;
+    for (int i = 0; i < nh; i++) {
+      int u = -1;
+      if (variant & 8)
+        for (size_t v = 0; v < am.size(); v++)
+          if (am[v] == su->pdg_mass[i] && as[v] == su->pdg_sign[i]) { u = (int)v; break; }
+      if (u < 0) { am.push_back(su->pdg_mass[i]); as.push_back(su->pdg_sign[i]); ag.push_back(su->pdg_degen[i]); }
+      else ag[u] += su->pdg_degen[i];
+    }
+    Hadrons h{(int)am.size(), am.data(), as.data(), ag.data()};
     const double fp2 = 4.0 * pow(M_PI, 2) * pow(kHbarC, 3);
     auto id = [](double v) { return v; };
     const long C = (chains > 0) ? (chains < n ? chains : n) : n;
@@ -383,4 +394,65 @@ extern "C" int emu_total_yield(const orc_params* p, const orc_setup* su, const o
   if (p->dimension == 2) Ntot *= 2.0 * y_cut;
   *n_total = Ntot;
   return 0;
+}
+
+// PTMA warm-start chain (one chain, MomentumSpectra.cpp:1308-1364) solved by parallel sweeps: sweep 0 solves
+// every cell from its cold start, sweep m solves cell i from the chain state sweep m - 1 left after cell i - 1.
+// The serial chain is the recurrence's unique fixed point, so once a sweep changes nothing the sweeps equal
+// the serial solve bit for bit.  changed[m] = cells whose chain state after sweep m differs (bitwise) from
+// sweep m - 1; wrong[m] = cells whose output differs from the serial chain's.  Returns the sweeps run.
+extern "C" int emu_chain_sweeps(const orc_params* p, const orc_setup* su, const orc_surface* S, int max_sweeps,
+                                long* changed, long* wrong) {
+  const long n = S->n;
+  EmuTables et(p, su, 1);
+  const PrepConsts& k = et.k;
+  std::vector<double> rec((size_t)n * NREC), aux((size_t)n * 9);
+  const double* fields[NSURF] = {S->tau, S->x, S->y, S->eta, S->dat, S->dax, S->day, S->dan, S->ux, S->uy, S->un,
+                                 S->E, S->T, S->P, S->pixx, S->pixy, S->pixn, S->piyy, S->piyn, S->bulkPi,
+                                 S->muB, S->nB, S->Vx, S->Vy, S->Vn};
+  for (long c = 0; c < n; c++) {
+    double s[NSURF];
+    for (int f = 0; f < NSURF; f++) s[f] = fields[f] ? fields[f][c] : 0.0;
+    prep_famod_a(k, s, &rec[(size_t)c * NREC], &aux[(size_t)c * 9]);
+  }
+  const int nh = su->npdg < 320 ? su->npdg : 320;
+  std::vector<double> am, as, ag;
+  for (int i = 0; i < nh; i++) {
+    int u = -1;
+    for (size_t v = 0; v < am.size(); v++)
+      if (am[v] == su->pdg_mass[i] && as[v] == su->pdg_sign[i]) { u = (int)v; break; }
+    if (u < 0) { am.push_back(su->pdg_mass[i]); as.push_back(su->pdg_sign[i]); ag.push_back(su->pdg_degen[i]); }
+    else ag[u] += su->pdg_degen[i];
+  }
+  Hadrons h{(int)am.size(), am.data(), as.data(), ag.data()};
+  const double fp2 = 4.0 * pow(M_PI, 2) * pow(kHbarC, 3);
+  auto id = [](double v) { return v; };
+  // serial reference: state after each cell
+  std::vector<double> sst((size_t)n * 4), sout((size_t)n * 6);
+  {
+    double state[4] = {0, 0, 0, 0};
+    long cnt[3] = {0, 0, 0};
+    for (long c = 0; c < n; c++) {
+      if (rec[(size_t)c * NREC + R_KIND] != 0.0) aniso_cell(&aux[(size_t)c * 9], h, 0, 1, id, fp2, state, &sout[(size_t)c * 6], cnt);
+      std::memcpy(&sst[(size_t)c * 4], state, sizeof(state));
+    }
+  }
+  std::vector<double> prev((size_t)n * 4, 0.0), cur((size_t)n * 4), out((size_t)n * 6, 0.0);
+  int m = 0;
+  for (; m < max_sweeps; m++) {
+    long ch = 0, wr = 0;
+    for (long c = 0; c < n; c++) {
+      double state[4] = {0, 0, 0, 0};
+      if (m > 0 && c > 0) std::memcpy(state, &prev[(size_t)(c - 1) * 4], sizeof(state));
+      long cnt[3] = {0, 0, 0};
+      if (rec[(size_t)c * NREC + R_KIND] != 0.0) aniso_cell(&aux[(size_t)c * 9], h, 0, 1, id, fp2, state, &out[(size_t)c * 6], cnt);
+      std::memcpy(&cur[(size_t)c * 4], state, sizeof(state));
+      if (m == 0 || std::memcmp(&cur[(size_t)c * 4], &prev[(size_t)c * 4], sizeof(state))) ch++;
+      if (rec[(size_t)c * NREC + R_KIND] != 0.0 && std::memcmp(&out[(size_t)c * 6], &sout[(size_t)c * 6], 6 * sizeof(double))) wr++;
+    }
+    changed[m] = ch; wrong[m] = wr;
+    prev.swap(cur);
+    if (m > 0 && ch == 0) { m++; break; }
+  }
+  return m;
 }

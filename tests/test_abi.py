@@ -25,3 +25,9 @@ def test_library_exports_every_declared_symbol():
 def test_abi_version():
     lib = _lib.load()
     assert lib.is3d_abi_version() == 3
+
+
+def test_build_id_names_the_sources():
+    """is3d_build_id() = the Makefile's SRC_ID: a hash of the sources + flags the library was built from."""
+    bid = _lib.build_id()
+    assert re.fullmatch(r"[0-9a-f]{12}-[0-9a-f]{4}", bid), bid

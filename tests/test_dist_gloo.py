@@ -20,7 +20,9 @@ def _worker(rank, world, port, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     s = synth.as_read(synth.surface(101, seed=5))
-    lo, hi = D.shard_range(101, rank, world)
+    s["dat"] = s["dat"].copy()
+    s["dat"][:40] *= -20.0                   # a free (u.dsigma <= 0) prefix: the shards are cost-balanced
+    lo, hi = D.shard_bounds(s, rank, world)
     shard = {k: v[lo:hi] for k, v in s.items()}
     avg = D.global_averages(D.average_sums(shard), D.torch_all_reduce(dist))
     spec = make_spec(hrg_eos=2, chosen="pikp", df_mode=4)        # PTB: needs the global T_avg
@@ -46,8 +48,29 @@ def test_two_rank_gloo_shard_and_allreduce():
         p.join(timeout=60)
         assert p.exitcode == 0
     s = synth.as_read(synth.surface(101, seed=5))
+    s["dat"] = s["dat"].copy()
+    s["dat"][:40] *= -20.0
     full_avg = O.averages(s)
     assert abs(avg[0] - full_avg[0]) <= 1e-14 * full_avg[0]
     spec = make_spec(hrg_eos=2, chosen="pikp", df_mode=4)
     ref = O.spectra(spec, s, T_avg=full_avg[0])
     np.testing.assert_allclose(got, ref, rtol=1e-11)
+
+
+def test_cost_balanced_ranges():
+    """contiguous ranges of ~equal estimated cost -- u.dsigma <= 0 cells cost SKIP_COST."""
+    from is3d2_amd import dist as D, synth
+    s = synth.as_read(synth.surface(1000, seed=3))
+    s["dat"] = s["dat"].copy()
+    s["dat"][:600] *= -20.0                  # 600 free cells, then 400 live ones
+    c = D.cell_costs(s)
+    assert (c[:600] == D.SKIP_COST).all() and (c[600:] == 1.0).mean() > 0.9
+    for world in (2, 4, 8):
+        r = D.balanced_ranges(c, world)
+        assert r[0][0] == 0 and r[-1][1] == 1000
+        assert all(r[k][1] == r[k + 1][0] for k in range(world - 1))
+        cost = [c[lo:hi].sum() for lo, hi in r]
+        assert max(cost) - min(cost) <= 1.0 + D.SKIP_COST * 2, cost
+        # equal counts would have given rank 0 only free cells
+        assert cost[0] > 0.5 * c.sum() / world
+    assert D.balanced_ranges(np.ones(3), 8)[-1] == (3, 3)     # more ranks than cells: empty tail ranges

@@ -1,0 +1,137 @@
+"""GPU tier: the multi-device engine (is3d_create_devices, group.hip) -- SURVEY.md 8(b)/(e): the fan-out over
+GPUs happens inside the compute call, cells are split into cost-balanced contiguous windows, and the
+per-device spectra are summed on the devices (one RCCL ncclAllReduce over distinct GPUs; peer copy +
+fixed-order add when the list repeats a GPU).
+
+A one-GPU box can only list GPU 0 repeatedly, which exercises the sharding, the windows, the concurrent
+launches and the copy reduction; IS3D_REDUCE=rccl on a one-device list runs the RCCL path itself (a
+one-rank communicator: ncclCommInitAll, grouped ncclAllReduce on the launch stream).  Results are compared
+with one single-device engine (summation order only: <= 1e-12) and with the oracle."""
+import os
+
+import numpy as np
+import pytest
+
+from helpers import parity
+from is3d2_amd import Engine, build_engine, make_spec, synth
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def spectra(spec, surf, devices=None, T_avg=None):
+    e = build_engine(spec, surf, T_avg=T_avg, devices=devices)
+    out = e.calculate_spectra()
+    st = e.stats()
+    e.close()
+    return out, st
+
+
+@pytest.mark.parametrize("mode,dim", [(1, 3), (2, 2), (3, 3), (4, 2)])
+@pytest.mark.parametrize("ndev", [2, 3])
+def test_group_equals_single_engine(mode, dim, ndev):
+    s = synth.as_read(synth.surface(300, seed=71, dimension=dim, full3d=(dim == 3)))
+    spec = make_spec(hrg_eos=2, chosen="pikp", df_mode=mode, dimension=dim)
+    one, st1 = spectra(spec, s)
+    grp, stg = spectra(spec, s, devices=[0] * ndev)
+    assert parity(grp, one)[0] < 1e-12
+    assert stg["cells"] == st1["cells"] == 300
+    assert stg["breakdown"] == st1["breakdown"]
+    ref = O.spectra(spec, s, threads=8)
+    assert parity(grp, ref)[0] < 1e-8
+
+
+def test_group_smash_grid_grad_table_launch():
+    s = synth.as_read(synth.surface(64, seed=2, dimension=3))
+    spec = make_spec(hrg_eos=2, chosen="smash", df_mode=1, dimension=3, pT="pT48", phi="phi32", y="y21")
+    one, _ = spectra(spec, s)
+    grp, _ = spectra(spec, s, devices=[0, 0, 0, 0])
+    # 444 species: the sum over shards reorders near-cancelling delta-f contributions (measured 6.5e-12)
+    assert parity(grp, one)[0] < 1e-10
+
+
+def test_group_ptma_chain_walks_whole_surface():
+    """PTMA with the reference's warm-start chain: every shard holds the whole surface and walks the chain,
+    integrating only its window -- same Newton solves (iteration count) as one device."""
+    s = synth.as_read(synth.surface(900, seed=73, dimension=2))
+    spec = make_spec(hrg_eos=2, chosen="pikp", df_mode=5, dimension=2, famod_chains=1)
+    one, st1 = spectra(spec, s)
+    grp, stg = spectra(spec, s, devices=[0, 0])
+    assert stg["iterations"] == st1["iterations"]
+    assert stg["breakdown"] == st1["breakdown"]
+    assert parity(grp, one)[0] < 1e-12
+
+
+def test_group_rccl_one_rank(monkeypatch):
+    monkeypatch.setenv("IS3D_REDUCE", "rccl")
+    s = synth.as_read(synth.surface(200, seed=79, dimension=2))
+    spec = make_spec(hrg_eos=2, chosen="pikp", df_mode=2, dimension=2)
+    one, _ = spectra(spec, s)
+    grp, _ = spectra(spec, s, devices=[0])
+    assert np.array_equal(grp, one)       # a one-rank all-reduce is the identity
+
+
+def test_group_balances_skipped_cells():
+    """The first two thirds of the surface are u.dsigma <= 0 (free): cost-balanced windows put them all on the
+    first shard, so the result still matches and every shard carries live cells."""
+    s = synth.as_read(synth.surface(600, seed=83, dimension=2))
+    s["dat"] = s["dat"].copy()
+    s["dat"][:400] *= -20.0
+    spec = make_spec(hrg_eos=2, chosen="pikp", df_mode=1, dimension=2)
+    one, _ = spectra(spec, s)
+    grp, _ = spectra(spec, s, devices=[0, 0, 0])
+    assert parity(grp, one)[0] < 1e-12
+
+
+def test_group_launch_on_caller_stream():
+    torch = pytest.importorskip("torch")
+    s = synth.as_read(synth.surface(300, seed=89, dimension=3, full3d=True))
+    spec = make_spec(hrg_eos=2, chosen="pikp", df_mode=2, dimension=3)
+    one, _ = spectra(spec, s)
+    e = build_engine(spec, s, devices=[0, 0])
+    out = torch.zeros(e.output_size(), dtype=torch.float64, device="cuda:0")
+    stream = torch.cuda.current_stream(0).cuda_stream
+    for _ in range(2):
+        e.launch(out.data_ptr(), stream)
+        e.finish()
+    got = out.cpu().numpy()
+    e.close()
+    assert parity(got, one)[0] < 1e-12
+
+
+def test_group_dndx_and_yield():
+    s = synth.as_read(synth.surface(400, seed=97, dimension=2))
+    spec = make_spec(hrg_eos=2, chosen="pikp", df_mode=1, dimension=2)
+    outs = []
+    for dv in (None, [0, 0, 0]):
+        e = build_engine(spec, s, devices=dv)
+        t, r, ph = e.calculate_dN_dX()
+        cy = e.cell_yields()
+        from is3d2_amd.engine import surface_averages
+        nt, dens = e.total_yield(surface_averages(s))
+        e.close()
+        outs.append((t, r, ph, cy, nt, dens))
+    for a, b in zip(outs[0][:4], outs[1][:4]):
+        assert parity(b, a, floor=1e-300)[0] < 1e-12
+    assert abs(outs[1][4] - outs[0][4]) <= 1e-12 * abs(outs[0][4])
+    assert np.array_equal(outs[1][5], outs[0][5])
+
+
+def test_group_surface_from_device():
+    torch = pytest.importorskip("torch")
+    s = synth.as_read(synth.surface(300, seed=101, dimension=2))
+    spec = make_spec(hrg_eos=2, chosen="pikp", df_mode=2, dimension=2)
+    one, _ = spectra(spec, s)
+    from is3d2_amd import _lib
+    dev = torch.from_numpy(np.stack([np.asarray(s[k], dtype=np.float64) if s.get(k) is not None
+                                     else np.zeros(300) for k in _lib.SURFACE_FIELDS])).to("cuda:0").contiguous()
+    e = build_engine(spec, s, devices=[0, 0])
+    e.set_surface_device(dev.data_ptr(), 300)
+    got = e.calculate_spectra()
+    e.close()
+    assert parity(got, one)[0] < 1e-12
+
+
+def test_group_bad_device_list():
+    with pytest.raises(Exception):
+        Engine(devices=[0, 97])

@@ -52,6 +52,27 @@ def test_ptma_chains_match_reference_thread_count():
         assert st[3] == st2[3]        # identical Newton iteration counts
 
 
+@pytest.mark.parametrize("hrg_eos,dim", [(2, 2), (2, 3), (1, 3)])
+def test_ptma_merged_hadron_sums(hrg_eos, dim):
+    """The engine sums the PTMA Newton integrands over hadrons merged by identical (mass, sign) (SMASH 320 ->
+    92, UrQMD 320 -> 83, engine.hip finalize_tables); the reference sums per hadron in PDG order
+    (AnisoVariables.cpp:30-117).  On the breakdown-heavy chain (bulk x10, one warm-start chain, the surface
+    of test_gpu_configs.py::test_modified_fallback_launch) both orders must take the same Newton steps and
+    agree with the oracle to rounding."""
+    s = synth.as_read(synth.surface(200, seed=31, dimension=dim, full3d=(dim == 3)))
+    s["bulkPi"] = s["bulkPi"].copy()
+    s["bulkPi"][::2] *= 10.0
+    chosen = "pikp" if hrg_eos == 2 else [211, 321, 2212]
+    spec = make_spec(hrg_eos=hrg_eos, chosen=chosen, df_mode=5, dimension=dim, famod_chains=1)
+    ref, rst = O.spectra(spec, s, threads=1, return_stats=True)
+    per, pst = emu_spectra(spec, s, chains=1, variant=4)
+    mrg, mst = emu_spectra(spec, s, chains=1, variant=4 | 8)
+    assert rst[3] == pst[3] == mst[3], (rst[3], pst[3], mst[3])
+    assert parity(np.nan_to_num(per), np.nan_to_num(ref))[0] < 1e-9
+    assert parity(np.nan_to_num(mrg), np.nan_to_num(ref))[0] < 1e-9
+    assert parity(np.nan_to_num(mrg), np.nan_to_num(per))[0] < 1e-9
+
+
 def test_kernel_exp_accuracy():
     """exp_dom690/exp_clamped (cf_math.h) against libm exp: <= 2 ulp over the fast-path domain,
     saturation to +inf past the overflow point, exact zero far below underflow."""

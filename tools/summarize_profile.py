@@ -44,8 +44,22 @@ def counters(path):
     return acc, dur
 
 
+def build_id(d):
+    """Identity of the library the profiled run loaded: bench.py prints it on stderr as 'build_id <id>' (the
+    trace pass log); falls back to the in-tree library (the same file the snapshot carried)."""
+    for log in (os.path.join(d, "trace.log"), os.path.join(d, "trace", "trace.log")):
+        if os.path.exists(log):
+            for ln in open(log, errors="replace"):
+                if ln.startswith("build_id "):
+                    return ln.split()[1]
+    sys.path.insert(0, ROOT)
+    from is3d2_amd import _lib
+    return _lib.build_id()
+
+
 def main():
     d, tag, config, mode = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4])
+    bid = build_id(d)
     prof = os.path.join(ROOT, "profiles")
     os.makedirs(prof, exist_ok=True)
     shutil.copy(os.path.join(d, "trace", "run_kernel_stats.csv"), os.path.join(prof, "%s_kernel_stats.csv" % tag))
@@ -80,13 +94,13 @@ def main():
     if spec and "hbm_bytes_per_launch" in out[spec[0]]:
         tp = os.path.join(prof, "pmc_traffic.json")
         t = json.load(open(tp)) if os.path.exists(tp) else {}
-        t[key] = out[spec[0]]["hbm_bytes_per_launch"]
+        t[key] = {"hbm_bytes_per_launch": out[spec[0]]["hbm_bytes_per_launch"], "tag": tag, "build_id": bid}
         json.dump(t, open(tp, "w"), indent=1, sort_keys=True)
     if spec and "valu_issue_frac" in out[spec[0]]:
         vp = os.path.join(prof, "pmc_valu.json")
         v = json.load(open(vp)) if os.path.exists(vp) else {}
         e = out[spec[0]]
-        v[key] = {"tag": tag, "valu_insts_per_launch": e["SQ_INSTS_VALU"], "valu_issue_frac": e["valu_issue_frac"],
+        v[key] = {"tag": tag, "build_id": bid, "valu_insts_per_launch": e["SQ_INSTS_VALU"], "valu_issue_frac": e["valu_issue_frac"],
                   "clock_ghz": e["clock_ghz"]}
         for c in ("ADD_F64", "MUL_F64", "FMA_F64", "TRANS_F64", "INT32", "INT64", "CVT"):
             if "SQ_INSTS_VALU_" + c in e:
