@@ -87,6 +87,21 @@ def cpu_baseline(spec, surf, units_per_cell, n_full, target_s=25.0, operation=1)
     (the cost is linear in the cell count).  Threads: OMP_NUM_THREADS when set (the GPU
     pool sets it to the box's CPU share, 16 per GPU; nproc there counts the whole host), else every
     CPU in this process's affinity mask."""
+    import subprocess
+    import tempfile
+    # BASELINE.md 4: -O3 -fopenmp -march=native, built here on the box's own host (a -march=native binary cannot
+    # ship from the build container); the portable in-tree build if no compiler is at hand
+    compiler = None
+    if not os.environ.get("IS3D_ORACLE_LIB"):
+        out = os.path.join(tempfile.gettempdir(), "is3d_oracle_native_%d.so" % os.getpid())
+        try:
+            r = subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "native", "NATIVE_OUT=" + out],
+                               capture_output=True, text=True, timeout=120)
+            if r.returncode == 0 and os.path.exists(out):
+                os.environ["IS3D_ORACLE_LIB"] = out
+                compiler = r.stdout.strip().splitlines()[-1] + " (built on this host)"
+        except (OSError, subprocess.SubprocessError):
+            pass
     from oracle import oracle as O
     model, nproc, affinity, quota = _host_cpu()
     threads = int(os.environ.get("OMP_NUM_THREADS") or affinity)
@@ -109,18 +124,19 @@ def cpu_baseline(spec, surf, units_per_cell, n_full, target_s=25.0, operation=1)
     t = time.perf_counter()
     run(sample)
     dt = time.perf_counter() - t
-    flags = ""
-    try:
-        mk = open(os.path.join(ROOT, "oracle", "Makefile")).read()
-        flags = [ln.split("=", 1)[1].strip() for ln in mk.splitlines() if ln.startswith("CFLAGS")][0]
-    except (OSError, IndexError):
-        pass
+    if compiler is None:
+        try:
+            mk = open(os.path.join(ROOT, "oracle", "Makefile")).read()
+            compiler = "gcc " + [ln.split("=", 1)[1].strip() for ln in mk.splitlines() if ln.startswith("CFLAGS")][0]
+            compiler += " (portable in-tree build: no compiler on this host)"
+        except (OSError, IndexError):
+            compiler = "unknown"
     return dict(value=n * units_per_cell / dt, unit="cell-species-mom-points/s", cores=threads, kind="port",
                 sample="first %d cells of rank 0's shard (same species/grid/df mode): %.1f s with %d OpenMP threads"
                        % (n, dt, threads),
                 sample_cells=n, sample_s=dt, extrapolated_s=dt * n_full / n, extrapolated_cells=n_full,
                 nproc=nproc, affinity_cpus=affinity, cgroup_cpu_quota=quota, cpu_model=model,
-                compiler="gcc " + flags,
+                compiler=compiler,
                 note="cores = OMP_NUM_THREADS when set: the GPU pool gives a one-GPU box a 16-CPU share "
                      "(cgroup_cpu_quota) of a host whose nproc counts every CPU")
 

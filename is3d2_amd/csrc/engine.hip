@@ -21,9 +21,6 @@
 #ifndef IS3D_ANISO_MERGE
 #define IS3D_ANISO_MERGE 1    // PTMA Newton sums over hadrons merged by identical (mass, sign)
 #endif
-#ifndef IS3D_TB2
-#define IS3D_TB2 0            // Grad table launch with two species per lane (F_S2), A/B variant
-#endif
 #ifndef IS3D_MAX_SPLITS
 #define IS3D_MAX_SPLITS 64    // cap on k_spectra's cell splits (one output-sized slab each)
 #endif
@@ -386,7 +383,6 @@ __global__ __launch_bounds__(1024) void k_fbscan(const double* rec, long n, int*
 struct ReduceArgs {
   const double* slab; long sstride; int nsplit;
   int nbx, npart, npT, nphi, nk, nl, ny_out, kj; long ntask;
-  int spl, npl;               // species per lane (F_S2: 2), species slots per row
   const int* sorig; const double* degen_orig; double prefactor;
   double* out;
 };
@@ -397,16 +393,15 @@ struct ReduceArgs {
 __global__ __launch_bounds__(256) void k_reduce(ReduceArgs A) {
   const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= A.sstride) return;
-  const int KJ = A.kj, SK = A.spl * KJ;
+  const int KJ = A.kj;
   const int lane = (int)(e % kBlock);
-  const int slot = (int)((e / kBlock) % SK), jj = slot % KJ;
-  const long rest = e / ((long)kBlock * SK);
+  const int jj = (int)((e / kBlock) % KJ);
+  const long rest = e / ((long)kBlock * KJ);
   const int lane_group = (int)(rest % A.nbx), ipt = (int)(rest / A.nbx);
   const long task = (long)lane_group * kBlock + lane;
   if (task >= A.ntask) return;
-  const int s = A.spl * (int)(task % A.npl) + slot / KJ;
-  if (s >= A.npart) return;
-  const long r = task / A.npl;
+  const int s = (int)(task % A.npart);
+  const long r = task / A.npart;
   const long nq = (long)A.nk * A.nl;
   const int q = (int)(r % nq);
   if (q % A.nl != 0) return;
@@ -414,8 +409,8 @@ __global__ __launch_bounds__(256) void k_reduce(ReduceArgs A) {
   if (j >= A.nphi) return;
   double acc = 0.0;
   for (int l = 0; l < A.nl; l++) {
-    const long tl = task + (long)l * A.npl;
-    const long el = ((long)ipt * A.nbx + tl / kBlock) * ((long)SK * kBlock) + (long)slot * kBlock + tl % kBlock;
+    const long tl = task + (long)l * A.npart;
+    const long el = ((long)ipt * A.nbx + tl / kBlock) * ((long)KJ * kBlock) + (long)jj * kBlock + tl % kBlock;
     for (int z = 0; z < A.nsplit; z++) acc += A.slab[(long)z * A.sstride + el];
   }
   const int so = A.sorig[s];
@@ -436,15 +431,15 @@ __global__ __launch_bounds__(256) void k_reduce_wave(ReduceArgs A) {
   const int j = (int)(r1 % A.nphi);
   const long r2 = r1 / A.nphi;
   const int ipt = (int)(r2 % A.npT), s = (int)(r2 / A.npT);
-  const int KJ = A.kj, jb = j / KJ, jj = j % KJ, SK = A.spl * KJ, slot = (s % A.spl) * KJ + jj;
+  const int KJ = A.kj, jb = j / KJ, jj = j % KJ;
   const long nq = (long)A.nk * A.nl;
-  const long task0 = s / A.spl + (long)A.npl * (k * A.nl + nq * jb);
+  const long task0 = s + (long)A.npart * (k * A.nl + nq * jb);
   const long nterm = (long)A.nl * A.nsplit;
   double acc = 0.0;
   for (long m = lane; m < nterm; m += 64) {
     const int l = (int)(m / A.nsplit), z = (int)(m % A.nsplit);
-    const long tl = task0 + (long)l * A.npl;
-    const long el = ((long)ipt * A.nbx + tl / kBlock) * ((long)SK * kBlock) + (long)slot * kBlock + tl % kBlock;
+    const long tl = task0 + (long)l * A.npart;
+    const long el = ((long)ipt * A.nbx + tl / kBlock) * ((long)KJ * kBlock) + (long)jj * kBlock + tl % kBlock;
     acc += A.slab[(long)z * A.sstride + el];
   }
 #pragma unroll
@@ -931,7 +926,6 @@ static int device_jonah_table(is3d_engine* e, const double* r2, const double* w2
 // pT sin} table finalize_tables builds for KJ-padded phi rows)
 struct SpectraPlan {
   int KJ, njb, nq, nqmax, tb, ly, t8, tile;
-  int s2, spl, npl;           // F_S2 (two species per lane), species per lane, species slots per row
   size_t shmem;
   size_t shmem_fb;            // modified modes: the F_FB launch (8-cell tiles, per-lane y-term rows, no q tables)
 };
@@ -941,13 +935,12 @@ static SpectraPlan spectra_plan(const is3d_engine* e) {
   const int np = (int)e->mass.size(), nphi = (int)e->phi.size();
   const int nk = (dim == 3) ? (int)e->y.size() : 1, nl = (dim == 3) ? 1 : (int)e->eta.size();
   P.nq = nk * nl;
-  P.spl = 1; P.npl = np; P.s2 = 0;
   auto shape = [&](int KJ) {
     P.KJ = KJ;
     P.njb = (nphi + KJ - 1) / KJ;
     // rows (r = q + nq jb) one workgroup's 256 consecutive tasks can span: a contiguous range of at most
-    // (kBlock - 1) / npl + 2 of the nq njb rows
-    P.nqmax = (int)std::min<long>((long)P.nq * P.njb, (kBlock - 1) / P.npl + 2);
+    // (kBlock - 1) / np + 2 of the nq njb rows
+    P.nqmax = (int)std::min<long>((long)P.nq * P.njb, (kBlock - 1) / np + 2);
     // Grad {PD, T1} table (F_TB, sep_quad_tb_t): exact only without baryon terms (R_SCB = R_SSB = 0:
     // V^mu and alphaB are only packed when include_baryon && include_baryondiff_deltaf (prep_grad_ce), and
     // df_eval leaves c1 = c3 = 0 without baryons); needs phi blocks of fours and at most kTbQ rows per
@@ -974,14 +967,6 @@ static SpectraPlan spectra_plan(const is3d_engine* e) {
 #else
   shape(spectra_kj_fill(nphi, (long)np * P.nq));
 #endif
-  // Grad table launch with two species per lane (F_S2, KJ = 16): phi tables in blocks of 16 and >= 86 species
-  // pairs, so a workgroup still spans <= kTbQ q rows
-  if (IS3D_TB2 && mode == GRAD && P.tb && nphi % 16 == 0 && (np + 1) / 2 >= 86) {
-    P.spl = 2; P.npl = (np + 1) / 2;
-    shape(16);
-    if (P.tb) P.s2 = F_S2;
-    else { P.spl = 1; P.npl = np; shape(spectra_kj_fill(nphi, (long)np * P.nq)); }
-  }
   P.ly = 0;
   P.shmem = lds_bytes(P.nqmax);
   // the modified path's 16-cell tiles fall back to 8 (F_T8) before giving up the q-row tables
@@ -1359,18 +1344,16 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   // --- main integral
   const SpectraPlan P = spectra_plan(e);
   const int KJ = P.KJ, njb = P.njb;
-  if (!spectra_kj_supported(KJ) && !(P.s2 && KJ == 16))
-    return e->fail(IS3D_ERR_ARG, "internal: no k_spectra instantiation for this phi block");
-  const int spl = P.spl, npl = P.npl;
+  if (!spectra_kj_supported(KJ)) return e->fail(IS3D_ERR_ARG, "internal: no k_spectra instantiation for this phi block");
   if (P.shmem > 160 * 1024) return e->fail(IS3D_ERR_ARG, "momentum grid too large for the LDS tile (phi table)");
-  const long ntask = (long)npl * nk * nl * njb;
+  const long ntask = (long)np * nk * nl * njb;
   const long bx = (ntask + kBlock - 1) / kBlock;
   if (!P.ly) {
     // k_spectra's LDS row tables hold nqmax rows per cell; a lane group spanning more would compute nothing
     // (its slab is NaN-filled, rows_ok), so refuse the launch here instead of returning NaN spectra
     for (long g = 0; g < bx; g++) {
       const long t0 = g * kBlock, t1 = std::min(ntask, t0 + kBlock) - 1;
-      if (t1 / npl - t0 / npl + 1 > P.nqmax)
+      if (t1 / np - t0 / np + 1 > P.nqmax)
         return e->fail(IS3D_ERR_ARG, "internal: k_spectra lane group spans more q rows than the LDS plan");
     }
   }
@@ -1388,7 +1371,7 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   long cps = std::max(1L, (nw + nsplit - 1) / nsplit);
   cps = ((cps + kTile - 1) / kTile) * kTile;
   nsplit = std::max(1L, (nw + cps - 1) / cps);
-  const long sstride = (long)npT * bx * spl * KJ * kBlock;
+  const long sstride = (long)npT * bx * KJ * kBlock;
   // modified modes: the F_FB launch (separable-fallback lanes, cells listed by k_fbscan) writes its own
   // nsplit_fb slabs after the main ones; k_reduce sums both
   const long nsplit_fb = (mode >= PTM) ? std::max(1L, std::min(nsplit, 8L)) : 0;
@@ -1404,12 +1387,11 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   sa.csg = e->d_csg;
   sa.pT = e->d_pT; sa.cphi = e->d_cphi; sa.sphi = e->d_sphi; sa.yv = e->d_y; sa.etav = e->d_eta; sa.etaw = e->d_etaw;
   sa.npart = np; sa.npT = npT; sa.nphi = nphi; sa.ny_out = ny_out; sa.nk = nk; sa.nl = nl; sa.nq = nk * nl; sa.njb = njb;
-  sa.npl = npl;
   sa.nqmax = P.nqmax;
   sa.ntask = ntask; sa.cells_per_split = cps; sa.nbx = (int)bx; sa.nsplit = (int)nsplit; sa.sstride = sstride;
   sa.regulate = e->p.regulate_deltaf; sa.outflow = e->p.outflow; sa.dim = dim; sa.op = 1;
   const size_t shmem = P.shmem;
-  const int tb = P.tb | P.ly | P.t8 | P.s2;
+  const int tb = P.tb | P.ly | P.t8;
   const dim3 grid((unsigned)(bx * npT * nsplit));
   const int kflags = (e->p.regulate_deltaf ? F_REG : 0) | (e->p.outflow ? F_OUT : 0) | tb;
   switch (mode) {
@@ -1437,7 +1419,6 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   ReduceArgs ra{};
   ra.slab = e->d_slab; ra.sstride = sstride; ra.nsplit = (int)(nsplit + nsplit_fb);
   ra.nbx = (int)bx; ra.npart = np; ra.npT = npT; ra.nphi = nphi; ra.nk = nk; ra.nl = nl; ra.ny_out = ny_out; ra.kj = KJ;
-  ra.spl = spl; ra.npl = npl;
   ra.ntask = ntask;
   ra.sorig = e->d_sorig; ra.degen_orig = e->d_degen_orig; ra.prefactor = std::pow(2.0 * M_PI * kHbarC, -3);
   ra.out = dev_out;

@@ -74,9 +74,8 @@ struct SpecArgs {
   const double *pT, *cphi, *sphi, *yv, *etav, *etaw;
   const double* csg;          // [npT][nphp] {pT cos, pT sin} (read by scalar loads when njb == 1)
   int npart, npT, nphi, ny_out, nk, nl, nq, njb;
-  int npl;                    // species slots per row: npart, or ceil(npart / 2) for the F_S2 launch
   int nqmax;                  // q rows a workgroup's lanes can span (LDS rows of the y-term / q tables)
-  long ntask;                 // npl * nq * njb lanes per pT: (species [pair], q = y x eta node, phi block)
+  long ntask;                 // npart * nq * njb lanes per pT: (species, q = y x eta node, phi block)
   long cells_per_split;
   int nbx, nsplit;            // lane groups per pT, cell splits (1-D grid of nbx * npT * nsplit)
   long sstride;               // doubles per slab: npT * nbx * KJ * kBlock
@@ -96,10 +95,7 @@ struct SpecArgs {
 // cells, narrow rapidity windows), over the cells listed by k_fbscan, per-lane y-term rows as F_LY.  Keeping
 // the separable code out of the modified launch takes its k_spectra from 241 to 164 VGPRs (3 waves per SIMD
 // instead of 2) and removes the 32-64 v_mov_b64 per lane and cell that merged two register assignments of acc
-// F_S2 (Grad F_TB, KJ = 16): a lane owns two mass-adjacent species of one (q, phi block), so every {b', Phi} and
-// {PD, T1} table read feeds two points -- half the LDS-array cycles per point (the Boltzmann-tail loop reads
-// 8 LDS cycles for 5 VALU ops per point and is LDS-bound at one species per lane)
-constexpr int F_REG = 1, F_OUT = 2, F_TB = 4, F_LY = 8, F_T8 = 16, F_FB = 32, F_S2 = 64;
+constexpr int F_REG = 1, F_OUT = 2, F_TB = 4, F_LY = 8, F_T8 = 16, F_FB = 32;
 constexpr int kTbQ = 4;
 
 #ifndef IS3D_SPLIT_BYTES
@@ -334,36 +330,6 @@ __device__ __forceinline__ void sep_phi_loop_tb_tail(const SepLane& L, double mT
   }
 }
 
-// F_S2: two Grad species of one lane over the same {b', Phi} / {PD, T1} rows -- one pair of table reads per two
-// points.  T0 / T1: that species is a Boltzmann-tail lane (sep_quad_tb_tail_t) or a fast one (sep_quad_tb_t);
-// acc = [species 0: KJ points][species 1: KJ points]
-template <int FLAGS, int KJ, bool T0, bool T1>
-__device__ __forceinline__ void sep_phi_loop_tb2(const SepLane& L0, double mT0, const SepLane& L1, double mT1,
-                                                 const dbl2* BP, const dbl2* PT, double* acc) {
-  constexpr bool REG = (FLAGS & F_REG) != 0, OUT = (FLAGS & F_OUT) != 0;
-  static_assert(KJ % 4 == 0, "F_S2 needs phi blocks of fours");
-#pragma unroll
-  for (int jj = 0; jj < KJ; jj += 4) {
-    dbl2 b[4], pt[4];
-#pragma unroll
-    for (int i = 0; i < 4; i++) { b[i] = BP[jj + i]; pt[i] = PT[jj + i]; }
-    if (T0) sep_quad_tb_tail_t<SEP_GRAD, REG, OUT>(L0, mT0, b, pt, nullptr, acc + jj);
-    else {
-      double v[4];
-      sep_quad_tb_t<SEP_GRAD, REG, OUT>(L0, mT0, b, pt, nullptr, v);
-#pragma unroll
-      for (int i = 0; i < 4; i++) acc[jj + i] += v[i];
-    }
-    if (T1) sep_quad_tb_tail_t<SEP_GRAD, REG, OUT>(L1, mT1, b, pt, nullptr, acc + KJ + jj);
-    else {
-      double v[4];
-      sep_quad_tb_t<SEP_GRAD, REG, OUT>(L1, mT1, b, pt, nullptr, v);
-#pragma unroll
-      for (int i = 0; i < 4; i++) acc[KJ + jj + i] += v[i];
-    }
-  }
-}
-
 // Boltzmann-tail Grad lanes of an F_TB launch, PD-table form: {b', Phi} and PD from LDS, {pc, ps} by scalar
 // loads (sep_quad_pd_tail_t; 6 LDS-array cycles per point instead of 8)
 template <int FLAGS, int KJ, typename CSP>
@@ -511,8 +477,6 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
   extern __shared__ double smem[];
   const int nphp = A.njb * KJ;                            // phi rows padded to KJ multiples
   constexpr bool TB = (MODE == GRAD || MODE == CE) && (FLAGS & F_TB) != 0 && KJ % 4 == 0;
-  constexpr bool S2 = TB && MODE == GRAD && (FLAGS & F_S2) != 0;   // two species per lane
-  constexpr int SPL = S2 ? 2 : 1;
   constexpr bool FB = MODE >= PTM && (FLAGS & F_FB) != 0;   // separable-fallback launch of a modified mode
   constexpr bool MODMAIN = MODE >= PTM && !FB;              // modified launch: separable lanes left to F_FB
   constexpr bool LY = (FLAGS & F_LY) != 0 || FB;
@@ -568,8 +532,8 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
   const bool active = task < A.ntask;
   int s = 0, q = 0, jb = 0;
   if (active) {
-    s = SPL * (int)(task % A.npl);
-    const long r = task / A.npl;
+    s = (int)(task % A.npart);
+    const long r = task / A.npart;
     q = (int)(r % A.nq);
     jb = (int)(r / A.nq);
   }
@@ -582,10 +546,10 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
   int nqw = 1;
   {
     const long t0 = (long)lane_group * kBlock, t1 = min(A.ntask, t0 + kBlock) - 1;
-    r0 = t0 / A.npl;
-    nqw = (int)(t1 / A.npl - r0) + 1;
+    r0 = t0 / A.npart;
+    nqw = (int)(t1 / A.npart - r0) + 1;
   }
-  const int row = active ? (int)(task / A.npl - r0) : 0;
+  const int row = active ? (int)(task / A.npart - r0) : 0;
   // the LDS row tables are sized for nqmax rows (host, spectra_plan): a launch whose workgroup spans more
   // would write past them, so it computes nothing and returns NaN spectra instead (never on a host plan)
   const bool rows_ok = LY || nqw <= A.nqmax;
@@ -596,11 +560,6 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
   const int yrow = allq ? q : row;
   const double mass = A.smass[s], m2 = mass * mass, sign = A.ssign[s], baryon = A.sbaryon[s];
   const double mT = sqrt(m2 + pT * pT), mT2 = mT * mT, mTb = mT * baryon;
-  // F_S2: the lane's second species (mass-sorted neighbour; none past the end of the list)
-  const bool has1 = S2 && active && s + 1 < A.npart;
-  const int s1 = has1 ? s + 1 : s;
-  const double mass1 = A.smass[s1], m2_1 = mass1 * mass1, sign1 = A.ssign[s1], baryon1 = A.sbaryon[s1];
-  const double mT1 = sqrt(m2_1 + pT * pT), mT2_1 = mT1 * mT1, mTb1 = mT1 * baryon1;
 
   // per-workgroup constants into LDS: inside the cell loop the only global loads are the
   // record prefetch (and PTM's renormalisation factor)
@@ -618,9 +577,9 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
     s_grid[A.nk + A.nl + i] = (A.dim == 3) ? 1.0 : A.etaw[i];
   }
 
-  double acc[SPL * KJ];     // F_S2: [species of the pair][phi point]
+  double acc[KJ];
 #pragma unroll
-  for (int jj = 0; jj < SPL * KJ; jj++) acc[jj] = 0.0;
+  for (int jj = 0; jj < KJ; jj++) acc[jj] = 0.0;
 
   // F_FB: positions in the fallback cell list (its length is known on the device only), split evenly
   long c_begin, c_end;
@@ -634,7 +593,7 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
   }
   const int* const fbl = FB ? A.fbcells : nullptr;
   // this thread's slab entries, layout [split][pT][lane group][phi slot][lane] (see the stores at the end)
-  double* const out = A.slab + (long)split * A.sstride + ((long)ipt * A.nbx + lane_group) * (SPL * KJ * kBlock) + tid;
+  double* const out = A.slab + (long)split * A.sstride + ((long)ipt * A.nbx + lane_group) * (KJ * kBlock) + tid;
 
   // ---- phase A / B of one tile (records s_rec, ntx cells) into table buffer tb: {b', Phi} and PD (or
   // the modified path's {PDm, Qv}) per (cell, phi), {TE, T2} for RTA-CE's table launch, y-terms per
@@ -784,35 +743,7 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
         // neither kernel carries the other's code)
         if (MODMAIN && sep) continue;
         if (FB && !sep) continue;
-        if constexpr (S2) {           // Grad F_TB, two species per lane
-          SepLane L0, L1;
-          sep_setup(SEP_GRAD, R, Y, mT, mT2, m2, mTb, pT, sign, baryon, s_etab, L0, IS3D_TAIL);
-          if (has1) sep_setup(SEP_GRAD, R, Y, mT1, mT2_1, m2_1, mTb1, pT, sign1, baryon1, s_etab, L1, IS3D_TAIL);
-          else L1.skip = 1;
-          const dbl2* PT = s_pt + ((long)t * nqw + row) * prow;
-          const bool f0 = !L0.skip && L0.fast, f1 = !L1.skip && L1.fast;
-          if (f0 && f1) {
-            const int v = (L0.tail ? 1 : 0) | (L1.tail ? 2 : 0);
-            if (v == 0) sep_phi_loop_tb2<FLAGS, KJ, false, false>(L0, mT, L1, mT1, BP, PT, acc);
-            else if (v == 1) sep_phi_loop_tb2<FLAGS, KJ, true, false>(L0, mT, L1, mT1, BP, PT, acc);
-            else if (v == 2) sep_phi_loop_tb2<FLAGS, KJ, false, true>(L0, mT, L1, mT1, BP, PT, acc);
-            else sep_phi_loop_tb2<FLAGS, KJ, true, true>(L0, mT, L1, mT1, BP, PT, acc);
-            continue;
-          }
-          // one species skipped (exp underflow) or on the per-point exp path: each on its own loop
-          if (!L0.skip) {
-            if (L0.tail) sep_phi_loop_tb_tail<MODE, FLAGS, KJ>(L0, mT, BP, PT, nullptr, acc);
-            else if (L0.fast) sep_phi_loop_tb<MODE, FLAGS, KJ>(L0, mT, BP, PT, nullptr, acc);
-            else sep_phi_loop<MODE, FLAGS, false, KJ>(L0, s_cs + j0, BP, acc);
-          }
-          if (!L1.skip) {
-            if (L1.tail) sep_phi_loop_tb_tail<MODE, FLAGS, KJ>(L1, mT1, BP, PT, nullptr, acc + KJ);
-            else if (L1.fast) sep_phi_loop_tb<MODE, FLAGS, KJ>(L1, mT1, BP, PT, nullptr, acc + KJ);
-            else sep_phi_loop<MODE, FLAGS, false, KJ>(L1, s_cs + j0, BP, acc + KJ);
-          }
-          continue;
-        }
-        if constexpr (!MODMAIN && !S2) {     // Grad / RTA-CE lanes (sep throughout), the F_FB launch's separable lanes
+        if constexpr (!MODMAIN) {     // Grad / RTA-CE lanes (sep throughout), the F_FB launch's separable lanes
           SepLane L;
           sep_setup(sep_flavor(MODE), R, Y, mT, mT2, m2, mTb, pT, sign, baryon, s_etab, L,
                     TB && IS3D_TAIL && (MODE == GRAD || IS3D_TAIL_CE));
@@ -857,7 +788,7 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
   // one contiguous 512-byte row; non-temporal so the stream does not evict the cell records the
   // XCD's other workgroups are still reading from L2.  k_reduce scatters into the reference layout.
 #pragma unroll
-  for (int jj = 0; jj < SPL * KJ; jj++) __builtin_nontemporal_store(rows_ok ? acc[jj] : __builtin_nan(""), out + jj * kBlock);
+  for (int jj = 0; jj < KJ; jj++) __builtin_nontemporal_store(rows_ok ? acc[jj] : __builtin_nan(""), out + jj * kBlock);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1113,23 +1044,8 @@ void launch_spectra_kj(dim3 grid, size_t shmem, hipStream_t st, const SpecArgs& 
   }
 }
 
-// the Grad two-species table launch (F_S2): its only instantiations are these KJ = 16 ones
-template <int MODE>
-void launch_spectra_s2(dim3 grid, size_t shmem, hipStream_t st, const SpecArgs& a, int flags) {
-  switch (flags & 3) {
-    case 0: hipLaunchKernelGGL((k_spectra<MODE, F_TB | F_S2, 16>), grid, dim3(kBlock), shmem, st, a); break;
-    case 1: hipLaunchKernelGGL((k_spectra<MODE, F_TB | F_S2 | 1, 16>), grid, dim3(kBlock), shmem, st, a); break;
-    case 2: hipLaunchKernelGGL((k_spectra<MODE, F_TB | F_S2 | 2, 16>), grid, dim3(kBlock), shmem, st, a); break;
-    default: hipLaunchKernelGGL((k_spectra<MODE, F_TB | F_S2 | 3, 16>), grid, dim3(kBlock), shmem, st, a); break;
-  }
-}
-
 template <int MODE>
 void launch_spectra(dim3 grid, size_t shmem, hipStream_t st, const SpecArgs& a, int flags, int kj) {
-  if (flags & F_S2) {
-    if constexpr (MODE == GRAD) { if (kj == 16) launch_spectra_s2<MODE>(grid, shmem, st, a, flags); }
-    return;
-  }
   switch (kj) {
 #ifdef IS3D_KJ16
     case 16: launch_spectra_kj<MODE, 16>(grid, shmem, st, a, flags); break;

@@ -60,8 +60,9 @@ def write_run_dir(d, surf, params, hrg_eos=2, chosen="pikp", pT="pT24", phi="phi
         synth.write_music(os.path.join(d, "input", "surface.dat"), surf, include_baryon=baryon)
     elif surface_format == 7:
         synth.write_hic(os.path.join(d, "input", "surface.dat"), surf)
-    else:
-        synth.write_mode1(os.path.join(d, "input", "surface.dat"), surf, include_baryon=baryon)
+    else:       # 1, or 5 = 1 + thermal-vorticity columns
+        synth.write_mode1(os.path.join(d, "input", "surface.dat"), surf, include_baryon=baryon,
+                          vorticity_seed=(5 if surface_format == 5 else None))
     write_pdg(d, hrg_eos)
     pp = np.load(os.path.join(_DATA, "pdg.npz"))
     mc = pp["chosen_" + chosen] if isinstance(chosen, str) else np.asarray(chosen)

@@ -74,9 +74,10 @@ def surface(n, seed=7, dimension=2, baryon=False, full3d=False):
     return {k: np.ascontiguousarray(s[k], dtype=np.float64) for k in FIELDS}
 
 
-def write_mode1(path, surf, include_baryon=False):
+def write_mode1(path, surf, include_baryon=False, vorticity_seed=None):
     """input/surface.dat in the CPU-VH format (readindata.cpp:179-202): E, T, P, pi, Pi and muB
-    stored in fm units (divided by hbarc), %.17g."""
+    stored in fm units (divided by hbarc), %.17g.  vorticity_seed: mode 5 -- six thermal-vorticity
+    columns wbar^{tx ty tn xy xn yn} after the rest (readindata.cpp:298-306; read, not used by the spectra)."""
     cols = ["tau", "x", "y", "eta", "dat", "dax", "day", "dan", "ux", "uy", "un", "E", "T", "P",
             "pixx", "pixy", "pixn", "piyy", "piyn", "bulkPi"]
     if include_baryon:
@@ -85,6 +86,9 @@ def write_mode1(path, surf, include_baryon=False):
     for k in cols:
         v = np.asarray(surf[k], dtype=np.float64)
         arr.append(v / HBARC if k in _HBARC_FIELDS else v)
+    if vorticity_seed is not None:
+        w = np.random.default_rng(vorticity_seed).normal(0.0, 0.05, (6, len(surf["tau"])))
+        arr.extend(list(w))
     a = np.stack(arr, axis=1)
     with open(path, "w") as f:
         for row in a:

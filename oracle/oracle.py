@@ -51,11 +51,14 @@ def build():
 
 
 def load():
+    """The oracle library: oracle/libis3d_oracle.so, or IS3D_ORACLE_LIB (bench.py's cpu_baseline leg points it at
+    a -march=native build made on the GPU box's host)."""
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB):
+        path = os.environ.get("IS3D_ORACLE_LIB") or LIB
+        if path == LIB and not os.path.exists(LIB):
             build()
-        lib = C.CDLL(LIB)
+        lib = C.CDLL(path)
         lib.orc_spectra.argtypes = [C.POINTER(OrcParams), C.POINTER(OrcSetup), C.POINTER(OrcSurface), PD,
                                     C.POINTER(C.c_long), C.c_char_p, C.c_int]
         lib.orc_dndx.argtypes = [C.POINTER(OrcParams), C.POINTER(OrcSetup), C.POINTER(OrcSurface),

@@ -25,7 +25,7 @@ def harness(args, cwd):
 
 
 @need_ref
-@pytest.mark.parametrize("fmt,dim,baryon", [(1, 2, 0), (1, 3, 1), (6, 3, 0), (6, 3, 1), (7, 2, 0)])
+@pytest.mark.parametrize("fmt,dim,baryon", [(1, 2, 0), (1, 3, 1), (5, 2, 0), (5, 3, 1), (6, 3, 0), (6, 3, 1), (7, 2, 0)])
 def test_surface_readers_match_reference(tmp_path, fmt, dim, baryon):
     s = synth.surface(200, seed=21, dimension=dim, baryon=bool(baryon), full3d=(dim == 3 and fmt != 7))
     d = rundir.write_run_dir(str(tmp_path), s, dict(dimension=dim, df_mode=1, include_baryon=baryon,
@@ -37,7 +37,7 @@ def test_surface_readers_match_reference(tmp_path, fmt, dim, baryon):
     ref_avg = np.array([float(v) for v in out[1 + n].split()])
     fields, avg = host.read_surface(d, fmt, dim, baryon)
     for k, name in enumerate(synth.FIELDS):
-        if not baryon and name in ("nB", "Vx", "Vy", "Vn") or (fmt == 1 and not baryon and name == "muB"):
+        if not baryon and name in ("nB", "Vx", "Vy", "Vn") or (fmt in (1, 5) and not baryon and name == "muB"):
             continue
         np.testing.assert_array_equal(fields[k], ref[:, k], err_msg=name)
     np.testing.assert_array_equal(avg, ref_avg)
