@@ -1580,10 +1580,36 @@ IS3D_HD double sqrt_nr(double v) {
 // table lanes (!clamp) e^chem is folded out of the exponential into sign and the p.dsigma
 // coefficients (en = e^chem e^-E/T: en / (1 + sign en) = e^chem e / (1 + (sign e^chem) e)), so a point
 // evaluates e^(-sig E_mod) alone.
+// Plus form (IS3D_MOD_PLUS, table lanes): f = 1 / (e^x + sign e^chem) e^chem with x = E_mod / T_mod evaluated as
+//   f = 2^-k / (E + s),  E = e^x 2^-k,  s = sign e^chem 2^-k,  2^-k e^chem folded into the p.dsigma coefficients,
+// where k = floor(x_min / ln2) over the lane's phi points (from mod_setup's lower bound) keeps E in [~1, 2^250]:
+// four denominators multiply without overflow and the scale costs nothing per point (2^-k enters the range
+// reduction's shift constant, shiftk = 1.5 2^52 - N k).  The numerator is 1, so a point saves the en x q_j product
+// of the en form (f = en / (1 + s en)); it is also the reference's own form, 1 / (exp(E/T - chem) + sign)
+// (MomentumSpectra.cpp:946-950).  Lanes whose phi range exceeds 250 binades take the clamped en form.
+#ifndef IS3D_MOD_PLUS
+#define IS3D_MOD_PLUS 1
+#endif
+// degree of the modified lanes' 2^(r/N) polynomial: 3 (minimax, 3.5e-14 relative) or 4 (Taylor, ~1 ulp)
+#ifndef IS3D_MOD_EXP_DEG
+#define IS3D_MOD_EXP_DEG 3
+#endif
+#if IS3D_EXP_TAB_BITS == 8 && IS3D_MOD_EXP_DEG == 3
+static constexpr int kModExpDeg = 3;
+// near-minimax (Chebyshev) coefficients of (2^(r/256) - 1) / r on |r| <= 1/2: 1 + r p(r) within 3.5e-14
+static constexpr double kModExpA[3] = {0.0027076061740622863, 3.6655660167967235e-06, 3.308302907918888e-09};
+#else
+static constexpr int kModExpDeg = kExpTabDeg;
+#define kModExpA kExpTabCoefs
+#endif
+struct ModExpCoef { double a[kModExpDeg]; };
+
 struct ModLane {
   double E0, Ec, Es, D0, Dc, Ds, chemm, sign;   // table lanes: sign = sign e^chem, D = |renorm| e^chem D
+                                                // (plus form: both x 2^-k)
   double mT, Dw;               // table form (mod_quad_tab_t): E_mod^2 = E0 + Qv + mT T2, p.dsigma = D0 + Dw PDm
-  ExpTabCoef et;               // pinned once per lane setup, reused by every phi point
+  double shiftk;               // plus form: 1.5 2^52 - kExpTabN k (the lane's 2^-k in the range reduction)
+  ModExpCoef et;               // pinned once per lane setup, reused by every phi point
   const double* etab;          // 2^(j/kExpTabN) table (LDS on the device)
   int skip, clamp;   // clamp: some point's exp argument may leave the table lanes' domain (exp_clamped instead)
 };
@@ -1621,7 +1647,7 @@ IS3D_HD void mod_setup(const double* R, const double* Y, double mT, double m2, d
   L.Es = tm * fma(ux, R[R_VSX], fma(uy, R[R_VSY], uz * R[R_VSZ]));
   L.mT = mT;
   L.chemm = baryon * R[R_CHEMM];
-  L.et = exp_tab_coef();
+  for (int i = 0; i < kModExpDeg; i++) L.et.a[i] = kconst(kModExpA[i]);
   L.etab = etab;
   // | |mT U| - pT |V|max | <= |p_mod| <= |mT U| + pT |V|max (sig units): if even the smallest E_mod
   // overflows exp, every phi point is exactly 0; if the largest could leave the table lanes' domain
@@ -1640,59 +1666,118 @@ IS3D_HD void mod_setup(const double* R, const double* Y, double mT, double m2, d
   const double emax = sqrt(m2s + hi * hi) * kLn2overN;
   L.clamp = (emax < kModTabX && fabs(L.chemm) < kModTabChem) ? 0 : 1;
 #endif
+  int k = 0;
+#if IS3D_MOD_PLUS
+  if (!L.clamp) {
+    // k = floor(x_min / ln2) from the lane's smallest sig E_mod (a lower bound of it: rounding down only
+    // raises E by a factor < 2); the largest point must stay within 250 binades of 2^k
+    const double e2 = m2s + (lo > 0.0 ? lo * lo : 0.0);
+#if defined(__HIP_DEVICE_COMPILE__)
+    const double emin = e2 * __builtin_amdgcn_rsq(e2);
+#else
+    const double emin = sqrt(e2);
+#endif
+    k = (int)(emin * ((1.0 - 1e-6) / kExpTabN));
+    const double xk = (k + 250.0) * kExpTabN;
+    if (!(m2s + hi * hi < xk * xk)) L.clamp = 1;
+  }
+#endif
   // e^chem of the table lanes (1 for mesons and without baryon chemistry: a wave-uniform skip there)
   double ec = 1.0;
-  if (!L.clamp && L.chemm != 0.0) ec = exp_tab(L.et, etab, L.chemm * kInvLn2xN);
-  const double d = renorm_abs * ec;
-  L.sign = sign * ec;
+  if (!L.clamp && L.chemm != 0.0) ec = exp_tab(exp_tab_coef(), etab, L.chemm * kInvLn2xN);
+  if (L.clamp) k = 0;
+  L.shiftk = 6755399441055744.0 - (double)k * kExpTabN;
+  const double d = ldexp(renorm_abs * ec, -k);
+  L.sign = ldexp(sign * ec, -k);
   L.D0 = d * (mT * Y[Y_MD]); L.Dc = d * Y[Y_WDX]; L.Ds = d * Y[Y_WDY];
   L.Dw = d * Y[Y_W];
 }
 
-// en at one phi point (qv = modqv of the cell at this phi): e^(chem - E_mod / T_mod) on clamped lanes,
-// e^(-E_mod / T_mod) on table lanes (e^chem folded into the lane, mod_setup)
+// The Fermi/Bose factor of one point as num / q: clamped lanes num = en = e^(chem - E_mod/T_mod),
+// q = 1 + sign en; table lanes in the plus form num = 1, q = E + s (see ModLane), in the en form (IS3D_MOD_PLUS 0)
+// num = en = e^(-E_mod/T_mod), q = 1 + s en.  X = (sig E_mod)^2: one Newton step of the v_rsq_f64 estimate y
+// folded into the exp argument, sig E_mod = g v with g = X y, v = 1.5 - 0.5 g y, and the range reduction folded
+// into the product (t = fma(g, v, shift) rounds g v to the integer K exactly, rs = fma(g, v, shift - t))
 template <bool CLAMP>
-IS3D_HD double mod_en(const ModLane& L, dbl2 cs, double qv) {
-  const double Emod = sqrt_nr(fma(L.Ec, cs.x, fma(L.Es, cs.y, L.E0 + qv)));   // sig E_mod
-  if (CLAMP) return exp_clamped(exp_coef(), fma(-Emod, kLn2overN, L.chemm));
-  return exp_tab(L.et, L.etab, -Emod);
+IS3D_HD void mod_nq_x(const ModLane& L, double X, double& num, double& q) {
+  if (CLAMP) {
+    num = exp_clamped(exp_coef(), fma(-sqrt_nr(X), kLn2overN, L.chemm));
+    q = fma(L.sign, num, 1.0);
+    return;
+  }
+#if defined(__HIP_DEVICE_COMPILE__)
+  const double y = __builtin_amdgcn_rsq(X);
+#else
+  const double y = 1.0 / sqrt(X);
+#endif
+  const double g = IS3D_MOD_PLUS ? X * y : -(X * y);
+  const double v = fma(-0.5, X * y * y, 1.5);
+  const double sh = IS3D_MOD_PLUS ? L.shiftk : kconst(6755399441055744.0);
+  const double t = fma(g, v, sh);
+  const double rs = fma(g, v, sh - t);
+  const int ki = (int)(unsigned)__builtin_bit_cast(unsigned long long, t);
+  double p = L.et.a[kModExpDeg - 1];
+#pragma unroll
+  for (int i = kModExpDeg - 2; i >= 0; i--) p = fma(p, rs, L.et.a[i]);
+  const double T = L.etab[ki & (kExpTabN - 1)];
+  const double e = ldexp(fma(T, rs * p, T), ki >> IS3D_EXP_TAB_BITS);
+  if (IS3D_MOD_PLUS) { num = 1.0; q = e + L.sign; }
+  else { num = e; q = fma(L.sign, e, 1.0); }
+}
+
+// the same from the lane's linear form (qv = modqv of the cell at this phi)
+template <bool CLAMP>
+IS3D_HD void mod_nq(const ModLane& L, dbl2 cs, double qv, double& num, double& q) {
+  mod_nq_x<CLAMP>(L, fma(L.Ec, cs.x, fma(L.Es, cs.y, L.E0 + qv)), num, q);
 }
 
 template <bool OUT, bool CLAMP>
 IS3D_HD double mod_point_t(const ModLane& L, dbl2 cs, double qv) {
-  const double en = mod_en<CLAMP>(L, cs, qv);
+  double num, q;
+  mod_nq<CLAMP>(L, cs, qv, num, q);
   const double pds = lin(L.D0, L.Dc, L.Ds, cs);
-  const double r = pds * (en * rcp1(fma(L.sign, en, 1.0)));
+  const double r = pds * (num * rcp1(q));
   return (OUT && pds <= 0.0) ? 0.0 : r;
+}
+
+// two points, one reciprocal: f_0 = num_0 q_1 / (q_0 q_1)
+IS3D_HD void mod_pair_f(double n0, double q0, double n1, double q1, double& f0, double& f1) {
+  const double r = rcp1(q0 * q1);
+  f0 = n0 * (r * q1);
+  f1 = n1 * (r * q0);
 }
 
 template <bool OUT, bool CLAMP>
 IS3D_HD void mod_pair_t(const ModLane& L, dbl2 c0, dbl2 c1, dbl2 qv, double& v0, double& v1) {
-  const double en0 = mod_en<CLAMP>(L, c0, qv.x), en1 = mod_en<CLAMP>(L, c1, qv.y);
-  const double q0 = fma(L.sign, en0, 1.0), q1 = fma(L.sign, en1, 1.0);
-  const double r = rcp1(q0 * q1);
+  double n0, q0, n1, q1, f0, f1;
+  mod_nq<CLAMP>(L, c0, qv.x, n0, q0);
+  mod_nq<CLAMP>(L, c1, qv.y, n1, q1);
+  mod_pair_f(n0, q0, n1, q1, f0, f1);
   const double pds0 = lin(L.D0, L.Dc, L.Ds, c0), pds1 = lin(L.D0, L.Dc, L.Ds, c1);
-  const double g0 = pds0 * (en0 * (r * q1)), g1 = pds1 * (en1 * (r * q0));
-  v0 = (OUT && pds0 <= 0.0) ? 0.0 : g0;
-  v1 = (OUT && pds1 <= 0.0) ? 0.0 : g1;
+  v0 = (OUT && pds0 <= 0.0) ? 0.0 : pds0 * f0;
+  v1 = (OUT && pds1 <= 0.0) ? 0.0 : pds1 * f1;
 }
 
-// four points, one reciprocal (1 + sign en lies in ~[1e-3, 2], so the product of four is normal)
-template <bool OUT, bool CLAMP>
-IS3D_HD void mod_quad_t(const ModLane& L, const dbl2* c, dbl2 qa, dbl2 qb, double* v) {
-  const double en[4] = {mod_en<CLAMP>(L, c[0], qa.x), mod_en<CLAMP>(L, c[1], qa.y), mod_en<CLAMP>(L, c[2], qb.x),
-                        mod_en<CLAMP>(L, c[3], qb.y)};
-  double q[4];
-#pragma unroll
-  for (int i = 0; i < 4; i++) q[i] = fma(L.sign, en[i], 1.0);
+// four points, one reciprocal (the four denominators lie in ~[1e-3, 2] (en form) or [~1, 2^250] (plus form),
+// so their product is normal): rq_i = 1 / q_i as r q_j q_k q_l
+IS3D_HD void mod_quad_rq(const double* q, double* rq) {
   const double q01 = q[0] * q[1], q23 = q[2] * q[3];
   const double r = rcp1(q01 * q23);
   const double r01 = r * q23, r23 = r * q01;
-  const double rq[4] = {r01 * q[1], r01 * q[0], r23 * q[3], r23 * q[2]};
+  rq[0] = r01 * q[1]; rq[1] = r01 * q[0]; rq[2] = r23 * q[3]; rq[3] = r23 * q[2];
+}
+
+template <bool OUT, bool CLAMP>
+IS3D_HD void mod_quad_t(const ModLane& L, const dbl2* c, dbl2 qa, dbl2 qb, double* v) {
+  double num[4], q[4], rq[4];
+  const double qv[4] = {qa.x, qa.y, qb.x, qb.y};
+#pragma unroll
+  for (int i = 0; i < 4; i++) mod_nq<CLAMP>(L, c[i], qv[i], num[i], q[i]);
+  mod_quad_rq(q, rq);
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     const double pds = lin(L.D0, L.Dc, L.Ds, c[i]);
-    const double g = pds * (en[i] * rq[i]);
+    const double g = pds * (num[i] * rq[i]);
     v[i] = (OUT && pds <= 0.0) ? 0.0 : g;
   }
 }
@@ -1710,38 +1795,22 @@ IS3D_HD double modt2(const double* R, const double* Y, dbl2 cs) {
   return 2.0 * fma(Y[Y_MUX], wx, fma(Y[Y_MUY], wy, Y[Y_MUZ] * wz));
 }
 
-// en from X = (sig E_mod)^2: one Newton step of the v_rsq_f64 estimate y folded into the exp argument,
-// sig E_mod = g v with g = X y, v = 1.5 - 0.5 g y, and the range reduction folded into the product
-// (exp_tab_fma): 6 ops + rsq where sqrt_nr, the 1/T_mod scale, chem and the reduction took 9
-template <bool CLAMP>
-IS3D_HD double mod_en_x(const ModLane& L, double X) {
-  if (CLAMP) return exp_clamped(exp_coef(), fma(-sqrt_nr(X), kLn2overN, L.chemm));
-#if defined(__HIP_DEVICE_COMPILE__)
-  const double y = __builtin_amdgcn_rsq(X);
-#else
-  const double y = 1.0 / sqrt(X);
-#endif
-  const double g = X * y;
-  const double v = fma(-0.5, g * y, 1.5);
-  return exp_tab_fma(L.et, L.etab, -g, v);
-}
-
-// mod_en_x for four points in stages: the four range reductions, then the four table reads issued
+// mod_nq_x for four points in stages: the four range reductions, then the four table reads issued
 // together, then the four polynomials (independent of the reads), then the products -- so one LDS
 // latency is waited for per four points instead of per one or two (same operations, same results)
 #ifndef IS3D_MOD_STAGED
 #define IS3D_MOD_STAGED 1
 #endif
 template <bool CLAMP>
-IS3D_HD void mod_en4(const ModLane& L, const double* X, double* en) {
+IS3D_HD void mod_nq4(const ModLane& L, const double* X, double* num, double* q) {
   if (CLAMP || !IS3D_MOD_STAGED) {
 #pragma unroll
-    for (int i = 0; i < 4; i++) en[i] = mod_en_x<CLAMP>(L, X[i]);
+    for (int i = 0; i < 4; i++) mod_nq_x<CLAMP>(L, X[i], num[i], q[i]);
     return;
   }
-  const ExpTabCoef& E = L.et;
   double t[4], rs[4], T[4], p[4];
   int ki[4];
+  const double sh = IS3D_MOD_PLUS ? L.shiftk : kconst(6755399441055744.0);
 #pragma unroll
   for (int i = 0; i < 4; i++) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -1749,82 +1818,71 @@ IS3D_HD void mod_en4(const ModLane& L, const double* X, double* en) {
 #else
     const double y = 1.0 / sqrt(X[i]);
 #endif
-    const double g = X[i] * y;
-    const double v = fma(-0.5, g * y, 1.5);
-    t[i] = fma(-g, v, E.shift);
-    rs[i] = fma(-g, v, E.shift - t[i]);
+    const double g = IS3D_MOD_PLUS ? X[i] * y : -(X[i] * y);
+    const double v = fma(-0.5, X[i] * y * y, 1.5);
+    t[i] = fma(g, v, sh);
+    rs[i] = fma(g, v, sh - t[i]);
     ki[i] = (int)(unsigned)__builtin_bit_cast(unsigned long long, t[i]);
   }
 #pragma unroll
   for (int i = 0; i < 4; i++) T[i] = L.etab[ki[i] & (kExpTabN - 1)];
 #pragma unroll
   for (int i = 0; i < 4; i++) {
-    double q = E.a[kExpTabDeg - 1];
+    double a = L.et.a[kModExpDeg - 1];
 #pragma unroll
-    for (int k = kExpTabDeg - 2; k >= 0; k--) q = fma(q, rs[i], E.a[k]);
-    p[i] = rs[i] * q;
+    for (int k = kModExpDeg - 2; k >= 0; k--) a = fma(a, rs[i], L.et.a[k]);
+    p[i] = rs[i] * a;
   }
 #pragma unroll
-  for (int i = 0; i < 4; i++) en[i] = ldexp(fma(T[i], p[i], T[i]), ki[i] >> IS3D_EXP_TAB_BITS);
+  for (int i = 0; i < 4; i++) {
+    const double e = ldexp(fma(T[i], p[i], T[i]), ki[i] >> IS3D_EXP_TAB_BITS);
+    if (IS3D_MOD_PLUS) { num[i] = 1.0; q[i] = e + L.sign; }
+    else { num[i] = e; q[i] = fma(L.sign, e, 1.0); }
+  }
 }
 
-// four points, one reciprocal, accumulated into acc: f_i = en_i / q_i = en_i q_j (1 / q_i q_j) with j the
-// pair partner, so acc_i = fma(pds_i en_i q_j, r_ij, acc_i) -- 4 ops per point after the shared reciprocal
+// four points, one reciprocal, accumulated into acc: f_i = num_i / q_i = num_i q_j (1 / q_i q_j) with j the
+// pair partner, so acc_i = fma(pds_i num_i q_j, r_ij, acc_i) (plus form: num_i = 1) -- 4 ops per point after the
+// shared reciprocal
 template <bool OUT, bool CLAMP, typename ACC>
 IS3D_HD void mod_quad_tab_t(const ModLane& L, const dbl2* mw, const double* mt, ACC acc) {
-  double en[4], q[4], X[4];
+  double num[4], q[4], X[4];
 #pragma unroll
   for (int i = 0; i < 4; i++) X[i] = fma(L.mT, mt[i], L.E0 + mw[i].y);
-  mod_en4<CLAMP>(L, X, en);
-#pragma unroll
-  for (int i = 0; i < 4; i++) q[i] = fma(L.sign, en[i], 1.0);
+  mod_nq4<CLAMP>(L, X, num, q);
   const double q01 = q[0] * q[1], q23 = q[2] * q[3];
   const double r = rcp1(q01 * q23);
-#if IS3D_MODQ_ACC
   const double rp[4] = {r * q23, r * q23, r * q01, r * q01};
-  const double h[4] = {en[0] * q[1], en[1] * q[0], en[2] * q[3], en[3] * q[2]};
+  const double h[4] = {num[0] * q[1], num[1] * q[0], num[2] * q[3], num[3] * q[2]};
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     double pds = fma(L.Dw, mw[i].x, L.D0);
     if (OUT) pds = (pds <= 0.0) ? 0.0 : pds;
     acc[i] = fma(pds * h[i], rp[i], acc[i]);
   }
-#else
-  const double r01 = r * q23, r23 = r * q01;
-  const double rq[4] = {r01 * q[1], r01 * q[0], r23 * q[3], r23 * q[2]};
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const double pds = fma(L.Dw, mw[i].x, L.D0);
-    const double g = pds * (en[i] * rq[i]);
-    acc[i] += (OUT && pds <= 0.0) ? 0.0 : g;
-  }
-#endif
 }
 
 template <bool OUT, bool CLAMP>
 IS3D_HD void mod_pair_tab_t(const ModLane& L, dbl2 mw0, dbl2 mw1, double mt0, double mt1, double& v0, double& v1) {
-  const double en0 = mod_en_x<CLAMP>(L, fma(L.mT, mt0, L.E0 + mw0.y));
-  const double en1 = mod_en_x<CLAMP>(L, fma(L.mT, mt1, L.E0 + mw1.y));
-  const double q0 = fma(L.sign, en0, 1.0), q1 = fma(L.sign, en1, 1.0);
-  const double r = rcp1(q0 * q1);
+  double n0, q0, n1, q1, f0, f1;
+  mod_nq_x<CLAMP>(L, fma(L.mT, mt0, L.E0 + mw0.y), n0, q0);
+  mod_nq_x<CLAMP>(L, fma(L.mT, mt1, L.E0 + mw1.y), n1, q1);
+  mod_pair_f(n0, q0, n1, q1, f0, f1);
   const double pds0 = fma(L.Dw, mw0.x, L.D0), pds1 = fma(L.Dw, mw1.x, L.D0);
-  const double g0 = pds0 * (en0 * (r * q1)), g1 = pds1 * (en1 * (r * q0));
-  v0 = (OUT && pds0 <= 0.0) ? 0.0 : g0;
-  v1 = (OUT && pds1 <= 0.0) ? 0.0 : g1;
+  v0 = (OUT && pds0 <= 0.0) ? 0.0 : pds0 * f0;
+  v1 = (OUT && pds1 <= 0.0) ? 0.0 : pds1 * f1;
 }
 
-// two points of a modified lane from its linear forms and Qv (no q-row table): as mod_pair_t with the
-// exp argument of mod_en_x
+// two points of a modified lane from its linear forms and Qv (no q-row table)
 template <bool OUT, bool CLAMP>
 IS3D_HD void mod_pair_lane_t(const ModLane& L, dbl2 c0, dbl2 c1, double qv0, double qv1, double& v0, double& v1) {
-  const double en0 = mod_en_x<CLAMP>(L, fma(L.Ec, c0.x, fma(L.Es, c0.y, L.E0 + qv0)));
-  const double en1 = mod_en_x<CLAMP>(L, fma(L.Ec, c1.x, fma(L.Es, c1.y, L.E0 + qv1)));
-  const double q0 = fma(L.sign, en0, 1.0), q1 = fma(L.sign, en1, 1.0);
-  const double r = rcp1(q0 * q1);
+  double n0, q0, n1, q1, f0, f1;
+  mod_nq<CLAMP>(L, c0, qv0, n0, q0);
+  mod_nq<CLAMP>(L, c1, qv1, n1, q1);
+  mod_pair_f(n0, q0, n1, q1, f0, f1);
   const double pds0 = lin(L.D0, L.Dc, L.Ds, c0), pds1 = lin(L.D0, L.Dc, L.Ds, c1);
-  const double g0 = pds0 * (en0 * (r * q1)), g1 = pds1 * (en1 * (r * q0));
-  v0 = (OUT && pds0 <= 0.0) ? 0.0 : g0;
-  v1 = (OUT && pds1 <= 0.0) ? 0.0 : g1;
+  v0 = (OUT && pds0 <= 0.0) ? 0.0 : pds0 * f0;
+  v1 = (OUT && pds1 <= 0.0) ? 0.0 : pds1 * f1;
 }
 
 IS3D_HD void mod_quad(const ModLane& L, const dbl2* c, dbl2 qa, dbl2 qb, int outflow, double* v) {
