@@ -201,9 +201,10 @@ def executed_roofline(args, mode, ms_spectra, ms_total, neta, units_local, n_loc
     return r
 
 
-def run_workload(args, cfg_name, mode, steps, warmup, rank, world, local_rank, dev, dist):
+def run_workload(args, cfg_name, mode, steps, warmup, rank, world, local_rank, dev, dist, classes=True):
     """Build the engine for one workload on this rank's shard, run `warmup` untimed and `steps` timed
-    passes (barrier + synchronize on both sides, max over ranks) and return the measurement."""
+    passes (barrier + synchronize on both sides, max over ranks) and return the measurement.  classes: the
+    engine's integrand classes (is3d_set_species_classes; the default) or one integral per species."""
     import torch
     from is3d2_amd import build_engine, make_spec
     from is3d2_amd import dist as D
@@ -226,7 +227,8 @@ def run_workload(args, cfg_name, mode, steps, warmup, rank, world, local_rank, d
     mine = surf if window is None else {k: v[window[0]:window[1]] for k, v in surf.items()}
     T_avg = D.global_averages(D.average_sums(mine, flags.get("include_baryon", 0)), reduce)[0]
 
-    eng = build_engine(spec, surf, T_avg=T_avg, device=local_rank)
+    eng = build_engine(spec, surf, T_avg=T_avg, device=local_rank, species_classes=classes)
+    n_integrated = eng.species_integrated()
     if window is not None:
         eng.set_cell_window(*window)
     outsize = eng.output_size()
@@ -289,6 +291,7 @@ def run_workload(args, cfg_name, mode, steps, warmup, rank, world, local_rank, d
                        "" if neta == 1 else " x %d eta" % neta),
         "operation": operation,
         "cells_per_gpu": n_local, "species": nsp, "grid": [npT, nphi, ny, neta], "df_mode": mode,
+        "species_integrated": n_integrated,
         "famod_chains": spec["params"]["famod_chains"] if mode == 5 else None,
         "parallelism": "dp%d (cell shards + RCCL all-reduce of spectra)" % world if world > 1 else "1 GPU",
     }
@@ -308,6 +311,8 @@ def main():
     ap.add_argument("--operation", type=int, default=1, choices=[0, 1],
                     help="1 continuous spectra (default, the BASELINE metric); 0 spacetime distributions dN/dX")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-per-species", action="store_true",
+                    help="skip the second timing of the main workload with one integral per species (classes off)")
     ap.add_argument("--cpu-seconds", type=float, default=25.0)
     ap.add_argument("--north-star-steps", type=int, default=3,
                     help="timed passes of the north_star workload (config4: 10^6 3+1D cells, SMASH, RTA-CE, "
@@ -331,6 +336,17 @@ def main():
     from is3d2_amd import _lib
     log("build_id %s" % _lib.build_id())
     m = run_workload(args, args.config, args.df_mode, args.steps, args.warmup, rank, world, local_rank, dev, dist)
+    per_species = None
+    if not args.no_per_species and m["config"]["species_integrated"] < m["config"]["species"]:
+        # the same workload with one integral per species (integrand classes off): bit-identical spectra, the
+        # kernel's per-species rate (tests/test_gpu_classes.py)
+        o = run_workload(args, args.config, args.df_mode, args.steps, 1, rank, world, local_rank, dev, dist,
+                         classes=False)
+        per_species = {"value": o["value"], "ms_per_step": 1e3 * o["elapsed"] / o["steps"], "steps": o["steps"],
+                       "species_integrated": o["config"]["species_integrated"],
+                       "kernel_ms": o["roofline"]["kernel_ms"],
+                       "note": "same workload and clock rules with integrand classes off (is3d_set_species_classes(e, 0)): "
+                               "every species integrated separately; the same spectra (bit for bit at the BASELINE sizes, tests/test_gpu_classes.py)"}
     ns = None
     if args.north_star_steps > 0 and args.config != "config4" and args.operation == 1:
         n = run_workload(args, "config4", 0, args.north_star_steps, 1, rank, world, local_rank, dev, dist)
@@ -356,6 +372,8 @@ def main():
             "config": m["config"],
             "roofline": m["roofline"],
         }
+        if per_species is not None:
+            res["per_species_integration"] = per_species
         if ns is not None:
             res["north_star"] = ns
         if world == 1 and not args.no_cpu_baseline:

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define IS3D_ABI_VERSION 3
+#define IS3D_ABI_VERSION 4
 
 enum {
   IS3D_OK = 0,
@@ -128,6 +128,16 @@ const char *is3d_last_error(const is3d_engine *e);
 int is3d_set_params(is3d_engine *e, const is3d_params *p);
 int is3d_set_species(is3d_engine *e, int n, const double *mass, const double *sign,
                      const double *degeneracy, const double *baryon);
+/* Integrand classes (no reference counterpart: an engine option, default on).  The momentum integrals see a
+ * species only through its (mass, sign, baryon) -- and, for PTM, its degeneracy, which enters the
+ * renormalisation (MomentumSpectra.cpp:800-808) -- while the degeneracy multiplies the result
+ * (MomentumSpectra.cpp:365).  With classes on, chosen species with identical keys are integrated once and the
+ * reduction writes every member (prefactor x its degeneracy x the shared cell sum): the spectra are
+ * bit-identical to integrating each species separately (on = 0) when both take the same launch plan (at the
+ * BASELINE sizes), otherwise equal to rounding (the class count can change the cell-split grouping).
+ * is3d_species_integrated returns the number of species the kernels integrate (SMASH 444 -> 193). */
+int is3d_set_species_classes(is3d_engine *e, int on);
+int is3d_species_integrated(is3d_engine *e);
 int is3d_set_pdg(is3d_engine *e, int n, const double *mass, const double *sign,
                  const double *degeneracy, const double *baryon);
 int is3d_set_momentum_grid(is3d_engine *e, int npT, const double *pT, int nphi, const double *phi,

@@ -382,13 +382,22 @@ __global__ __launch_bounds__(1024) void k_fbscan(const double* rec, long n, int*
 
 struct ReduceArgs {
   const double* slab; long sstride; int nsplit;
-  int nbx, npart, npT, nphi, nk, nl, ny_out, kj; long ntask;
+  int nbx, npart, npT, nphi, nk, nl, ny_out, kj; long ntask;   // npart: lane species (integrand classes)
   const int* sorig; const double* degen_orig; double prefactor;
+  const int *cmem_off, *cmem;   // member sorted species of each class
   double* out;
 };
 
+// every member species of class c gets (2 pi hbarc)^-3 g_s x the class's sum
+__device__ __forceinline__ void write_members(const ReduceArgs& A, int c, long off, double acc, int m0, int dm) {
+  for (int m = A.cmem_off[c] + m0; m < A.cmem_off[c + 1]; m += dm) {
+    const int so = A.sorig[A.cmem[m]];
+    A.out[(long)so * A.npT * A.nphi * A.ny_out + off] = A.prefactor * A.degen_orig[so] * acc;
+  }
+}
+
 // dN[s][pT][phi][y] = (2 pi hbarc)^-3 g_s * sum over eta nodes (2+1D) and cell splits, in fixed order.
-// One thread per slab entry of an l = 0 lane; the lanes of the other eta nodes of the same (species, y,
+// One thread per slab entry of an l = 0 lane; the lanes of the other eta nodes of the same (class, y,
 // phi block) are task + l * npart.
 __global__ __launch_bounds__(256) void k_reduce(ReduceArgs A) {
   const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -413,8 +422,7 @@ __global__ __launch_bounds__(256) void k_reduce(ReduceArgs A) {
     const long el = ((long)ipt * A.nbx + tl / kBlock) * ((long)KJ * kBlock) + (long)jj * kBlock + tl % kBlock;
     for (int z = 0; z < A.nsplit; z++) acc += A.slab[(long)z * A.sstride + el];
   }
-  const int so = A.sorig[s];
-  A.out[(((long)so * A.npT + ipt) * A.nphi + j) * A.ny_out + k] = A.prefactor * A.degen_orig[so] * acc;
+  write_members(A, s, ((long)ipt * A.nphi + j) * A.ny_out + k, acc, 0, 1);
 }
 
 // The same sum with one wavefront per output entry, for slabs with many (eta node, cell split) terms per
@@ -444,10 +452,7 @@ __global__ __launch_bounds__(256) void k_reduce_wave(ReduceArgs A) {
   }
 #pragma unroll
   for (int w = 32; w >= 1; w >>= 1) acc += __shfl_xor(acc, w, 64);
-  if (lane == 0) {
-    const int so = A.sorig[s];
-    A.out[(((long)so * A.npT + ipt) * A.nphi + j) * A.ny_out + k] = A.prefactor * A.degen_orig[so] * acc;
-  }
+  write_members(A, s, ((long)ipt * A.nphi + j) * A.ny_out + k, acc, lane, 64);
 }
 
 // per-cell spacetime bin indices (SpacetimeDistribution.cpp:380-392): keys[0..2][c] = itau, ir, iphi (-1 outside)
@@ -477,9 +482,10 @@ __global__ __launch_bounds__(256) void k_stkeys(KeyArgs A) {
 // part[s_orig][e] = prefactor g_s x sum over the cells of entry e = (distribution, thread slice n, bin),
 // cells in ascending order (the reference's per-thread order); perm/offs: CSR built on the host
 struct BinArgs {
-  const double* ycell; long n; int npart;
+  const double* ycell; long n; int npart;          // ycell: [class][n]; npart sorted species
   const int *perm; const long* offs; long nent;
   const int* sorig; const double* sdegen; double prefactor;
+  const int* scls;                                  // sorted species -> integrand class
   double* part;
 };
 
@@ -491,7 +497,7 @@ __global__ __launch_bounds__(256) void k_stbin(BinArgs A) {
   const double f = A.prefactor * A.sdegen[s];
   double acc = 0.0;
   for (long i = A.offs[e]; i < A.offs[e + 1]; i++) {
-    acc += f * A.ycell[(long)s * A.n + A.perm[i]];
+    acc += f * A.ycell[(long)A.scls[s] * A.n + A.perm[i]];
   }
   A.part[(long)A.sorig[s] * A.nent + e] = acc;
 }
@@ -681,6 +687,18 @@ struct is3d_engine {
   int* d_rcls = nullptr;
   int* d_rrep = nullptr;
   int nrcls = 0;
+  // integrand classes (is3d_set_species_classes, default on): the momentum integrals see a species only through
+  // its (mass, sign, baryon) -- plus its degeneracy in PTM, whose renormalisation is evaluated per (mass, sign,
+  // degeneracy, baryon) -- and the engine applies the degeneracy once, to the cell sum, in k_reduce (the reference
+  // multiplies every cell's term by prefactor x degeneracy, MomentumSpectra.cpp:365: the same product up to
+  // rounding), so sorted species with identical keys have bit-identical cell sums: k_spectra / k_dndx integrate one lane species per class (SMASH 444 -> 193, UrQMD 305 -> 124) and the
+  // reduction writes every member.  d_cmass/d_csign/d_cbaryon: class values, d_crcls: class -> renorm class,
+  // d_cmem[d_cmem_off[c] ..]: member sorted species of class c, d_scls: sorted species -> class.
+  bool classes = true;
+  int ncls = 0;
+  std::vector<int> scls;   // host copy of d_scls
+  const double *d_cmass = nullptr, *d_csign = nullptr, *d_cbaryon = nullptr;
+  int *d_crcls = nullptr, *d_cmem_off = nullptr, *d_cmem = nullptr, *d_scls = nullptr;
   double* d_surf = nullptr; bool surf_owned = false; long ncell = 0; long surf_cap = 0;
   double* d_chain = nullptr; long chain_cap = 0;   // PTMA warm-start chain segments (k_chain_pass)
   double *d_rec = nullptr, *d_aux = nullptr, *d_sol = nullptr, *d_renorm = nullptr, *d_slab = nullptr, *d_out = nullptr;
@@ -809,6 +827,23 @@ extern "C" int is3d_set_species(is3d_engine* e, int n, const double* mass, const
   return IS3D_OK;
 }
 
+static int finalize_tables(is3d_engine* e);
+
+extern "C" int is3d_set_species_classes(is3d_engine* e, int on) {
+  if (e && e->grp) return is3d::group_set_species_classes(e->grp, on);
+  if (!e) return IS3D_ERR_ARG;
+  e->classes = on != 0;
+  e->tables_dirty = true;
+  return IS3D_OK;
+}
+
+extern "C" int is3d_species_integrated(is3d_engine* e) {
+  if (e && e->grp) return is3d::group_species_integrated(e->grp);
+  if (!e) return IS3D_ERR_ARG;
+  const int rc = finalize_tables(e);
+  return rc ? rc : e->ncls;
+}
+
 extern "C" int is3d_set_pdg(is3d_engine* e, int n, const double* mass, const double* sign, const double* degeneracy,
                             const double* baryon) {
   if (e && e->grp) return is3d::group_set_pdg(e->grp, n, mass, sign, degeneracy, baryon);
@@ -932,7 +967,7 @@ struct SpectraPlan {
 static SpectraPlan spectra_plan(const is3d_engine* e) {
   SpectraPlan P{};
   const int mode = e->p.df_mode, dim = e->p.dimension;
-  const int np = (int)e->mass.size(), nphi = (int)e->phi.size();
+  const int np = e->ncls, nphi = (int)e->phi.size();     // lane species: the integrand classes
   const int nk = (dim == 3) ? (int)e->y.size() : 1, nl = (dim == 3) ? 1 : (int)e->eta.size();
   P.nq = nk * nl;
   auto shape = [&](int KJ) {
@@ -1076,6 +1111,36 @@ static int finalize_tables(is3d_engine* e) {
   std::vector<double> pTw(e->pT.size(), 0.0), phiw(e->phi.size(), 0.0);
   if (e->have_weights) { pTw = e->pT_w; phiw = e->phi_w; }
   const size_t opw = cput(pTw.data(), pTw.size()), ophw = cput(phiw.data(), phiw.size());
+  // integrand classes of the sorted species (first occurrence order, so the class list stays mass-sorted)
+  std::vector<int> scls(np), crep, cmem_off, cmem;
+  {
+    std::map<std::array<uint64_t, 4>, int> cls;
+    for (int i = 0; i < np; i++) {
+      const std::array<uint64_t, 4> key{__builtin_bit_cast(uint64_t, sm[i]), __builtin_bit_cast(uint64_t, ss[i]),
+                                        __builtin_bit_cast(uint64_t, sb[i]),
+                                        mode == PTM ? __builtin_bit_cast(uint64_t, sd[i]) : (uint64_t)0};
+      int c = (int)crep.size();
+      if (e->classes) {
+        auto it = cls.find(key);
+        if (it == cls.end()) it = cls.emplace(key, c).first;
+        c = it->second;
+      }
+      if (c == (int)crep.size()) crep.push_back(i);
+      scls[i] = c;
+    }
+    const int nc = (int)crep.size();
+    cmem_off.assign(nc + 1, 0);
+    for (int i = 0; i < np; i++) cmem_off[scls[i] + 1]++;
+    for (int c = 0; c < nc; c++) cmem_off[c + 1] += cmem_off[c];
+    cmem.resize(np);
+    std::vector<int> fill(cmem_off.begin(), cmem_off.end() - 1);
+    for (int i = 0; i < np; i++) cmem[fill[scls[i]]++] = i;
+    e->ncls = nc;
+    e->scls = scls;
+  }
+  std::vector<double> cm(e->ncls), csn(e->ncls), cby(e->ncls);
+  for (int c = 0; c < e->ncls; c++) { cm[c] = sm[crep[c]]; csn[c] = ss[crep[c]]; cby[c] = sb[crep[c]]; }
+  const size_t ocm = cput(cm.data(), e->ncls), ocs_ = cput(csn.data(), e->ncls), ocb = cput(cby.data(), e->ncls);
   // {pT cos phi, pT sin phi} per (pT, padded phi slot) for k_spectra's scalar loads (same products as
   // its LDS copy s_cs); 16-byte aligned
   if (cb.size() & 1) cb.push_back(0.0);
@@ -1130,20 +1195,33 @@ static int finalize_tables(is3d_engine* e) {
     }
   }
   e->nrcls = (int)rrep.size();
-  std::vector<double> sorig(np);
+  const int nc = e->ncls;
+  std::vector<int> crcls(nc);
+  for (int c = 0; c < nc; c++) crcls[c] = rcls[crep[c]];
+  // ints after the doubles: sorig[np] | rcls[np] | rrep[np] | crcls[nc] | cmem_off[nc + 1] | cmem[np] | scls[np]
+  std::vector<int> ib;
+  for (int i = 0; i < np; i++) ib.push_back(e->order[i]);
+  ib.insert(ib.end(), rcls.begin(), rcls.end());
+  rrep.resize(np, 0);
+  ib.insert(ib.end(), rrep.begin(), rrep.end());
+  ib.insert(ib.end(), crcls.begin(), crcls.end());
+  ib.insert(ib.end(), cmem_off.begin(), cmem_off.end());
+  ib.insert(ib.end(), cmem.begin(), cmem.end());
+  ib.insert(ib.end(), scls.begin(), scls.end());
   dfree(e->d_const);
-  const size_t nconst = cb.size() + 3 * (size_t)np;   // ints appended as raw space: sorig, rcls, rrep
-  e->d_const = dalloc<double>(nconst);
+  e->d_const = dalloc<double>(cb.size() + (ib.size() + 1) / 2);
   if (!e->d_const) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(constants) failed");
   HIPCHK(e, hipMemcpy(e->d_const, cb.data(), cb.size() * sizeof(double), hipMemcpyHostToDevice));
-  std::vector<int> so(np);
-  for (int i = 0; i < np; i++) so[i] = e->order[i];
-  e->d_sorig = (int*)(e->d_const + cb.size());
-  HIPCHK(e, hipMemcpy(e->d_sorig, so.data(), np * sizeof(int), hipMemcpyHostToDevice));
-  e->d_rcls = (int*)(e->d_const + cb.size() + np);
-  e->d_rrep = (int*)(e->d_const + cb.size() + 2 * (size_t)np);
-  HIPCHK(e, hipMemcpy(e->d_rcls, rcls.data(), np * sizeof(int), hipMemcpyHostToDevice));
-  if (!rrep.empty()) HIPCHK(e, hipMemcpy(e->d_rrep, rrep.data(), rrep.size() * sizeof(int), hipMemcpyHostToDevice));
+  int* const di = (int*)(e->d_const + cb.size());
+  HIPCHK(e, hipMemcpy(di, ib.data(), ib.size() * sizeof(int), hipMemcpyHostToDevice));
+  e->d_sorig = di;
+  e->d_rcls = di + np;
+  e->d_rrep = di + 2 * (size_t)np;
+  e->d_crcls = di + 3 * (size_t)np;
+  e->d_cmem_off = e->d_crcls + nc;
+  e->d_cmem = e->d_cmem_off + nc + 1;
+  e->d_scls = e->d_cmem + np;
+  e->d_cmass = e->d_const + ocm; e->d_csign = e->d_const + ocs_; e->d_cbaryon = e->d_const + ocb;
   e->d_smass = e->d_const + osm; e->d_ssign = e->d_const + oss; e->d_sbaryon = e->d_const + osb; e->d_sdegen = e->d_const + osd;
   e->d_degen_orig = e->d_const + odg; e->d_pT = e->d_const + opt; e->d_cphi = e->d_const + oc; e->d_sphi = e->d_const + os;
   e->d_y = e->d_const + oy; e->d_eta = e->d_const + oe; e->d_etaw = e->d_const + ow;
@@ -1346,14 +1424,15 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   const int KJ = P.KJ, njb = P.njb;
   if (!spectra_kj_supported(KJ)) return e->fail(IS3D_ERR_ARG, "internal: no k_spectra instantiation for this phi block");
   if (P.shmem > 160 * 1024) return e->fail(IS3D_ERR_ARG, "momentum grid too large for the LDS tile (phi table)");
-  const long ntask = (long)np * nk * nl * njb;
+  const int nc = e->ncls;      // lane species: one per integrand class (the reduction writes the members)
+  const long ntask = (long)nc * nk * nl * njb;
   const long bx = (ntask + kBlock - 1) / kBlock;
   if (!P.ly) {
     // k_spectra's LDS row tables hold nqmax rows per cell; a lane group spanning more would compute nothing
     // (its slab is NaN-filled, rows_ok), so refuse the launch here instead of returning NaN spectra
     for (long g = 0; g < bx; g++) {
       const long t0 = g * kBlock, t1 = std::min(ntask, t0 + kBlock) - 1;
-      if (t1 / np - t0 / np + 1 > P.nqmax)
+      if (t1 / nc - t0 / nc + 1 > P.nqmax)
         return e->fail(IS3D_ERR_ARG, "internal: k_spectra lane group spans more q rows than the LDS plan");
     }
   }
@@ -1382,11 +1461,11 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
     HIPCHK(e, hipGetLastError());
   }
   SpecArgs sa{};
-  sa.rec = rec_w; sa.n = nw; sa.renorm = e->d_renorm; sa.rcls = e->d_rcls; sa.nrcls = e->nrcls; sa.slab = e->d_slab; sa.outsize = outsize;
-  sa.smass = e->d_smass; sa.ssign = e->d_ssign; sa.sbaryon = e->d_sbaryon; sa.sorig = e->d_sorig;
+  sa.rec = rec_w; sa.n = nw; sa.renorm = e->d_renorm; sa.rcls = e->d_crcls; sa.nrcls = e->nrcls; sa.slab = e->d_slab; sa.outsize = outsize;
+  sa.smass = e->d_cmass; sa.ssign = e->d_csign; sa.sbaryon = e->d_cbaryon; sa.sorig = e->d_sorig;
   sa.csg = e->d_csg;
   sa.pT = e->d_pT; sa.cphi = e->d_cphi; sa.sphi = e->d_sphi; sa.yv = e->d_y; sa.etav = e->d_eta; sa.etaw = e->d_etaw;
-  sa.npart = np; sa.npT = npT; sa.nphi = nphi; sa.ny_out = ny_out; sa.nk = nk; sa.nl = nl; sa.nq = nk * nl; sa.njb = njb;
+  sa.npart = nc; sa.npT = npT; sa.nphi = nphi; sa.ny_out = ny_out; sa.nk = nk; sa.nl = nl; sa.nq = nk * nl; sa.njb = njb;
   sa.nqmax = P.nqmax;
   sa.ntask = ntask; sa.cells_per_split = cps; sa.nbx = (int)bx; sa.nsplit = (int)nsplit; sa.sstride = sstride;
   sa.regulate = e->p.regulate_deltaf; sa.outflow = e->p.outflow; sa.dim = dim; sa.op = 1;
@@ -1418,13 +1497,14 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   HIPCHK(e, hipEventRecord(e->ev[2], st));
   ReduceArgs ra{};
   ra.slab = e->d_slab; ra.sstride = sstride; ra.nsplit = (int)(nsplit + nsplit_fb);
-  ra.nbx = (int)bx; ra.npart = np; ra.npT = npT; ra.nphi = nphi; ra.nk = nk; ra.nl = nl; ra.ny_out = ny_out; ra.kj = KJ;
+  ra.nbx = (int)bx; ra.npart = nc; ra.npT = npT; ra.nphi = nphi; ra.nk = nk; ra.nl = nl; ra.ny_out = ny_out; ra.kj = KJ;
   ra.ntask = ntask;
   ra.sorig = e->d_sorig; ra.degen_orig = e->d_degen_orig; ra.prefactor = std::pow(2.0 * M_PI * kHbarC, -3);
+  ra.cmem_off = e->d_cmem_off; ra.cmem = e->d_cmem;
   ra.out = dev_out;
   // one wavefront per output when each output sums many (eta node, split) terms and there are few outputs
   if ((long)nl * ra.nsplit >= 128 && sstride / nl < (1L << 20)) {
-    const long nout = (long)np * npT * nphi * ny_out;
+    const long nout = (long)nc * npT * nphi * ny_out;
     hipLaunchKernelGGL(k_reduce_wave, dim3((unsigned)((nout + 3) / 4)), dim3(256), 0, st, ra);
   } else {
     hipLaunchKernelGGL(k_reduce, dim3((unsigned)((sstride + 255) / 256)), dim3(256), 0, st, ra);
@@ -1539,20 +1619,21 @@ extern "C" int is3d_calculate_dN_dX(is3d_engine* e, double* dN_taudtaudy, double
     const int KJ = spectra_kj(nphi);
     const int njb = (nphi + KJ - 1) / KJ;
     DndxArgs da{};
+    const int nc = e->ncls;    // lane species: the integrand classes (k_stbin scales and writes the members)
     da.ntask = nk * njb * nl;
-    da.Sl = std::min(np, 64);
+    da.Sl = std::min(nc, 64);
     da.Yl = 64 / da.Sl;
-    da.nbx = (np + da.Sl - 1) / da.Sl;
+    da.nbx = (nc + da.Sl - 1) / da.Sl;
     long cpw = 4L * kTile;
     if ((long)da.nbx * ((n + cpw - 1) / cpw) < 4096) cpw = kTile;
     da.cells_per_wg = cpw;
     da.nchunk = (n + cpw - 1) / cpw;
-    if (!ensure(e->d_ycell, e->ycell_cap, (long)np * n)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(cell yields) failed");
-    da.rec = e->d_rec; da.n = n; da.renorm = e->d_renorm; da.rcls = e->d_rcls; da.nrcls = e->nrcls; da.ycell = e->d_ycell;
-    da.smass = e->d_smass; da.ssign = e->d_ssign; da.sbaryon = e->d_sbaryon;
+    if (!ensure(e->d_ycell, e->ycell_cap, (long)nc * n)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(cell yields) failed");
+    da.rec = e->d_rec; da.n = n; da.renorm = e->d_renorm; da.rcls = e->d_crcls; da.nrcls = e->nrcls; da.ycell = e->d_ycell;
+    da.smass = e->d_cmass; da.ssign = e->d_csign; da.sbaryon = e->d_cbaryon;
     da.pT = e->d_pT; da.pTw = e->d_pTw; da.cphi = e->d_cphi; da.sphi = e->d_sphi; da.phiw = e->d_phiw;
     da.yv = e->d_y; da.etav = e->d_eta; da.etaw = e->d_etaw;
-    da.npart = np; da.npT = npT; da.nphi = nphi; da.nk = nk; da.nl = nl; da.nq = nk * nl; da.njb = njb; da.dim = dim;
+    da.npart = nc; da.npT = npT; da.nphi = nphi; da.nk = nk; da.nl = nl; da.nq = nk * nl; da.njb = njb; da.dim = dim;
     const size_t nphp = (size_t)njb * KJ;
     const size_t shmem = sizeof(double) * ((size_t)kTile * NREC + 2 * nphp + 2 * nphp + nphp + 3 * (size_t)kTile * nphp +
                                            (size_t)kTile * kBlock + (size_t)(nk + 2 * nl) + (size_t)kTile * da.nq * kYRowLY + kExpTabN);
@@ -1609,6 +1690,7 @@ extern "C" int is3d_calculate_dN_dX(is3d_engine* e, double* dN_taudtaudy, double
     ba.ycell = e->d_ycell; ba.n = n; ba.npart = np;
     ba.perm = e->d_perm; ba.offs = e->d_offs; ba.nent = nent;
     ba.sorig = e->d_sorig; ba.sdegen = e->d_sdegen; ba.prefactor = std::pow(2.0 * M_PI * kHbarC, -3);
+    ba.scls = e->d_scls;
     ba.part = e->d_part;
     const long nthr = nent * np;
     hipLaunchKernelGGL(k_stbin, dim3((unsigned)((nthr + 255) / 256)), dim3(256), 0, st, ba);
@@ -1666,13 +1748,13 @@ extern "C" int is3d_get_cell_yields(const is3d_engine* e, double* dN_dy_cell) {
   const long n = e->ycell_n;
   const int np = (int)e->mass.size();
   if (n == 0) return IS3D_OK;
-  std::vector<double> y((size_t)np * n);
+  std::vector<double> y((size_t)e->ncls * n);
   if (hipSetDevice(e->device) != hipSuccess) return IS3D_ERR_DEVICE;
   if (hipMemcpy(y.data(), e->d_ycell, y.size() * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess) return IS3D_ERR_DEVICE;
   const double pref = std::pow(2.0 * M_PI * kHbarC, -3);
   for (int s = 0; s < np; s++) {
     const int so = e->order[s];
-    for (long c = 0; c < n; c++) dN_dy_cell[(size_t)so * n + c] = pref * e->degen[so] * y[(size_t)s * n + c];
+    for (long c = 0; c < n; c++) dN_dy_cell[(size_t)so * n + c] = pref * e->degen[so] * y[(size_t)e->scls[s] * n + c];
   }
   return IS3D_OK;
 }

@@ -164,6 +164,10 @@ int group_set_species(Group* g, int n, const double* m, const double* s, const d
   if (!rc) g->np = n;
   return rc;
 }
+int group_set_species_classes(Group* g, int on) {
+  return each(g, [&](is3d_engine* e) { return is3d_set_species_classes(e, on); });
+}
+int group_species_integrated(Group* g) { return is3d_species_integrated(g->sh[0]); }
 int group_set_pdg(Group* g, int n, const double* m, const double* s, const double* d, const double* b) {
   return each(g, [&](is3d_engine* e) { return is3d_set_pdg(e, n, m, s, d, b); });
 }

@@ -88,6 +88,17 @@ class Engine:
         self._chk(self.lib.is3d_set_species(self._e, len(a[0]), *[_dp(x) for x in a]))
         self.npart = len(a[0])
 
+    def set_species_classes(self, on=True):
+        """Integrate species with identical (mass, sign, baryon [, degeneracy for PTM]) once (default on);
+        the spectra equal the per-species integration (bit for bit at the BASELINE sizes, include/is3d_amd.h)."""
+        self._chk(self.lib.is3d_set_species_classes(self._e, int(bool(on))))
+
+    def species_integrated(self):
+        n = self.lib.is3d_species_integrated(self._e)
+        if n < 0:
+            self._chk(n)
+        return n
+
     def set_pdg(self, mass, sign, degen, baryon):
         a = [_arr(x) for x in (mass, sign, degen, baryon)]
         self._chk(self.lib.is3d_set_pdg(self._e, len(a[0]), *[_dp(x) for x in a]))
@@ -223,12 +234,14 @@ def make_spec(hrg_eos=2, chosen="pikp", pT="pT24", phi="phi24", y="y21", eta="et
                 pT_w=pTw, phi_w=phiw, bins=bins, gla=(roots, weights), df=(T, muB, tab), hrg_eos=hrg_eos)
 
 
-def build_engine(spec, surf, T_avg=None, device=0, devices=None):
+def build_engine(spec, surf, T_avg=None, device=0, devices=None, species_classes=True):
     e = Engine(device, devices)
     p = spec["params"]
     e.set_params(**p)
     sp = spec["species"]
     e.set_species(sp["mass"], sp["sign"], sp["degen"], sp["baryon"])
+    if not species_classes:
+        e.set_species_classes(False)
     pdg = spec["pdg"]
     e.set_pdg(pdg["mass"], pdg["sign"], pdg["gspin"], pdg["baryon"])
     e.set_momentum_grid(spec["pT"], spec["phi"], spec["y"], spec["eta"], spec["eta_w"])

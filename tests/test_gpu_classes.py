@@ -1,0 +1,112 @@
+"""GPU tier: integrand classes (is3d_set_species_classes, include/is3d_amd.h).
+
+The momentum integrals see a chosen species only through its (mass, sign, baryon) -- plus its degeneracy in
+PTM, whose n_linear / n_mod renormalisation carries it (MomentumSpectra.cpp:800-808) -- and the degeneracy
+multiplies the result (MomentumSpectra.cpp:365).  The engine therefore integrates one lane species per class
+(SMASH 444 -> 193, UrQMD 305 -> 124) and its reduction writes every member.  These tests check that the
+spectra, dN/dX and per-cell yields are bit-identical to the per-species integration (classes off) wherever
+both launches take the same plan (phi block, cell splits: the BASELINE sizes), and equal to rounding where
+the class count changes the plan; every oracle comparison elsewhere in the GPU tier runs with classes on (the default)."""
+import numpy as np
+import pytest
+
+from helpers import parity
+from is3d2_amd import build_engine, make_spec, synth
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def spectra(spec, s, classes):
+    e = build_engine(spec, s, species_classes=classes)
+    n = e.species_integrated()
+    out = e.calculate_spectra()
+    st = e.stats()
+    e.close()
+    return out, n, st
+
+
+@pytest.mark.parametrize("mode", [1, 2, 3, 4, 5])
+def test_classes_bit_identical_config3_grid(mode):
+    """Config 3's shape (SMASH 444 x 48 x 32 x 21, 3+1D, shear + bulk (+ baryon + diffusion; PTB without,
+    DeltafData.cpp:480-483)): classes on and off give the same bits, and the class count is the key's."""
+    baryon = mode != 4
+    s = synth.as_read(synth.surface(10, seed=41, dimension=3, baryon=baryon, full3d=True))
+    spec = make_spec(hrg_eos=2, chosen="smash", df_mode=mode, dimension=3, pT="pT48", phi="phi32", y="y21",
+                     include_baryon=int(baryon), include_baryondiff_deltaf=int(baryon), famod_chains=1)
+    on, n_on, st_on = spectra(spec, s, True)
+    off, n_off, st_off = spectra(spec, s, False)
+    sp = spec["species"]
+    key = zip(sp["mass"], sp["sign"], sp["baryon"], sp["degen"] if mode == 3 else [0] * len(sp["mass"]))
+    assert n_off == len(sp["mass"]) == 444
+    assert n_on == len(set(key)) == (205 if mode == 3 else 193)
+    assert np.array_equal(on, off)
+    assert st_on["breakdown"] == st_off["breakdown"]
+
+
+def test_classes_grad_config2_full_size():
+    """Config 2 at full size (10^5 cells, Grad without baryon: the headline's F_TB table launch): the class and
+    per-species launches pick the same phi block and cell splits here, so the spectra agree bit for bit."""
+    s = synth.as_read(synth.surface(100000, seed=7, dimension=3))
+    spec = make_spec(hrg_eos=2, chosen="smash", df_mode=1, dimension=3, pT="pT48", phi="phi32", y="y21")
+    on, n_on, _ = spectra(spec, s, True)
+    off, _, _ = spectra(spec, s, False)
+    assert n_on == 193
+    assert np.array_equal(on, off)
+
+
+def test_classes_small_surface_split_plan():
+    """On a small surface the cell-split count follows the launch's workgroup count (engine.hip: >= 8k
+    workgroups), which the class count changes (16 vs 8 splits at 2000 cells): the slabs group the cells
+    differently, so the sums agree to rounding, not bit for bit (4.3e-11 measured, on entries where the
+    delta-f terms nearly cancel; the oracle bar elsewhere is 1e-8)."""
+    s = synth.as_read(synth.surface(2000, seed=7, dimension=3))
+    spec = make_spec(hrg_eos=2, chosen="smash", df_mode=1, dimension=3, pT="pT48", phi="phi32", y="y21")
+    on, _, _ = spectra(spec, s, True)
+    off, _, _ = spectra(spec, s, False)
+    assert parity(on, off, floor=1e-290)[0] < 1e-9
+
+
+@pytest.mark.parametrize("mode", [1, 3, 5])
+def test_classes_urqmd_2d(mode):
+    """UrQMD (305 -> 124 classes) in 2+1D with 24 eta nodes: a different class count can change the phi-block
+    plan, so the check is the oracle's tolerance plus agreement with the per-species run to rounding."""
+    s = synth.as_read(synth.surface(30, seed=5, dimension=2, baryon=mode == 5))
+    spec = make_spec(hrg_eos=1, chosen="urqmd", df_mode=mode, dimension=2, include_baryon=int(mode == 5),
+                     famod_chains=1)
+    on, n_on, _ = spectra(spec, s, True)
+    off, n_off, _ = spectra(spec, s, False)
+    assert n_off == 305 and n_on < n_off
+    assert parity(on, off, floor=1e-290)[0] < 1e-12
+    ref = O.spectra(spec, s, threads=1)
+    assert parity(on, ref, floor=1e-290)[0] < 1e-8
+
+
+@pytest.mark.parametrize("mode", [1, 3])
+def test_classes_dndx_and_cell_yields(mode):
+    """operation = 0 (k_dndx integrates the classes, k_stbin scales each member): bit-identical bins and
+    per-cell yields."""
+    s = synth.as_read(synth.surface(200, seed=3, dimension=2))
+    spec = make_spec(hrg_eos=2, chosen="smash", df_mode=mode, dimension=2)
+    res = []
+    for classes in (True, False):
+        e = build_engine(spec, s, species_classes=classes)
+        t, r, ph = e.calculate_dN_dX()
+        res.append((t, r, ph, e.cell_yields()))
+        e.close()
+    for a, b in zip(*res):
+        assert np.array_equal(a, b)
+
+
+def test_classes_device_group():
+    """A device list that repeats GPU 0 (the group engine forwards the setting to every shard); two shards sum
+    the cells in another grouping, so the comparison is to rounding (1.6e-10 measured on near-cancelling
+    entries)."""
+    s = synth.as_read(synth.surface(300, seed=9, dimension=3))
+    spec = make_spec(hrg_eos=2, chosen="smash", df_mode=2, dimension=3, pT="pT48", phi="phi32", y="y21")
+    e = build_engine(spec, s, devices=[0, 0])
+    assert e.species_integrated() == 193
+    got = e.calculate_spectra()
+    e.close()
+    off, _, _ = spectra(spec, s, False)
+    assert parity(got, off, floor=1e-290)[0] < 1e-9
