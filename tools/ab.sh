@@ -6,7 +6,7 @@ EXTRA=${AB_EXTRA:-}
 for m in $MODES; do
   for LIB in "$@"; do
     if [ "$LIB" = default ]; then L=""; else L="$LIB"; fi
-    IS3D_LIB=$L timeout -k 10 300 python bench.py --no-cpu-baseline --north-star-steps 0 --steps 3 --warmup 1 \
+    IS3D_LIB=$L timeout -k 10 300 python bench.py --no-cpu-baseline --no-per-species --north-star-steps 0 --steps 3 --warmup 1 \
       --config "$CFG" --df-mode "$m" $EXTRA > /tmp/ab_out.json || exit $?
     python - "$m" "${LIB##*/}" <<'PY'
 import json, sys

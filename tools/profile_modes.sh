@@ -15,7 +15,7 @@ PY=$(command -v python3)
 for M in $MODES; do
   OUT=$R/gpurun_out/prof_${TAG}_${CFG}_m$M
   mkdir -p "$OUT"
-  B="$R/bench.py --no-cpu-baseline --north-star-steps 0 --config $CFG --df-mode $M --steps 2 --warmup 1 $*"
+  B="$R/bench.py --no-cpu-baseline --no-per-species --north-star-steps 0 --config $CFG --df-mode $M --steps 2 --warmup 1 $*"
   timeout -s KILL 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- "$PY" $B > "$OUT/trace.log" 2>&1
   timeout -s KILL 240 rocprofv3 --kernel-trace --output-format csv --pmc SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_INSTS_LDS SQ_WAIT_INST_ANY SQ_BUSY_CYCLES GRBM_GUI_ACTIVE -d "$OUT/pmcA" -o run -- "$PY" $B > "$OUT/pmcA.log" 2>&1
   timeout -s KILL 240 rocprofv3 --kernel-trace --output-format csv --pmc SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_INSTS_VALU_CVT SQ_INSTS_VALU_FLOPS_FP64 -d "$OUT/pmcE" -o run -- "$PY" $B > "$OUT/pmcE.log" 2>&1
