@@ -1591,12 +1591,6 @@ IS3D_HD double sqrt_nr(double v) {
 #define IS3D_MOD_PLUS 1
 #endif
 // degree of the modified lanes' 2^(r/N) polynomial: 3 (minimax, 3.5e-14 relative) or 4 (Taylor, ~1 ulp)
-// Boltzmann-tail lanes (IS3D_MOD_TAIL): where |s| < 2^-55 <= 2^-55 E at every point, E + s == E exactly, so
-// f = 2^-k / E = e^-(x - k ln2) 2^-k: the point evaluates that exponential directly (the shift constant
-// 1.5 2^52 + N k) and skips the denominators and the shared reciprocal (mod_quad_tab_tail_t)
-#ifndef IS3D_MOD_TAIL
-#define IS3D_MOD_TAIL 0
-#endif
 #ifndef IS3D_MOD_EXP_DEG
 #define IS3D_MOD_EXP_DEG 3
 #endif
@@ -1618,7 +1612,6 @@ struct ModLane {
   ModExpCoef et;               // pinned once per lane setup, reused by every phi point
   const double* etab;          // 2^(j/kExpTabN) table (LDS on the device)
   int skip, clamp;   // clamp: some point's exp argument may leave the table lanes' domain (exp_clamped instead)
-  int tail;          // IS3D_MOD_TAIL: Boltzmann-tail table lane (shiftk = 1.5 2^52 + N k, mod_quad_tab_tail_t)
 };
 
 // Qv = |pc Vc + ps Vs|^2 for one (cell, phi), exp-table units (sig^2)
@@ -1644,7 +1637,7 @@ static constexpr double kModTabX = 1.0e6, kModTabChem = 30.0;
 #endif
 
 IS3D_HD void mod_setup(const double* R, const double* Y, double mT, double m2, double pT, double sign, double baryon,
-                       double renorm_abs, const double* etab, ModLane& L, bool ymu = true, bool allow_tail = false) {
+                       double renorm_abs, const double* etab, ModLane& L, bool ymu = true) {
   const double ux = Y[Y_MUX], uy = Y[Y_MUY], uz = Y[Y_MUZ];   // sig U
   const double u2 = ymu ? Y[Y_MU2] : fma(ux, ux, fma(uy, uy, uz * uz));
   const double sig = R[R_INVTM] * kInvLn2xN, m2s = m2 * (sig * sig);
@@ -1693,9 +1686,7 @@ IS3D_HD void mod_setup(const double* R, const double* Y, double mT, double m2, d
   double ec = 1.0;
   if (!L.clamp && L.chemm != 0.0) ec = exp_tab(exp_tab_coef(), etab, L.chemm * kInvLn2xN);
   if (L.clamp) k = 0;
-  // only callers that evaluate tail lanes with mod_quad_tab_tail_t pass allow_tail
-  L.tail = (IS3D_MOD_PLUS && IS3D_MOD_TAIL && allow_tail && !L.clamp && L.chemm * 1.4426950408889634 < k - 55) ? 1 : 0;
-  L.shiftk = 6755399441055744.0 + (L.tail ? 1.0 : -1.0) * ((double)k * kExpTabN);
+  L.shiftk = 6755399441055744.0 - (double)k * kExpTabN;
   const double d = ldexp(renorm_abs * ec, -k);
   L.sign = ldexp(sign * ec, -k);
   L.D0 = d * (mT * Y[Y_MD]); L.Dc = d * Y[Y_WDX]; L.Ds = d * Y[Y_WDY];
@@ -1810,9 +1801,9 @@ IS3D_HD double modt2(const double* R, const double* Y, dbl2 cs) {
 #ifndef IS3D_MOD_STAGED
 #define IS3D_MOD_STAGED 1
 #endif
-template <bool CLAMP, bool TAIL = false>
+template <bool CLAMP>
 IS3D_HD void mod_nq4(const ModLane& L, const double* X, double* num, double* q) {
-  if (!TAIL && (CLAMP || !IS3D_MOD_STAGED)) {
+  if (CLAMP || !IS3D_MOD_STAGED) {
 #pragma unroll
     for (int i = 0; i < 4; i++) mod_nq_x<CLAMP>(L, X[i], num[i], q[i]);
     return;
@@ -1827,7 +1818,7 @@ IS3D_HD void mod_nq4(const ModLane& L, const double* X, double* num, double* q) 
 #else
     const double y = 1.0 / sqrt(X[i]);
 #endif
-    const double g = (IS3D_MOD_PLUS && !TAIL) ? X[i] * y : -(X[i] * y);
+    const double g = IS3D_MOD_PLUS ? X[i] * y : -(X[i] * y);
     const double v = fma(-0.5, X[i] * y * y, 1.5);
     t[i] = fma(g, v, sh);
     rs[i] = fma(g, v, sh - t[i]);
@@ -1845,8 +1836,7 @@ IS3D_HD void mod_nq4(const ModLane& L, const double* X, double* num, double* q) 
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     const double e = ldexp(fma(T[i], p[i], T[i]), ki[i] >> IS3D_EXP_TAB_BITS);
-    if (TAIL) { num[i] = e; q[i] = 1.0; }
-    else if (IS3D_MOD_PLUS) { num[i] = 1.0; q[i] = e + L.sign; }
+    if (IS3D_MOD_PLUS) { num[i] = 1.0; q[i] = e + L.sign; }
     else { num[i] = e; q[i] = fma(L.sign, e, 1.0); }
   }
 }
@@ -1869,21 +1859,6 @@ IS3D_HD void mod_quad_tab_t(const ModLane& L, const dbl2* mw, const double* mt, 
     double pds = fma(L.Dw, mw[i].x, L.D0);
     if (OUT) pds = (pds <= 0.0) ? 0.0 : pds;
     acc[i] = fma(pds * h[i], rp[i], acc[i]);
-  }
-}
-
-// Boltzmann-tail table lane: f 2^k = e^-(x - k ln2) per point, no denominators
-template <bool OUT, typename ACC>
-IS3D_HD void mod_quad_tab_tail_t(const ModLane& L, const dbl2* mw, const double* mt, ACC acc) {
-  double num[4], q[4], X[4];
-#pragma unroll
-  for (int i = 0; i < 4; i++) X[i] = fma(L.mT, mt[i], L.E0 + mw[i].y);
-  mod_nq4<false, true>(L, X, num, q);
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    double pds = fma(L.Dw, mw[i].x, L.D0);
-    if (OUT) pds = (pds <= 0.0) ? 0.0 : pds;
-    acc[i] = fma(pds, num[i], acc[i]);
   }
 }
 

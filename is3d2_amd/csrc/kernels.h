@@ -385,16 +385,6 @@ __device__ __forceinline__ void mod_phi_loop_tab(const ModLane& M, const dbl2* M
   }
 }
 
-// Boltzmann-tail modified lanes, table form (mod_quad_tab_tail_t; KJ % 4 == 0 only: mod_setup's allow_tail)
-template <int FLAGS, int KJ, typename ACC>
-__device__ __forceinline__ void mod_phi_loop_tab_tail(const ModLane& M, const dbl2* MW, const double* MT, ACC acc) {
-  constexpr bool OUT = (FLAGS & F_OUT) != 0;
-  if constexpr (KJ % 4 == 0) {
-#pragma unroll
-    for (int jj = 0; jj < KJ; jj += 4) mod_quad_tab_tail_t<OUT>(M, MW + jj, MT + jj, acc + jj);
-  }
-}
-
 // modified lanes without q-row tables (lane_y launches): {pc, ps} and the {PDm, Qv} rows, the lane's
 // linear forms for E_mod^2 and p.dsigma (mod_quad_lane_t), pairs of points per reciprocal
 template <int FLAGS, bool CLAMP, int KJ, typename ACC>
@@ -779,7 +769,7 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
         }
         if constexpr (MODMAIN) {
           ModLane M;
-          mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, s_etab, M, !LY, !LY && KJ % 4 == 0);
+          mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, s_etab, M, !LY);
           if (M.skip) continue;
           const dbl2* MW = mwt + t * nphp + j0;
           if constexpr (LY) {        // no T2 rows: the lane's linear forms (mod_pair_lane_t)
@@ -789,7 +779,6 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
           }
           const double* MT = s_mt + ((long)t * nqw + row) * prow;
           if (M.clamp) mod_phi_loop_tab<FLAGS, true, KJ>(M, MW, MT, acc);
-          else if (IS3D_MOD_TAIL && M.tail) mod_phi_loop_tab_tail<FLAGS, KJ>(M, MW, MT, acc);
           else mod_phi_loop_tab<FLAGS, false, KJ>(M, MW, MT, acc);
         }
       }
