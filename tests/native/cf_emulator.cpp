@@ -66,6 +66,11 @@ struct EmuTables {
 // 4 = the modified path's table form (mod_quad_tab_t / mod_pair_tab_t), 8 = PTMA Newton sums over hadrons
 // merged by identical (mass, sign) with summed degeneracies, first-occurrence order (engine.hip
 // finalize_tables, IS3D_ANISO_MERGE); without it the sums run per hadron in PDG order as the reference
+// optional lane census of the separable lanes (tools/lane_census.py): [pT][3] counts of skipped, Boltzmann-tail
+// and other lanes per (cell, species, q)
+static long* g_census = nullptr;
+extern "C" void emu_set_census(long* counts) { g_census = counts; }
+
 extern "C" int emu_spectra_v(const orc_params* p, const orc_setup* su, const orc_surface* S, int chains, int op,
                              double* out, long* stats, int variant) {
   const int mode = p->df_mode, dim = p->dimension;
@@ -189,6 +194,7 @@ extern "C" int emu_spectra_v(const orc_params* p, const orc_setup* su, const orc
               SepLane L;
               sep_setup(sep_flavor(mode), R, Y, mT, mT * mT, m2, mT * baryon, pT, sign, baryon, kExp2Tab, L,
                         use_tb && tail);
+              if (g_census) g_census[i * 3 + (L.skip ? 0 : (L.tail ? 1 : 2))]++;
               if (L.skip) continue;
               if (use_tb && L.fast) {   // k_spectra's F_TB fours (normal or Boltzmann-tail lanes)
                 const dbl2* PT = &PTq[(size_t)(kk * nl + l) * nphi];
