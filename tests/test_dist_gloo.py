@@ -1,4 +1,4 @@
-"""N > 1 decomposition on CPU: world_size-2 gloo processes shard the cells, integrate their
+"""N > 1 decomposition on CPU: world_size-2 and -4 gloo processes shard the cells, integrate their
 shard (oracle as the per-rank worker; on the GPU the engine does this) and all-reduce the
 spectra -- the result equals the single-process integral over the whole surface."""
 import os
@@ -33,14 +33,16 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_two_rank_gloo_shard_and_allreduce():
+@pytest.mark.parametrize("world", [2, 4])
+def test_gloo_shard_and_allreduce(world):
     import torch.multiprocessing as mp
     from is3d2_amd import make_spec, synth
     from oracle import oracle as O
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = 29500 + os.getpid() % 1000
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    port += 7 * world
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
     avg, got = q.get(timeout=300)

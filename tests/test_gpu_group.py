@@ -28,7 +28,7 @@ def spectra(spec, surf, devices=None, T_avg=None):
 
 
 @pytest.mark.parametrize("mode,dim", [(1, 3), (2, 2), (3, 3), (4, 2)])
-@pytest.mark.parametrize("ndev", [2, 3])
+@pytest.mark.parametrize("ndev", [2, 3, 8])
 def test_group_equals_single_engine(mode, dim, ndev):
     s = synth.as_read(synth.surface(300, seed=71, dimension=dim, full3d=(dim == 3)))
     spec = make_spec(hrg_eos=2, chosen="pikp", df_mode=mode, dimension=dim)
