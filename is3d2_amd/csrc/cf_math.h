@@ -1152,6 +1152,12 @@ IS3D_HD double rcp1(double d) {
 // 1 - sign f_eq = 1 exactly, and the lane keeps the delta-f coefficients unscaled (sa = 1) and 1/a
 // folded into the p.dsigma coefficients D0, Dc, Ds, escw: a point is (w p.dsigma f_eq)(1 + delta-f)
 // with no reciprocal (Grad: 5 VALU ops instead of 12).
+// sep_setup's skip test alone (the same two operations): callers test it first, so a wavefront whose lanes all
+// skip the cell branches past the lane setup (~65 instructions) instead of computing it
+IS3D_HD bool sep_skips(const double* R, const double* Y, double mT, double pT, double baryon) {
+  return fma(mT, Y[Y_AT], -baryon * R[R_CHEM]) - pT * R[R_ZB] > kExpMax;
+}
+
 IS3D_HD void sep_setup(int flavor, const double* R, const double* Y, double mT, double mT2, double m2, double mTb,
                        double pT, double sign, double baryon, const double* etab, SepLane& L, int allow_tail = 0) {
   L.sign = sign;
@@ -1635,6 +1641,17 @@ static constexpr double kModTabX = 1.0e6, kModTabChem = 30.0;
 #ifndef IS3D_MOD_SQ_BOUNDS
 #define IS3D_MOD_SQ_BOUNDS 1
 #endif
+
+// mod_setup's skip test alone (same operations, IS3D_MOD_SQ_BOUNDS form), for an early branch past the setup
+IS3D_HD bool mod_skips(const double* R, const double* Y, double mT, double m2, double pT, double baryon, bool ymu = true) {
+  const double ux = Y[Y_MUX], uy = Y[Y_MUY], uz = Y[Y_MUZ];
+  const double u2 = ymu ? Y[Y_MU2] : fma(ux, ux, fma(uy, uy, uz * uz));
+  const double sig = R[R_INVTM] * kInvLn2xN, m2s = m2 * (sig * sig);
+  const double mu = mT * (ymu ? Y[Y_MU] : sqrt(u2));
+  const double lo = mu - pT * R[R_VB];
+  const double thr = (kExpMax + 1.0 + baryon * R[R_CHEMM]) * kInvLn2xN;
+  return thr < 0.0 || (lo > 0.0 && (m2s + lo * lo) * (1.0 - 2e-12) > thr * thr);
+}
 
 IS3D_HD void mod_setup(const double* R, const double* Y, double mT, double m2, double pT, double sign, double baryon,
                        double renorm_abs, const double* etab, ModLane& L, bool ymu = true) {

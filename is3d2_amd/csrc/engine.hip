@@ -1004,6 +1004,14 @@ static SpectraPlan spectra_plan(const is3d_engine* e) {
 #endif
   P.ly = 0;
   P.shmem = lds_bytes(P.nqmax);
+  // RTA-CE's table launch adds {TE, T2} to the {PD, T1} rows: where that costs the third workgroup per CU
+  // (LDS above 160 KB / 3 -- SMASH as 193 integrand classes spans 3 q rows per workgroup: 54.5 KB) the
+  // per-lane launch is faster (config 2 RTA-CE 349.7 -> 324.3 ms, profiles/round3_r3h_ab_ce_tb.log; with
+  // 444 species, 2 rows, 47.8 KB, the table launch had won 723 -> 676 ms in round 1)
+  if (P.tb && mode == CE && 3 * P.shmem > 160 * 1024) {
+    P.tb = 0;
+    P.shmem = lds_bytes(P.nqmax);
+  }
   // the modified path's 16-cell tiles fall back to 8 (F_T8) before giving up the q-row tables
   if (P.shmem > IS3D_LDS_QROW_LIMIT && mode >= PTM && kTile != is3d::kern::kTile) {
     kTile = is3d::kern::kTile;

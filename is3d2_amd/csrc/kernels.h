@@ -142,6 +142,12 @@ constexpr int kTbQ = 4;
 #ifndef IS3D_PIPE
 #define IS3D_PIPE 1           // k_spectra: tables of tile i + 1 built between the lane work of tile i (2 barriers per tile)
 #endif
+#ifndef IS3D_EARLY_SKIP
+// k_spectra tests a lane's overflow skip before its setup, so a wavefront whose lanes all skip a cell branches
+// past the setup: bit 1 separable lanes (sep_skips; config 2 Grad 222.0 -> 215.4 ms, RTA-CE 320.4 -> 317.5 ms),
+// bit 2 modified lanes (mod_skips; PTM 465.1 -> 471.8 ms, PTMA unchanged: off), profiles/round3_r3i_ab_skip.log
+#define IS3D_EARLY_SKIP 1
+#endif
 #ifndef IS3D_PAIR_RCP
 #define IS3D_PAIR_RCP 1       // fast path: two phi points per reciprocal (sep_pair_t)
 #endif
@@ -744,6 +750,7 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
         if (MODMAIN && sep) continue;
         if (FB && !sep) continue;
         if constexpr (!MODMAIN) {     // Grad / RTA-CE lanes (sep throughout), the F_FB launch's separable lanes
+          if ((IS3D_EARLY_SKIP & 1) && sep_skips(R, Y, mT, pT, baryon)) continue;
           SepLane L;
           sep_setup(sep_flavor(MODE), R, Y, mT, mT2, m2, mTb, pT, sign, baryon, s_etab, L,
                     TB && IS3D_TAIL && (MODE == GRAD || IS3D_TAIL_CE));
@@ -768,6 +775,7 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
           else sep_phi_loop<MODE, FLAGS, false, KJ>(L, s_cs + j0, BP, acc);
         }
         if constexpr (MODMAIN) {
+          if ((IS3D_EARLY_SKIP & 2) && IS3D_MOD_SQ_BOUNDS && mod_skips(R, Y, mT, m2, pT, baryon, !LY)) continue;
           ModLane M;
           mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, s_etab, M, !LY);
           if (M.skip) continue;
