@@ -22,7 +22,7 @@
 #define IS3D_ANISO_MERGE 1    // PTMA Newton sums over hadrons merged by identical (mass, sign)
 #endif
 #ifndef IS3D_MAX_SPLITS
-#define IS3D_MAX_SPLITS 64    // cap on k_spectra's cell splits (one output-sized slab each)
+#define IS3D_MAX_SPLITS 256   // cap on k_spectra's cell splits (one output-sized slab each; config 4: 256 x 50 MB)
 #endif
 #include <hip/hip_runtime.h>
 
@@ -1446,7 +1446,7 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   }
   const long wgs = bx * npT;
   // cell splits: enough workgroups to fill the chip (>= 8k), and each split's records small enough
-  // (~2 MB) to stay in one XCD's 4 MB L2 while that XCD's workgroups stream them; a multiple of 8
+  // (~0.5 MB, with the PTM renormalisation rows 2 MB) to stay in one XCD's 4 MB L2 while that XCD's workgroups stream them; a multiple of 8
   // so every XCD owns whole splits; at most IS3D_MAX_SPLITS slabs (each one output-sized)
   const long kTile = P.tile;                              // cells per tile of this mode's k_spectra
   const long max_split = std::max(1L, (nw + kTile - 1) / kTile);

@@ -99,7 +99,9 @@ constexpr int F_REG = 1, F_OUT = 2, F_TB = 4, F_LY = 8, F_T8 = 16, F_FB = 32;
 constexpr int kTbQ = 4;
 
 #ifndef IS3D_SPLIT_BYTES
-#define IS3D_SPLIT_BYTES (2L << 20)   // record bytes per cell split (k_spectra grid sizing)
+#define IS3D_SPLIT_BYTES (512L << 10) // record bytes per cell split (k_spectra grid sizing): 0.5 MB (2 MB before round 3:
+                                      // config2 PTM 467 -> 461 ms, PTB 437 -> 431, config4 3194 -> 3180 ms, Grad unchanged;
+                                      // profiles/round3_r3j_ab_split.log)
 #endif
 #ifndef IS3D_NOPF_MODES
 #define IS3D_NOPF_MODES 0     // bit m: mode m's fours skip the one-quad-ahead prefetch (register-starved builds)
