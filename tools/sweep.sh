@@ -12,3 +12,5 @@ for m in 2 3 4 5; do run --steps 3 --warmup 1 --config config2 --df-mode $m; don
 for m in 1 2 3 4 5; do run --steps 2 --warmup 1 --config config3 --df-mode $m --no-per-species; done
 for m in 1 3; do run --steps 2 --warmup 1 --config config2 --operation 0 --df-mode $m --no-per-species; done
 run --steps 1 --warmup 1 --config config5 --cells $C5 --no-per-species
+# config 1's shape (pikp 2+1D, 24 pT x 24 phi x 24 eta, 1e5 cells) in every mode
+for m in 1 2 3 4 5; do run --steps 3 --warmup 1 --config config1 --cells 100000 --df-mode $m --no-per-species; done
