@@ -21,6 +21,9 @@
 #ifndef IS3D_ANISO_MERGE
 #define IS3D_ANISO_MERGE 1    // PTMA Newton sums over hadrons merged by identical (mass, sign)
 #endif
+#ifndef IS3D_CHAIN_L
+#define IS3D_CHAIN_L 32       // PTMA warm-start chains: positions per segment (k_chain_pass), at least
+#endif
 #ifndef IS3D_MAX_SPLITS
 #define IS3D_MAX_SPLITS 256   // cap on k_spectra's cell splits (one output-sized slab each; config 4: 256 x 50 MB)
 #endif
@@ -1394,7 +1397,7 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
       ChainArgs ca{};
       ca.rec = e->d_rec; ca.ain = e->d_aux; ca.sol = e->d_sol; ca.n = n; ca.C = aa.chains; ca.h = aa.h; ca.fp2 = aa.fp2;
       const long P = (n + ca.C - 1) / ca.C;
-      ca.L = std::max(32L, (n + 16383) / 16384);
+      ca.L = std::max((long)IS3D_CHAIN_L, (n + 16383) / 16384);
       ca.nspc = (P + ca.L - 1) / ca.L;
       const long nseg = ca.C * ca.nspc;
       const long need = 4 * n + (n + 1) / 2 + 12 * nseg + kChainPasses;
