@@ -21,6 +21,9 @@
 #ifndef IS3D_ANISO_MERGE
 #define IS3D_ANISO_MERGE 1    // PTMA Newton sums over hadrons merged by identical (mass, sign)
 #endif
+#ifndef IS3D_MP
+#define IS3D_MP 1             // k_spectra's F_MP launch (several pT per workgroup) for few lane tasks per pT
+#endif
 #ifndef IS3D_CHAIN_L
 #define IS3D_CHAIN_L 32       // PTMA warm-start chains: positions per segment (k_chain_pass), at least
 #endif
@@ -964,13 +967,16 @@ static int device_jonah_table(is3d_engine* e, const double* r2, const double* w2
 // pT sin} table finalize_tables builds for KJ-padded phi rows)
 struct SpectraPlan {
   int KJ, njb, nq, nqmax, tb, ly, t8, tile;
+  int mp, npw;                // F_MP: pT values per workgroup (1 otherwise)
   size_t shmem;
   size_t shmem_fb;            // modified modes: the F_FB launch (8-cell tiles, per-lane y-term rows, no q tables)
 };
 static SpectraPlan spectra_plan(const is3d_engine* e) {
   SpectraPlan P{};
+  P.npw = 1;
   const int mode = e->p.df_mode, dim = e->p.dimension;
   const int np = e->ncls, nphi = (int)e->phi.size();     // lane species: the integrand classes
+  const int npT = (int)e->pT.size();
   const int nk = (dim == 3) ? (int)e->y.size() : 1, nl = (dim == 3) ? 1 : (int)e->eta.size();
   P.nq = nk * nl;
   auto shape = [&](int KJ) {
@@ -993,7 +999,8 @@ static SpectraPlan spectra_plan(const is3d_engine* e) {
     // pipelined launches (F_TB, the modified path's 16-cell tiles): 3 record tiles, 2 table buffers
     const bool pipe = IS3D_PIPE && (P.tb || (mode >= PTM && qrows && !P.t8 && !P.ly));
     const size_t rb = pipe ? 3 : 2, tb = pipe ? 2 : 1, qvf = (mode >= PTM || !pipe) ? 2 : 1;
-    return sizeof(double) * (rb * tile * NREC + 4 * nphp + tb * 2 * tile * nphp + tb * qvf * tile * nphp +
+    const size_t w = (size_t)P.npw;     // F_MP: pT blocks of {pc, ps} and of the per-(cell, phi) tables
+    return sizeof(double) * (rb * tile * NREC + (2 + 2 * w) * nphp + tb * 2 * w * tile * nphp + tb * qvf * w * tile * nphp +
                              (size_t)(nk + 2 * nl) +
                              (qrows ? tb * tile * std::min(qrows, P.nq) * kYRow : (size_t)kBlock * kYRowLY) + kExpTabN +
                              (P.tb ? 2 * tile * qrows * (P.KJ + 1) + 1 : 0) +
@@ -1033,6 +1040,31 @@ static SpectraPlan spectra_plan(const is3d_engine* e) {
     P.ly = F_LY;
     kTile = is3d::kern::kTile;     // spectra_tile<MODE, F_LY | ...>
     P.shmem = lds_bytes(0);
+  }
+  // F_MP (Grad / RTA-CE, no table launch): when one pT's tasks with a single phi block of KJ >= nphi fill at
+  // most half a workgroup (pikp 2+1D: 3 x 24 = 72), a workgroup takes npw = 256 / tasks pT values and every
+  // lane a whole phi row -- the lane setup (~4.5 points' work) is paid once per row instead of once per
+  // 8-point block; chosen by the same cost model as spectra_kj_fill (lane slots x (KJ + 4.5))
+  if (IS3D_MP && mode <= CE && !P.tb && !P.ly && nphi <= 32) {
+    const long tpp = (long)np * P.nq;
+    const int kjm = nphi <= 24 ? 24 : 32;
+    if (tpp * 2 <= kBlock) {
+      const long slots = (tpp * P.njb + kBlock - 1) / kBlock * kBlock;
+      const double cost_now = (double)slots * (P.KJ + 4.5);
+      const int npw = (int)std::min<long>(kBlock / tpp, npT);
+      const double cost_mp = (double)kBlock / npw * (kjm + 4.5);
+      if (cost_mp < cost_now) {
+        SpectraPlan Q = P;
+        shape(kjm);
+        P.tb = 0;
+        P.nqmax = P.nq;
+        P.mp = F_MP;
+        P.npw = npw;
+        const size_t sm = lds_bytes(P.nqmax);
+        if (sm <= IS3D_LDS_QROW_LIMIT) P.shmem = sm;
+        else P = Q;
+      }
+    }
   }
   P.tile = kTile;
   if (mode >= PTM) {
@@ -1437,7 +1469,7 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   if (P.shmem > 160 * 1024) return e->fail(IS3D_ERR_ARG, "momentum grid too large for the LDS tile (phi table)");
   const int nc = e->ncls;      // lane species: one per integrand class (the reduction writes the members)
   const long ntask = (long)nc * nk * nl * njb;
-  const long bx = (ntask + kBlock - 1) / kBlock;
+  const long bx = (ntask + kBlock - 1) / kBlock;            // lane groups per pT (F_MP: 1, ntask <= 128)
   if (!P.ly) {
     // k_spectra's LDS row tables hold nqmax rows per cell; a lane group spanning more would compute nothing
     // (its slab is NaN-filled, rows_ok), so refuse the launch here instead of returning NaN spectra
@@ -1447,7 +1479,9 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
         return e->fail(IS3D_ERR_ARG, "internal: k_spectra lane group spans more q rows than the LDS plan");
     }
   }
-  const long wgs = bx * npT;
+  // workgroups per cell split: lane groups x pT values, or F_MP's pT groups of npw
+  const long npg = P.mp ? (npT + P.npw - 1) / P.npw : npT;
+  const long wgs = bx * npg;
   // cell splits: enough workgroups to fill the chip (>= 8k), and each split's records small enough
   // (~0.5 MB, with the PTM renormalisation rows 2 MB) to stay in one XCD's 4 MB L2 while that XCD's workgroups stream them; a multiple of 8
   // so every XCD owns whole splits; at most IS3D_MAX_SPLITS slabs (each one output-sized)
@@ -1479,10 +1513,11 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   sa.npart = nc; sa.npT = npT; sa.nphi = nphi; sa.ny_out = ny_out; sa.nk = nk; sa.nl = nl; sa.nq = nk * nl; sa.njb = njb;
   sa.nqmax = P.nqmax;
   sa.ntask = ntask; sa.cells_per_split = cps; sa.nbx = (int)bx; sa.nsplit = (int)nsplit; sa.sstride = sstride;
+  sa.npw = P.npw;
   sa.regulate = e->p.regulate_deltaf; sa.outflow = e->p.outflow; sa.dim = dim; sa.op = 1;
   const size_t shmem = P.shmem;
-  const int tb = P.tb | P.ly | P.t8;
-  const dim3 grid((unsigned)(bx * npT * nsplit));
+  const int tb = P.tb | P.ly | P.t8 | P.mp;
+  const dim3 grid((unsigned)(wgs * nsplit));
   const int kflags = (e->p.regulate_deltaf ? F_REG : 0) | (e->p.outflow ? F_OUT : 0) | tb;
   switch (mode) {
     case GRAD: launch_spectra<GRAD>(grid, shmem, st, sa, kflags, KJ); break;

@@ -78,6 +78,7 @@ struct SpecArgs {
   long ntask;                 // npart * nq * njb lanes per pT: (species, q = y x eta node, phi block)
   long cells_per_split;
   int nbx, nsplit;            // lane groups per pT, cell splits (1-D grid of nbx * npT * nsplit)
+  int npw;                    // F_MP: pT values per workgroup (1-D grid of ceil(npT / npw) * nsplit)
   long sstride;               // doubles per slab: npT * nbx * KJ * kBlock
   int regulate, outflow, dim;
   int op;                     // 1 spectra / 0 spacetime (yterms variants)
@@ -95,7 +96,11 @@ struct SpecArgs {
 // cells, narrow rapidity windows), over the cells listed by k_fbscan, per-lane y-term rows as F_LY.  Keeping
 // the separable code out of the modified launch takes its k_spectra from 241 to 164 VGPRs (3 waves per SIMD
 // instead of 2) and removes the 32-64 v_mov_b64 per lane and cell that merged two register assignments of acc
-constexpr int F_REG = 1, F_OUT = 2, F_TB = 4, F_LY = 8, F_T8 = 16, F_FB = 32;
+// F_MP (Grad / RTA-CE with few lane tasks per pT: np x nq <= 128, e.g. pikp 2+1D = 72): a lane owns a whole
+// phi row (one block of KJ >= nphi) and a workgroup holds npw = 256 / (np nq) pT values, whose {b', Phi} /
+// PD / {pc, ps} tables it builds side by side; the lane setup is amortised over every phi point instead of
+// an 8-point block
+constexpr int F_REG = 1, F_OUT = 2, F_TB = 4, F_LY = 8, F_T8 = 16, F_FB = 32, F_MP = 64;
 constexpr int kTbQ = 4;
 
 #ifndef IS3D_SPLIT_BYTES
@@ -488,6 +493,8 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
   constexpr bool FB = MODE >= PTM && (FLAGS & F_FB) != 0;   // separable-fallback launch of a modified mode
   constexpr bool MODMAIN = MODE >= PTM && !FB;              // modified launch: separable lanes left to F_FB
   constexpr bool LY = (FLAGS & F_LY) != 0 || FB;
+  constexpr bool MP = (FLAGS & F_MP) != 0;                  // several pT per workgroup, one phi block per lane
+  const int npw = MP ? A.npw : 1;                           // pT values of this launch's workgroups
   // per-(cell, q, phi) tables built from the per-tile tables (phase C below): Grad / RTA-CE {PD, T1},
   // modified path T2
   constexpr bool HAS_C = TB || (MODE >= PTM && !LY);
@@ -499,7 +506,7 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
   constexpr int kRecBufs = PIPE ? 3 : 2, kTabBufs = PIPE ? 2 : 1;
   constexpr int kQvF = (MODE >= PTM || !PIPE) ? 2 : 1;    // doubles per (cell, phi) of s_qv
   const int nqm = A.nqmax;                                // rows per cell (>= every workgroup's nqw)
-  const long recsz = (long)kTile * NREC, bpsz = (long)kTile * nphp, qvsz = kQvF * bpsz;
+  const long recsz = (long)kTile * NREC, bpsz = (long)npw * kTile * nphp, qvsz = kQvF * bpsz;
   // y-term rows per cell: per row, or per q once the rows cover every q (nyr below): min(nqm, nq);
   // LY launches: one y-term row per lane instead ([kBlock][kYRowLY], single; odd row stride: no conflicts)
   const long ysz = LY ? (long)kBlock * kYRowLY : (long)kTile * min(nqm, A.nq) * kYRow;
@@ -508,8 +515,8 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
   double* s_etab = smem;                                  // [kExpTabN] 2^(j/kExpTabN)
   double* s_recb = smem + kExpTabN;                       // [kRecBufs][kTile][NREC]
   dbl2* s_trig = (dbl2*)(s_recb + kRecBufs * recsz);      // [nphp]        {cos, sin}
-  dbl2* s_cs = s_trig + nphp;                             // [nphp]        {pT cos, pT sin}
-  dbl2* s_bp = s_cs + nphp;                               // [kTabBufs][kTile][nphp] {b', Phi}
+  dbl2* s_cs = s_trig + nphp;                             // [npw][nphp]   {pT cos, pT sin}
+  dbl2* s_bp = s_cs + npw * nphp;                         // [kTabBufs][npw][kTile][nphp] {b', Phi}
   // Grad / RTA-CE: [kTabBufs][kTile][nphp] PD table; modified path: {PDm, Qv} pairs (s_mw)
   double* s_qv = (double*)(s_bp + kTabBufs * bpsz);
   double* s_grid = s_qv + kTabBufs * qvsz;                // y[nk] | eta[nl] | eta_w[nl]
@@ -529,15 +536,20 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
   // XCD-aware block order (cdna_hip_programming.md T1): blocks that share an XCD (same
   // blockIdx % 8) take one contiguous range of logical ids, and logical ids run split-major, so
   // each XCD's L2 sees only its own cell splits (sized to fit) instead of every split
-  const long nwg = (long)A.nbx * A.npT * A.nsplit;
+  // F_MP: the workgroup's pT group pg holds pT values pg npw .. pg npw + npw - 1; lane tid is task tid % ntask
+  // of pT lp = tid / ntask
+  const long npg = MP ? (A.npT + npw - 1) / npw : A.npT;
+  const long nwg = (long)A.nbx * npg * A.nsplit;
   const long bid = blockIdx.x, q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
   const long lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
   const int lane_group = (int)(lid % A.nbx);
-  const int ipt = (int)((lid / A.nbx) % A.npT);
-  const int split = (int)(lid / ((long)A.nbx * A.npT));
+  const int pg = (int)((lid / A.nbx) % npg);
+  const int split = (int)(lid / ((long)A.nbx * npg));
+  const int lp = MP ? tid / (int)A.ntask : 0;
+  const int ipt = MP ? min(pg * npw + lp, A.npT - 1) : pg;
   const double pT = A.pT[ipt];
-  const long task = (long)lane_group * kBlock + tid;
-  const bool active = task < A.ntask;
+  const long task = MP ? (long)(tid % (int)A.ntask) : (long)lane_group * kBlock + tid;
+  const bool active = MP ? (lp < npw && pg * npw + lp < A.npT) : task < A.ntask;
   int s = 0, q = 0, jb = 0;
   if (active) {
     s = (int)(task % A.npart);
@@ -571,13 +583,15 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
 
   // per-workgroup constants into LDS: inside the cell loop the only global loads are the
   // record prefetch (and PTM's renormalisation factor)
-  for (int j = tid; j < nphp; j += kBlock) {
+  for (int i = tid; i < npw * nphp; i += kBlock) {
+    const int j = i % nphp;
     const bool in = j < A.nphi;
     const double c = in ? A.cphi[j] : 0.0, sn = in ? A.sphi[j] : 0.0;
     dbl2 v; v.x = c; v.y = sn;
-    s_trig[j] = v;
-    v.x = pT * c; v.y = pT * sn;
-    s_cs[j] = v;
+    if (i < nphp) s_trig[j] = v;
+    const double pTi = MP ? A.pT[min(pg * npw + i / nphp, A.npT - 1)] : pT;
+    v.x = pTi * c; v.y = pTi * sn;
+    s_cs[i] = v;
   }
   for (int i = tid; i < A.nk; i += kBlock) s_grid[i] = (A.dim == 3) ? A.yv[i] : 0.0;
   for (int i = tid; i < A.nl; i += kBlock) {
@@ -600,8 +614,10 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
     c_end = min(A.n, c_begin + A.cells_per_split);
   }
   const int* const fbl = FB ? A.fbcells : nullptr;
-  // this thread's slab entries, layout [split][pT][lane group][phi slot][lane] (see the stores at the end)
-  double* const out = A.slab + (long)split * A.sstride + ((long)ipt * A.nbx + lane_group) * (KJ * kBlock) + tid;
+  // this thread's slab entries, layout [split][pT][lane group][phi slot][lane] (see the stores at the end); F_MP:
+  // lane group 0 of the lane's own pT, slot = its task
+  double* const out = A.slab + (long)split * A.sstride + ((long)ipt * A.nbx + lane_group) * (KJ * kBlock) +
+                      (MP ? task : (long)tid);
 
   // ---- phase A / B of one tile (records s_rec, ntx cells) into table buffer tb: {b', Phi} and PD (or
   // the modified path's {PDm, Qv}) per (cell, phi), {TE, T2} for RTA-CE's table launch, y-terms per
@@ -612,22 +628,27 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
     dbl2* mw = (dbl2*)qvt;
     dbl2* pe = s_pe + tb * bpsz;
     double* yb = s_y + tb * ysz;
-    for (int idx = tid; idx < ntx * nphp; idx += kBlock) {
-      const int t = idx / nphp, j = idx % nphp;
+    // F_MP: npw pT blocks of [kTile][nphp]; o = the entry's offset in its block, csj = its {pc, ps}
+    for (int idx = tid; idx < npw * ntx * nphp; idx += kBlock) {
+      const int l2 = MP ? idx / (ntx * nphp) : 0, ix = MP ? idx % (ntx * nphp) : idx;
+      const int t = ix / nphp, j = ix % nphp;
+      const int o = (l2 * kTile + t) * nphp + j;
+      const dbl2 csj = s_cs[l2 * nphp + j];
+      const double pTl = MP ? A.pT[min(pg * npw + l2, A.npT - 1)] : pT;
       const double* R = s_rec + t * NREC;
       dbl2 v; v.x = 0.0; v.y = 0.0;                        // padding: finite, never written out
       double qv = 0.0;
       if (j < A.nphi && R[R_KIND] != 0.0) {
         const dbl2 tr = s_trig[j];
-        v = phiterms(MODE, R, pT, tr.x, tr.y, s_etab);
-        if (MODE >= PTM && R[R_KIND] == 2.0) qv = modqv(R, s_cs[j]);
+        v = phiterms(MODE, R, pTl, tr.x, tr.y, s_etab);
+        if (MODE >= PTM && R[R_KIND] == 2.0) qv = modqv(R, csj);
       }
-      bp[t * nphp + j] = v;
+      bp[o] = v;
       if constexpr (MODE >= PTM) {
-        dbl2 m; m.x = modpdm(R, s_cs[j]); m.y = qv;        // zero rows / padding give 0
-        mw[t * nphp + j] = m;
+        dbl2 m; m.x = modpdm(R, csj); m.y = qv;           // zero rows / padding give 0
+        mw[o] = m;
       } else {
-        qvt[t * nphp + j] = sep_pd(R, s_cs[j], v.x);      // PD table (sep_pd)
+        qvt[o] = sep_pd(R, csj, v.x);                     // PD table (sep_pd)
       }
       if constexpr (TB && MODE == CE) {
         const dbl2 c = s_cs[j];
@@ -738,7 +759,10 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
           if (!isfinite(rn)) continue;    // species skipped (MomentumSpectra.cpp:828-832)
           rn_abs = fabs(rn);
         }
-        const dbl2* BP = bpt + t * nphp + j0;
+        // this lane's (pT block, cell) row of the per-(cell, phi) tables (F_MP: block lp, else 0) and {pc, ps}
+        const long tro = ((long)lp * kTile + t) * nphp + j0;
+        const dbl2* BP = bpt + tro;
+        const dbl2* CSl = s_cs + lp * nphp + j0;
         const double* Y = yb + ((long)t * nyr + yrow) * kYRow;
         if constexpr (LY) {        // this lane's own y-terms, in its LDS row
           double* Yl = s_y + (long)tid * kYRowLY;
@@ -766,15 +790,15 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
                 sep_phi_loop_tb_tail<MODE, FLAGS, KJ>(L, mT, BP, PT, pet + t * nphp + j0, acc);
             }
             else if (L.fast) sep_phi_loop_tb<MODE, FLAGS, KJ>(L, mT, BP, PT, pet + t * nphp + j0, acc);
-            else sep_phi_loop<MODE, FLAGS, false, KJ>(L, s_cs + j0, BP, acc);
-          } else if (IS3D_PD_TABLE && IS3D_CS_SCALAR && MODE <= CE && KJ % 4 == 0 && L.fast && A.njb == 1)
+            else sep_phi_loop<MODE, FLAGS, false, KJ>(L, CSl, BP, acc);
+          } else if (IS3D_PD_TABLE && IS3D_CS_SCALAR && !MP && MODE <= CE && KJ % 4 == 0 && L.fast && A.njb == 1)
             // one phi block: every lane reads the same {pc, ps}, so they come by scalar loads into SGPRs
-            // (VALU operands) instead of LDS
+            // (VALU operands) instead of LDS (not F_MP: a wavefront can straddle two pT blocks)
             sep_phi_loop_pd<MODE, FLAGS, KJ, true>(L, (cs_sptr)A.csg + 2L * ipt * nphp, BP, qvt + t * nphp, acc);
           else if (IS3D_PD_TABLE && MODE <= CE && KJ % 4 == 0 && L.fast)
-            sep_phi_loop_pd<MODE, FLAGS, KJ, true>(L, s_cs + j0, BP, qvt + t * nphp + j0, acc);
-          else if (L.fast) sep_phi_loop<MODE, FLAGS, true, KJ>(L, s_cs + j0, BP, acc);
-          else sep_phi_loop<MODE, FLAGS, false, KJ>(L, s_cs + j0, BP, acc);
+            sep_phi_loop_pd<MODE, FLAGS, KJ, true>(L, CSl, BP, qvt + tro, acc);
+          else if (L.fast) sep_phi_loop<MODE, FLAGS, true, KJ>(L, CSl, BP, acc);
+          else sep_phi_loop<MODE, FLAGS, false, KJ>(L, CSl, BP, acc);
         }
         if constexpr (MODMAIN) {
           if ((IS3D_EARLY_SKIP & 2) && IS3D_MOD_SQ_BOUNDS && mod_skips(R, Y, mT, m2, pT, baryon, !LY)) continue;
@@ -783,8 +807,8 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
           if (M.skip) continue;
           const dbl2* MW = mwt + t * nphp + j0;
           if constexpr (LY) {        // no T2 rows: the lane's linear forms (mod_pair_lane_t)
-            if (M.clamp) mod_phi_loop_lane<FLAGS, true, KJ>(M, s_cs + j0, MW, acc);
-            else mod_phi_loop_lane<FLAGS, false, KJ>(M, s_cs + j0, MW, acc);
+            if (M.clamp) mod_phi_loop_lane<FLAGS, true, KJ>(M, CSl, MW, acc);
+            else mod_phi_loop_lane<FLAGS, false, KJ>(M, CSl, MW, acc);
             continue;
           }
           const double* MT = s_mt + ((long)t * nqw + row) * prow;
@@ -797,6 +821,7 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
   // partial sums, slab layout [split][pT][lane group][phi slot][lane]: every store of the wave is
   // one contiguous 512-byte row; non-temporal so the stream does not evict the cell records the
   // XCD's other workgroups are still reading from L2.  k_reduce scatters into the reference layout.
+  if (MP && !active) return;    // lanes past the workgroup's pT blocks own no slab entries
 #pragma unroll
   for (int jj = 0; jj < KJ; jj++) __builtin_nontemporal_store(rows_ok ? acc[jj] : __builtin_nan(""), out + jj * kBlock);
 }
@@ -1031,6 +1056,17 @@ void launch_spectra_kj(dim3 grid, size_t shmem, hipStream_t st, const SpecArgs& 
         case 1: hipLaunchKernelGGL((k_spectra<MODE, 9, KJ>), grid, dim3(kBlock), shmem, st, a); break;
         case 2: hipLaunchKernelGGL((k_spectra<MODE, 10, KJ>), grid, dim3(kBlock), shmem, st, a); break;
         default: hipLaunchKernelGGL((k_spectra<MODE, 11, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+      }
+      return;
+    }
+  }
+  if constexpr ((MODE == GRAD || MODE == CE) && (KJ == 24 || KJ == 32)) {
+    if (flags & F_MP) {
+      switch (flags & 3) {
+        case 0: hipLaunchKernelGGL((k_spectra<MODE, 64, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+        case 1: hipLaunchKernelGGL((k_spectra<MODE, 65, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+        case 2: hipLaunchKernelGGL((k_spectra<MODE, 66, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+        default: hipLaunchKernelGGL((k_spectra<MODE, 67, KJ>), grid, dim3(kBlock), shmem, st, a); break;
       }
       return;
     }
