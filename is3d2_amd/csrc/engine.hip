@@ -24,6 +24,12 @@
 #ifndef IS3D_MP
 #define IS3D_MP 1             // k_spectra's F_MP launch (several pT per workgroup) for few lane tasks per pT
 #endif
+#ifndef IS3D_FILL_WGS
+#define IS3D_FILL_WGS 8192    // k_spectra workgroups the cell splits aim for (>= 8k fills the chip evenly)
+#endif
+#ifndef IS3D_FILL_WGS_MP
+#define IS3D_FILL_WGS_MP 2048 // the same for F_MP launches
+#endif
 #ifndef IS3D_CHAIN_L
 #define IS3D_CHAIN_L 32       // PTMA warm-start chains: positions per segment (k_chain_pass), at least
 #endif
@@ -1487,7 +1493,10 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   // so every XCD owns whole splits; at most IS3D_MAX_SPLITS slabs (each one output-sized)
   const long kTile = P.tile;                              // cells per tile of this mode's k_spectra
   const long max_split = std::max(1L, (nw + kTile - 1) / kTile);
-  const long by_fill = (8192 + wgs - 1) / wgs;
+  // (F_MP launches aim for 2k: their 2+1D slabs hold every eta node, and k_reduce_wave's reads across 1k
+  // splits cost config 1's shape 0.5 ms of a 4.7 ms pass -- Grad 4.7 -> 4.2 ms, RTA-CE 5.4 -> 5.0 ms with 2k,
+  // while the F_LY launch of the modified modes lost 14% with it: profiles/round3_r3p_ab_fill.log)
+  const long by_fill = ((P.mp ? IS3D_FILL_WGS_MP : IS3D_FILL_WGS) + wgs - 1) / wgs;
   const long by_l2 = ((long)NREC * 8 * nw + IS3D_SPLIT_BYTES - 1) / IS3D_SPLIT_BYTES;
   long nsplit = std::max(by_fill, std::min(by_l2, (long)IS3D_MAX_SPLITS));
   if (nsplit >= 8) nsplit = (nsplit + 7) / 8 * 8;
