@@ -1147,7 +1147,8 @@ IS3D_HD double rcp1(double d) {
 //   PTB   as CE, delta-f = (1 - sign feq) S + dz - 3 dlambda
 // mT2 = mT * mT and mTb = mT * b are per-lane constants hoisted by the caller.
 //
-// allow_tail (callers with a tail loop, sep_quad_tb_tail_t): lanes whose smallest exponent xs = x - zb
+// allow_tail (callers with a tail loop, sep_quad_tb_tail_t; 2 = decided per wavefront on the device): lanes
+// whose smallest exponent xs = x - zb
 // exceeds kTailX get tail = 1; their den = a + ssc b' equals a for every phi (kTailX), so f_eq = b'/a and
 // 1 - sign f_eq = 1 exactly, and the lane keeps the delta-f coefficients unscaled (sa = 1) and 1/a
 // folded into the p.dsigma coefficients D0, Dc, Ds, escw: a point is (w p.dsigma f_eq)(1 + delta-f)
@@ -1173,6 +1174,17 @@ IS3D_HD void sep_setup(int flavor, const double* R, const double* Y, double mT, 
   const double xs = L.x - zb;
   L.fast = (xs >= -300.0) ? 1 : 0;
   L.tail = (allow_tail && xs > kTailX) ? 1 : 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+  // allow_tail == 2: one decision per wavefront (all its live lanes in the tail, or none), so a wavefront
+  // whose lanes straddle the tail bound runs the normal fours only instead of both phi loops back to back
+  // (the vote is passed through a VGPR: as a wave-uniform SGPR value it made the compiler restructure the
+  // lane loops and spill 97 VGPRs)
+  if (allow_tail == 2) {
+    int t = __all(L.tail);
+    asm volatile("" : "+v"(t));
+    L.tail = t;
+  }
+#endif
   const int k = (L.fast && xs > 150.0) ? (int)((xs - 150.0) * 1.4426950408889634) : 0;
   L.a = L.fast ? exp_tab(exp_tab_coef(), etab, xs * kInvLn2xN, k) : 0.0;
   const double esc = ldexp(1.0, -k);

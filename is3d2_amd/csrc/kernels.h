@@ -139,6 +139,9 @@ constexpr int kTbQ = 4;
 #ifndef IS3D_TAIL
 #define IS3D_TAIL 1           // Boltzmann-tail lanes skip the per-point reciprocal (kTailX): Grad F_TB 497 -> 481 ms (r2d)
 #endif
+#ifndef IS3D_TAIL_WAVE
+#define IS3D_TAIL_WAVE 1      // the tail decision per wavefront: a wave mixing tail and other lanes runs one loop
+#endif
 #ifndef IS3D_TAIL_PD
 #define IS3D_TAIL_PD 0        // Grad tail lanes: PD table + scalar {pc, ps} instead of {PD, T1}: 2.2% slower (r2d A/B)
 #endif
@@ -779,7 +782,7 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
           if ((IS3D_EARLY_SKIP & 1) && sep_skips(R, Y, mT, pT, baryon)) continue;
           SepLane L;
           sep_setup(sep_flavor(MODE), R, Y, mT, mT2, m2, mTb, pT, sign, baryon, s_etab, L,
-                    TB && IS3D_TAIL && (MODE == GRAD || IS3D_TAIL_CE));
+                    (TB && IS3D_TAIL && (MODE == GRAD || IS3D_TAIL_CE)) ? (IS3D_TAIL_WAVE ? 2 : 1) : 0);
           if (L.skip) continue;
           if constexpr (TB) {
             const dbl2* PT = s_pt + ((long)t * nqw + row) * prow;

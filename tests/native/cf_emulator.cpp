@@ -70,6 +70,9 @@ struct EmuTables {
 // and other lanes per (cell, species, q)
 static long* g_census = nullptr;
 extern "C" void emu_set_census(long* counts) { g_census = counts; }
+// optional per-lane record (tools/lane_census.py --waves): [pT][cell][species][q] = 1 + (skip 0 / tail 1 / other 2)
+static signed char* g_census_lane = nullptr;
+extern "C" void emu_set_census_lanes(signed char* buf) { g_census_lane = buf; }
 
 extern "C" int emu_spectra_v(const orc_params* p, const orc_setup* su, const orc_surface* S, int chains, int op,
                              double* out, long* stats, int variant) {
@@ -195,6 +198,8 @@ extern "C" int emu_spectra_v(const orc_params* p, const orc_setup* su, const orc
               sep_setup(sep_flavor(mode), R, Y, mT, mT * mT, m2, mT * baryon, pT, sign, baryon, kExp2Tab, L,
                         use_tb && tail);
               if (g_census) g_census[i * 3 + (L.skip ? 0 : (L.tail ? 1 : 2))]++;
+              if (g_census_lane)
+                g_census_lane[(((size_t)i * n + c) * np + s) * nq + kk * nl + l] = (signed char)(1 + (L.skip ? 0 : (L.tail ? 1 : 2)));
               if (L.skip) continue;
               if (use_tb && L.fast) {   // k_spectra's F_TB fours (normal or Boltzmann-tail lanes)
                 const dbl2* PT = &PTq[(size_t)(kk * nl + l) * nphi];

@@ -5,8 +5,9 @@ PTM, whose n_linear / n_mod renormalisation carries it (MomentumSpectra.cpp:800-
 multiplies the result (MomentumSpectra.cpp:365).  The engine therefore integrates one lane species per class
 (SMASH 444 -> 193, UrQMD 305 -> 124) and its reduction writes every member.  These tests check that the
 spectra, dN/dX and per-cell yields are bit-identical to the per-species integration (classes off) wherever
-both launches take the same plan (phi block, cell splits: the BASELINE sizes), and equal to rounding where
-the class count changes the plan; every oracle comparison elsewhere in the GPU tier runs with classes on (the default)."""
+both launches take the same plan (phi block, cell splits: the BASELINE sizes) and the same lane forms, and
+equal to rounding where the class count changes the plan or the wavefront-wide tail decision of the Grad
+F_TB launch; every oracle comparison elsewhere in the GPU tier runs with classes on (the default)."""
 import numpy as np
 import pytest
 
@@ -46,13 +47,19 @@ def test_classes_bit_identical_config3_grid(mode):
 
 def test_classes_grad_config2_full_size():
     """Config 2 at full size (10^5 cells, Grad without baryon: the headline's F_TB table launch): the class and
-    per-species launches pick the same phi block and cell splits here, so the spectra agree bit for bit."""
+    per-species launches pick the same phi block and cell splits here.  The F_TB launch decides the
+    Boltzmann-tail form once per wavefront (sep_setup allow_tail = 2) and the two launches group different
+    lanes into their wavefronts, so a lane may take the tail form in one and the normal fours in the other:
+    the same f_eq (1 + delta-f) to rounding (the tail form drops a sign e^-x < 2^-54 term), not bit for bit."""
     s = synth.as_read(synth.surface(100000, seed=7, dimension=3))
     spec = make_spec(hrg_eos=2, chosen="smash", df_mode=1, dimension=3, pT="pT48", phi="phi32", y="y21")
     on, n_on, _ = spectra(spec, s, True)
     off, _, _ = spectra(spec, s, False)
     assert n_on == 193
-    assert np.array_equal(on, off)
+    rel, _, _ = parity(on, off, floor=1e-290)
+    print("classes on vs off: max rel %.3g" % rel)
+    assert rel < 1e-9, rel
+    assert np.array_equal(np.isfinite(on), np.isfinite(off))
 
 
 def test_classes_small_surface_split_plan():
