@@ -1492,19 +1492,39 @@ IS3D_HD void sep_quad_tb_tail_t(const SepLane& L, double mT, const dbl2* b, cons
   }
 }
 
-// Boltzmann-tail Grad fours with the PD table (pd[i]) and {pc, ps} (c[i], SGPR operands when read by
-// scalar loads) instead of the {PD, T1} table: 6 VALU ops and 6 LDS-array cycles per point (b128 + b64)
-// where sep_quad_tb_tail_t needs 5 ops but 8 LDS cycles -- the tail loop is LDS-bound otherwise.
-// acc += pb (1 + S), S = S0 + Sc pc + Ss ps + Phi (unscaled coefficients, sep_setup allow_tail)
-template <bool REG, bool OUT>
+// Boltzmann-tail fours with the PD table (pd[i]) and {pc, ps} (c[i], SGPR operands when read by scalar loads)
+// instead of the F_TB tables (sep_setup allow_tail: 1/a folded into D0 / escw, delta-f coefficients unscaled):
+//   Grad    acc += pb (1 + S),           S = S0 + Sc pc + Ss ps + Phi                  6 ops per point
+//   RTA-CE  acc += pb (1 + L + S / E),   L = L0 + Lc pc + Ls ps, E = E0 + Ec pc + Es ps, one 1/E per four
+// (pb = w p.dsigma f_eq = fma(D0, b', escw PD); against the fast fours' ~12 (Grad) / ~20 (RTA-CE) ops).
+// The F_TB launch's Grad tail lanes in this form read 6 LDS-array cycles per point instead of 8 but were
+// 2.2% slower there (IS3D_TAIL_PD, r2d); the per-lane launches (baryon on, RTA-CE with many classes) use it.
+template <int FL, bool REG, bool OUT>
 IS3D_HD void sep_quad_pd_tail_t(const SepLane& L, const dbl2* c, const dbl2* b, const double* pd, double* acc) {
+  constexpr bool needE = FL == SEP_CE;
+  double rE[4] = {0.0, 0.0, 0.0, 0.0};
+  if (needE) {
+    double E[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) E[i] = lin(L.E0, L.Ec, L.Es, c[i]);
+    const double e01 = E[0] * E[1], e23 = E[2] * E[3];
+    const double r = rcp1(e01 * e23);
+    const double r01 = r * e23, r23 = r * e01;
+    rE[0] = r01 * E[1]; rE[1] = r01 * E[0]; rE[2] = r23 * E[3]; rE[3] = r23 * E[2];
+  }
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     double pb = fma(L.D0, b[i].x, L.escw * pd[i]);
     if (OUT) pb = (pb <= 0.0) ? 0.0 : pb;
     double t;
-    if (REG) t = 1.0 + fmax(-1.0, fmin(lin(L.S0, L.Sc, L.Ss, c[i]) + b[i].y, 1.0));
-    else t = lin(L.S0 + 1.0, L.Sc, L.Ss, c[i]) + b[i].y;
+    if (REG) {
+      const double S = lin(L.S0, L.Sc, L.Ss, c[i]) + b[i].y;
+      const double dfv = needE ? fma(S, rE[i], lin(L.L0, L.Lc, L.Ls, c[i])) : S;
+      t = 1.0 + fmax(-1.0, fmin(dfv, 1.0));
+    } else {   // 1 + S0 and 1 + L0 are lane constants (hoisted by the compiler)
+      t = needE ? fma(lin(L.S0, L.Sc, L.Ss, c[i]) + b[i].y, rE[i], lin(1.0 + L.L0, L.Lc, L.Ls, c[i]))
+                : lin(L.S0 + 1.0, L.Sc, L.Ss, c[i]) + b[i].y;
+    }
     acc[i] = fma(pb, t, acc[i]);
   }
 }
@@ -1609,6 +1629,13 @@ IS3D_HD double sqrt_nr(double v) {
 #define IS3D_MOD_PLUS 1
 #endif
 // degree of the modified lanes' 2^(r/N) polynomial: 3 (minimax, 3.5e-14 relative) or 4 (Taylor, ~1 ulp)
+// Boltzmann-tail lanes (IS3D_MOD_TAIL): where |s| < 2^-55 <= 2^-55 E at every point, E + s == E exactly, so
+// f = 2^-k / E = e^-(x - k ln2) 2^-k: the point evaluates that exponential directly (the shift constant
+// 1.5 2^52 + N k) and skips the denominators and the shared reciprocal (mod_quad_tab_tail_t).  Decided once
+// per wavefront (mod_setup allow_tail): a wave whose lanes straddle the bound runs the normal fours only
+#ifndef IS3D_MOD_TAIL
+#define IS3D_MOD_TAIL 0
+#endif
 #ifndef IS3D_MOD_EXP_DEG
 #define IS3D_MOD_EXP_DEG 3
 #endif
@@ -1630,6 +1657,7 @@ struct ModLane {
   ModExpCoef et;               // pinned once per lane setup, reused by every phi point
   const double* etab;          // 2^(j/kExpTabN) table (LDS on the device)
   int skip, clamp;   // clamp: some point's exp argument may leave the table lanes' domain (exp_clamped instead)
+  int tail;          // IS3D_MOD_TAIL: Boltzmann-tail table lane (shiftk = 1.5 2^52 + N k, mod_quad_tab_tail_t)
 };
 
 // Qv = |pc Vc + ps Vs|^2 for one (cell, phi), exp-table units (sig^2)
@@ -1666,7 +1694,7 @@ IS3D_HD bool mod_skips(const double* R, const double* Y, double mT, double m2, d
 }
 
 IS3D_HD void mod_setup(const double* R, const double* Y, double mT, double m2, double pT, double sign, double baryon,
-                       double renorm_abs, const double* etab, ModLane& L, bool ymu = true) {
+                       double renorm_abs, const double* etab, ModLane& L, bool ymu = true, bool allow_tail = false) {
   const double ux = Y[Y_MUX], uy = Y[Y_MUY], uz = Y[Y_MUZ];   // sig U
   const double u2 = ymu ? Y[Y_MU2] : fma(ux, ux, fma(uy, uy, uz * uz));
   const double sig = R[R_INVTM] * kInvLn2xN, m2s = m2 * (sig * sig);
@@ -1715,7 +1743,16 @@ IS3D_HD void mod_setup(const double* R, const double* Y, double mT, double m2, d
   double ec = 1.0;
   if (!L.clamp && L.chemm != 0.0) ec = exp_tab(exp_tab_coef(), etab, L.chemm * kInvLn2xN);
   if (L.clamp) k = 0;
-  L.shiftk = 6755399441055744.0 - (double)k * kExpTabN;
+  // only callers that evaluate tail lanes with mod_quad_tab_tail_t pass allow_tail
+  L.tail = (IS3D_MOD_PLUS && IS3D_MOD_TAIL && allow_tail && !L.clamp && L.chemm * 1.4426950408889634 < k - 55) ? 1 : 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (IS3D_MOD_TAIL && allow_tail) {   // one decision per wavefront, passed through a VGPR (see sep_setup)
+    int t = __all(L.tail);
+    asm volatile("" : "+v"(t));
+    L.tail = t;
+  }
+#endif
+  L.shiftk = 6755399441055744.0 + (L.tail ? 1.0 : -1.0) * ((double)k * kExpTabN);
   const double d = ldexp(renorm_abs * ec, -k);
   L.sign = ldexp(sign * ec, -k);
   L.D0 = d * (mT * Y[Y_MD]); L.Dc = d * Y[Y_WDX]; L.Ds = d * Y[Y_WDY];
@@ -1830,9 +1867,9 @@ IS3D_HD double modt2(const double* R, const double* Y, dbl2 cs) {
 #ifndef IS3D_MOD_STAGED
 #define IS3D_MOD_STAGED 1
 #endif
-template <bool CLAMP>
+template <bool CLAMP, bool TAIL = false>
 IS3D_HD void mod_nq4(const ModLane& L, const double* X, double* num, double* q) {
-  if (CLAMP || !IS3D_MOD_STAGED) {
+  if (!TAIL && (CLAMP || !IS3D_MOD_STAGED)) {
 #pragma unroll
     for (int i = 0; i < 4; i++) mod_nq_x<CLAMP>(L, X[i], num[i], q[i]);
     return;
@@ -1847,7 +1884,7 @@ IS3D_HD void mod_nq4(const ModLane& L, const double* X, double* num, double* q) 
 #else
     const double y = 1.0 / sqrt(X[i]);
 #endif
-    const double g = IS3D_MOD_PLUS ? X[i] * y : -(X[i] * y);
+    const double g = (IS3D_MOD_PLUS && !TAIL) ? X[i] * y : -(X[i] * y);
     const double v = fma(-0.5, X[i] * y * y, 1.5);
     t[i] = fma(g, v, sh);
     rs[i] = fma(g, v, sh - t[i]);
@@ -1865,7 +1902,8 @@ IS3D_HD void mod_nq4(const ModLane& L, const double* X, double* num, double* q) 
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     const double e = ldexp(fma(T[i], p[i], T[i]), ki[i] >> IS3D_EXP_TAB_BITS);
-    if (IS3D_MOD_PLUS) { num[i] = 1.0; q[i] = e + L.sign; }
+    if (TAIL) { num[i] = e; q[i] = 1.0; }
+    else if (IS3D_MOD_PLUS) { num[i] = 1.0; q[i] = e + L.sign; }
     else { num[i] = e; q[i] = fma(L.sign, e, 1.0); }
   }
 }
@@ -1888,6 +1926,21 @@ IS3D_HD void mod_quad_tab_t(const ModLane& L, const dbl2* mw, const double* mt, 
     double pds = fma(L.Dw, mw[i].x, L.D0);
     if (OUT) pds = (pds <= 0.0) ? 0.0 : pds;
     acc[i] = fma(pds * h[i], rp[i], acc[i]);
+  }
+}
+
+// Boltzmann-tail table lane: f 2^k = e^-(x - k ln2) per point, no denominators
+template <bool OUT, typename ACC>
+IS3D_HD void mod_quad_tab_tail_t(const ModLane& L, const dbl2* mw, const double* mt, ACC acc) {
+  double num[4], q[4], X[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) X[i] = fma(L.mT, mt[i], L.E0 + mw[i].y);
+  mod_nq4<false, true>(L, X, num, q);
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    double pds = fma(L.Dw, mw[i].x, L.D0);
+    if (OUT) pds = (pds <= 0.0) ? 0.0 : pds;
+    acc[i] = fma(pds, num[i], acc[i]);
   }
 }
 

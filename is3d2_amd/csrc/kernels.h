@@ -142,6 +142,9 @@ constexpr int kTbQ = 4;
 #ifndef IS3D_TAIL_WAVE
 #define IS3D_TAIL_WAVE 1      // the tail decision per wavefront: a wave mixing tail and other lanes runs one loop
 #endif
+#ifndef IS3D_TAIL_PDL
+#define IS3D_TAIL_PDL 1       // Boltzmann-tail lanes in the per-lane Grad / RTA-CE launches too (sep_quad_pd_tail_t)
+#endif
 #ifndef IS3D_TAIL_PD
 #define IS3D_TAIL_PD 0        // Grad tail lanes: PD table + scalar {pc, ps} instead of {PD, T1}: 2.2% slower (r2d A/B)
 #endif
@@ -348,9 +351,10 @@ __device__ __forceinline__ void sep_phi_loop_tb_tail(const SepLane& L, double mT
 
 // Boltzmann-tail Grad lanes of an F_TB launch, PD-table form: {b', Phi} and PD from LDS, {pc, ps} by scalar
 // loads (sep_quad_pd_tail_t; 6 LDS-array cycles per point instead of 8)
-template <int FLAGS, int KJ, typename CSP>
+template <int MODE, int FLAGS, int KJ, typename CSP>
 __device__ __forceinline__ void sep_phi_loop_pd_tail(const SepLane& L, CSP CS, const dbl2* BP, const double* PD,
                                                      double* acc) {
+  constexpr int FL = (MODE == GRAD) ? SEP_GRAD : SEP_CE;
   constexpr bool REG = (FLAGS & F_REG) != 0, OUT = (FLAGS & F_OUT) != 0;
 #pragma unroll
   for (int jj = 0; jj < KJ; jj += 4) {
@@ -358,7 +362,7 @@ __device__ __forceinline__ void sep_phi_loop_pd_tail(const SepLane& L, CSP CS, c
     double pd[4];
 #pragma unroll
     for (int i = 0; i < 4; i++) { c[i] = cs_at(CS, jj + i); b[i] = BP[jj + i]; pd[i] = PD[jj + i]; }
-    sep_quad_pd_tail_t<REG, OUT>(L, c, b, pd, acc + jj);
+    sep_quad_pd_tail_t<FL, REG, OUT>(L, c, b, pd, acc + jj);
   }
 }
 
@@ -398,6 +402,16 @@ __device__ __forceinline__ void mod_phi_loop_tab(const ModLane& M, const dbl2* M
     double v0, v1;
     mod_pair_tab_t<OUT, CLAMP>(M, MW[jj], MW[jj + 1], MT[jj], MT[jj + 1], v0, v1);
     acc[jj] += v0; acc[jj + 1] += v1;
+  }
+}
+
+// Boltzmann-tail modified lanes, table form (mod_quad_tab_tail_t; KJ % 4 == 0 only: mod_setup's allow_tail)
+template <int FLAGS, int KJ, typename ACC>
+__device__ __forceinline__ void mod_phi_loop_tab_tail(const ModLane& M, const dbl2* MW, const double* MT, ACC acc) {
+  constexpr bool OUT = (FLAGS & F_OUT) != 0;
+  if constexpr (KJ % 4 == 0) {
+#pragma unroll
+    for (int jj = 0; jj < KJ; jj += 4) mod_quad_tab_tail_t<OUT>(M, MW + jj, MT + jj, acc + jj);
   }
 }
 
@@ -496,6 +510,8 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
   constexpr bool FB = MODE >= PTM && (FLAGS & F_FB) != 0;   // separable-fallback launch of a modified mode
   constexpr bool MODMAIN = MODE >= PTM && !FB;              // modified launch: separable lanes left to F_FB
   constexpr bool LY = (FLAGS & F_LY) != 0 || FB;
+  // Boltzmann-tail lanes of the per-lane Grad / RTA-CE launches (PD-table fours, sep_quad_pd_tail_t)
+  constexpr bool PDT = IS3D_TAIL_PDL && !TB && MODE <= CE && IS3D_PD_TABLE && KJ % 4 == 0;
   constexpr bool MP = (FLAGS & F_MP) != 0;                  // several pT per workgroup, one phi block per lane
   const int npw = MP ? A.npw : 1;                           // pT values of this launch's workgroups
   // per-(cell, q, phi) tables built from the per-tile tables (phase C below): Grad / RTA-CE {PD, T1},
@@ -782,31 +798,34 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
           if ((IS3D_EARLY_SKIP & 1) && sep_skips(R, Y, mT, pT, baryon)) continue;
           SepLane L;
           sep_setup(sep_flavor(MODE), R, Y, mT, mT2, m2, mTb, pT, sign, baryon, s_etab, L,
-                    (TB && IS3D_TAIL && (MODE == GRAD || IS3D_TAIL_CE)) ? (IS3D_TAIL_WAVE ? 2 : 1) : 0);
+                    ((TB && IS3D_TAIL && (MODE == GRAD || IS3D_TAIL_CE)) || PDT) ? (IS3D_TAIL_WAVE ? 2 : 1) : 0);
           if (L.skip) continue;
           if constexpr (TB) {
             const dbl2* PT = s_pt + ((long)t * nqw + row) * prow;
             if (IS3D_TAIL && L.tail) {
               if (MODE == GRAD && IS3D_TAIL_PD)
-                sep_phi_loop_pd_tail<FLAGS, KJ>(L, (cs_sptr)A.csg + 2L * (ipt * nphp + j0), BP, qvt + t * nphp + j0, acc);
+                sep_phi_loop_pd_tail<MODE, FLAGS, KJ>(L, (cs_sptr)A.csg + 2L * (ipt * nphp + j0), BP, qvt + t * nphp + j0, acc);
               else
                 sep_phi_loop_tb_tail<MODE, FLAGS, KJ>(L, mT, BP, PT, pet + t * nphp + j0, acc);
             }
             else if (L.fast) sep_phi_loop_tb<MODE, FLAGS, KJ>(L, mT, BP, PT, pet + t * nphp + j0, acc);
             else sep_phi_loop<MODE, FLAGS, false, KJ>(L, CSl, BP, acc);
-          } else if (IS3D_PD_TABLE && IS3D_CS_SCALAR && !MP && MODE <= CE && KJ % 4 == 0 && L.fast && A.njb == 1)
+          } else if (IS3D_PD_TABLE && IS3D_CS_SCALAR && !MP && MODE <= CE && KJ % 4 == 0 && L.fast && A.njb == 1) {
             // one phi block: every lane reads the same {pc, ps}, so they come by scalar loads into SGPRs
             // (VALU operands) instead of LDS (not F_MP: a wavefront can straddle two pT blocks)
-            sep_phi_loop_pd<MODE, FLAGS, KJ, true>(L, (cs_sptr)A.csg + 2L * ipt * nphp, BP, qvt + t * nphp, acc);
-          else if (IS3D_PD_TABLE && MODE <= CE && KJ % 4 == 0 && L.fast)
-            sep_phi_loop_pd<MODE, FLAGS, KJ, true>(L, CSl, BP, qvt + tro, acc);
+            if (PDT && L.tail) sep_phi_loop_pd_tail<MODE, FLAGS, KJ>(L, (cs_sptr)A.csg + 2L * ipt * nphp, BP, qvt + t * nphp, acc);
+            else sep_phi_loop_pd<MODE, FLAGS, KJ, true>(L, (cs_sptr)A.csg + 2L * ipt * nphp, BP, qvt + t * nphp, acc);
+          } else if (IS3D_PD_TABLE && MODE <= CE && KJ % 4 == 0 && L.fast) {
+            if (PDT && L.tail) sep_phi_loop_pd_tail<MODE, FLAGS, KJ>(L, CSl, BP, qvt + tro, acc);
+            else sep_phi_loop_pd<MODE, FLAGS, KJ, true>(L, CSl, BP, qvt + tro, acc);
+          }
           else if (L.fast) sep_phi_loop<MODE, FLAGS, true, KJ>(L, CSl, BP, acc);
           else sep_phi_loop<MODE, FLAGS, false, KJ>(L, CSl, BP, acc);
         }
         if constexpr (MODMAIN) {
           if ((IS3D_EARLY_SKIP & 2) && IS3D_MOD_SQ_BOUNDS && mod_skips(R, Y, mT, m2, pT, baryon, !LY)) continue;
           ModLane M;
-          mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, s_etab, M, !LY);
+          mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, s_etab, M, !LY, !LY && KJ % 4 == 0);
           if (M.skip) continue;
           const dbl2* MW = mwt + t * nphp + j0;
           if constexpr (LY) {        // no T2 rows: the lane's linear forms (mod_pair_lane_t)
@@ -816,6 +835,7 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
           }
           const double* MT = s_mt + ((long)t * nqw + row) * prow;
           if (M.clamp) mod_phi_loop_tab<FLAGS, true, KJ>(M, MW, MT, acc);
+          else if (IS3D_MOD_TAIL && M.tail) mod_phi_loop_tab_tail<FLAGS, KJ>(M, MW, MT, acc);
           else mod_phi_loop_tab<FLAGS, false, KJ>(M, MW, MT, acc);
         }
       }

@@ -195,8 +195,10 @@ extern "C" int emu_spectra_v(const orc_params* p, const orc_setup* su, const orc
             const bool sep = (mode <= CE) || kind == 1.0 || Y[Y_NARROW] != 0.0;
             if (sep) {
               SepLane L;
+              // tail lanes: the F_TB fours, or k_spectra's per-lane PD-table fours (Grad / RTA-CE, phi blocks of fours)
+              const bool pd_tail = tail && !use_tb && mode <= CE && spectra_kj(nphi) % 4 == 0;
               sep_setup(sep_flavor(mode), R, Y, mT, mT * mT, m2, mT * baryon, pT, sign, baryon, kExp2Tab, L,
-                        use_tb && tail);
+                        (use_tb || pd_tail) && tail);
               if (g_census) g_census[i * 3 + (L.skip ? 0 : (L.tail ? 1 : 2))]++;
               if (g_census_lane)
                 g_census_lane[(((size_t)i * n + c) * np + s) * nq + kk * nl + l] = (signed char)(1 + (L.skip ? 0 : (L.tail ? 1 : 2)));
@@ -222,6 +224,29 @@ extern "C" int emu_spectra_v(const orc_params* p, const orc_setup* su, const orc
 #undef EMU_TB
                     for (int i = 0; i < 4; i++) a[j4 + i] += v[i];
                   }
+                }
+                continue;
+              }
+              if (L.fast && L.tail) {   // pd_tail: k_spectra's per-lane Boltzmann-tail fours over the padded phi row
+                const int rg = p->regulate_deltaf, of = p->outflow;
+                for (int j4 = 0; j4 < nphi; j4 += 4) {
+                  dbl2 c4[4], b4[4];
+                  double P[4], a4[4];
+                  for (int i = 0; i < 4; i++) {
+                    const int jj = j4 + i;
+                    const bool in = jj < nphi;
+                    c4[i].x = in ? CS[jj].x : 0.0; c4[i].y = in ? CS[jj].y : 0.0;
+                    b4[i].x = in ? BP[jj].x : 0.0; b4[i].y = in ? BP[jj].y : 0.0;
+                    P[i] = in ? sep_pd(R, CS[jj], BP[jj].x) : 0.0;
+                    a4[i] = in ? a[jj] : 0.0;
+                  }
+#define EMU_PDT(FLV, RG, OF) sep_quad_pd_tail_t<FLV, RG, OF>(L, c4, b4, P, a4)
+                  if (mode == GRAD) { if (rg) { if (of) EMU_PDT(SEP_GRAD, true, true); else EMU_PDT(SEP_GRAD, true, false); }
+                                      else { if (of) EMU_PDT(SEP_GRAD, false, true); else EMU_PDT(SEP_GRAD, false, false); } }
+                  else { if (rg) { if (of) EMU_PDT(SEP_CE, true, true); else EMU_PDT(SEP_CE, true, false); }
+                         else { if (of) EMU_PDT(SEP_CE, false, true); else EMU_PDT(SEP_CE, false, false); } }
+#undef EMU_PDT
+                  for (int i = 0; i < 4 && j4 + i < nphi; i++) a[j4 + i] = a4[i];
                 }
                 continue;
               }

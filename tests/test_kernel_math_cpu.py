@@ -154,6 +154,30 @@ def test_table_and_tail_algebra(dim, mode, reg_out):
         assert not np.array_equal(got, base)       # the variant's arithmetic really ran
 
 
+PHI30 = (2 * np.pi * np.arange(30) / 30, np.full(30, 2 * np.pi / 30))
+
+
+@pytest.mark.parametrize("dim,mode,baryon,reg_out,phi", [
+    (3, 1, 1, (0, 0), "phi32"), (3, 2, 1, (0, 0), "phi32"), (3, 2, 0, (1, 1), "phi24"), (3, 1, 1, (1, 0), PHI30),
+    (3, 2, 1, (0, 1), PHI30), (2, 1, 0, (0, 0), "phi24"), (2, 2, 1, (1, 0), "phi24")])
+def test_pd_tail_lanes(dim, mode, baryon, reg_out, phi):
+    """Boltzmann-tail lanes of k_spectra's per-lane Grad / RTA-CE launches (variant 2, sep_quad_pd_tail_t: the
+    PD-table fours with 1/a folded into p.dsigma, 1 - sign f_eq = 1, one 1/E per four points for RTA-CE) on the
+    host, against the oracle: baryon on (the launches that carry it), regulate / outflow, a 30-point phi
+    row padded to the 32-point block, 2+1D eta-weighted lanes."""
+    s = synth.as_read(synth.surface(6, seed=23, dimension=dim, baryon=bool(baryon), full3d=(dim == 3)))
+    spec = make_spec(hrg_eos=2, chosen="smash", df_mode=mode, dimension=dim, pT="pT24", phi=phi,
+                     include_baryon=baryon, include_baryondiff_deltaf=baryon,
+                     regulate_deltaf=reg_out[0], outflow=reg_out[1])
+    ref = O.spectra(spec, s, threads=1)
+    base, _ = emu_spectra(spec, s)
+    got, _ = emu_spectra(spec, s, variant=2)
+    rel, zr, zg = parity(got, ref, floor=1e-290)
+    assert rel < 1e-8, rel
+    assert zr == zg
+    assert not np.array_equal(got, base)       # the tail arithmetic really ran
+
+
 @pytest.mark.parametrize("mode,baryon", [(3, 0), (4, 0), (5, 0), (3, 1), (5, 1)])
 def test_modified_table_lanes(mode, baryon):
     """k_spectra's modified-path table lanes (variant 4: mod_quad_tab_t in exp-table units -- e^(-E_mod/T_mod)
