@@ -9,6 +9,8 @@
 #include <cstring>
 #include <vector>
 
+// the modified path's Boltzmann-tail lanes are compiled in (taken only under variant 16)
+#define IS3D_MOD_TAIL 1
 #include "../../is3d2_amd/csrc/aniso_math.h"
 #include "../../is3d2_amd/csrc/cf_math.h"
 #include "../../is3d2_amd/csrc/spline_host.h"
@@ -278,7 +280,9 @@ extern "C" int emu_spectra_v(const orc_params* p, const orc_setup* su, const orc
                 a[j] += sep_point(sep_flavor(mode), L, CS[j], BP[j], p->regulate_deltaf, p->outflow);
             } else {
               ModLane M;
-              mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, kExp2Tab, M);
+              // variant 16 (with 4): k_spectra's Boltzmann-tail table lanes (IS3D_MOD_TAIL builds; per lane here)
+              const bool mtail = (variant & 20) == 20 && op != 0 && nphi % 4 == 0;
+              mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, kExp2Tab, M, true, mtail);
               if (M.skip) continue;
               int j = 0;
               if ((variant & 4) && op != 0) {   // k_spectra's table form: {PDm, Qv} and T2 rows
@@ -291,7 +295,8 @@ extern "C" int emu_spectra_v(const orc_params* p, const orc_setup* su, const orc
                 const bool of = p->outflow != 0;
                 if (spectra_kj(nphi) % 4 == 0)
                   for (; j + 3 < nphi; j += 4) {
-                    if (M.clamp) { if (of) mod_quad_tab_t<true, true>(M, &MW[j], &MT[j], &a[j]); else mod_quad_tab_t<false, true>(M, &MW[j], &MT[j], &a[j]); }
+                    if (M.tail) { if (of) mod_quad_tab_tail_t<true>(M, &MW[j], &MT[j], &a[j]); else mod_quad_tab_tail_t<false>(M, &MW[j], &MT[j], &a[j]); }
+                    else if (M.clamp) { if (of) mod_quad_tab_t<true, true>(M, &MW[j], &MT[j], &a[j]); else mod_quad_tab_t<false, true>(M, &MW[j], &MT[j], &a[j]); }
                     else { if (of) mod_quad_tab_t<true, false>(M, &MW[j], &MT[j], &a[j]); else mod_quad_tab_t<false, false>(M, &MW[j], &MT[j], &a[j]); }
                   }
                 for (; j + 1 < nphi; j += 2) {

@@ -28,11 +28,11 @@ def spectra(spec, s, classes):
 
 
 @pytest.mark.parametrize("mode", [1, 2, 3, 4, 5])
-def test_classes_bit_identical_config3_grid(mode):
+def test_classes_config3_grid(mode):
     """Config 3's shape (SMASH 444 x 48 x 32 x 21, 3+1D, shear + bulk (+ baryon + diffusion; PTB without,
-    DeltafData.cpp:480-483)): classes on and off give the same bits (Grad / RTA-CE: the same to rounding, their
-    Boltzmann-tail form is decided per wavefront and the two launches group different lanes into wavefronts),
-    and the class count is the key's."""
+    DeltafData.cpp:480-483)): classes on and off give the same spectra to rounding (every mode's Boltzmann-tail
+    form is decided per wavefront, and the two launches group different lanes into wavefronts; before the
+    wavefront-wide decisions they agreed bit for bit), the same breakdown count, and the class count is the key's."""
     baryon = mode != 4
     s = synth.as_read(synth.surface(10, seed=41, dimension=3, baryon=baryon, full3d=True))
     spec = make_spec(hrg_eos=2, chosen="smash", df_mode=mode, dimension=3, pT="pT48", phi="phi32", y="y21",
@@ -43,11 +43,9 @@ def test_classes_bit_identical_config3_grid(mode):
     key = zip(sp["mass"], sp["sign"], sp["baryon"], sp["degen"] if mode == 3 else [0] * len(sp["mass"]))
     assert n_off == len(sp["mass"]) == 444
     assert n_on == len(set(key)) == (205 if mode == 3 else 193)
-    if mode <= 2:   # Boltzmann-tail form decided per wavefront (sep_setup allow_tail = 2): equal to rounding
-        assert parity(on, off, floor=1e-290)[0] < 1e-9
-        assert np.array_equal(np.isfinite(on), np.isfinite(off))
-    else:
-        assert np.array_equal(on, off)
+    # Boltzmann-tail forms decided per wavefront (sep_setup allow_tail = 2, mod_setup allow_tail): equal to rounding
+    assert parity(on, off, floor=1e-290)[0] < 1e-9
+    assert np.array_equal(np.isfinite(on), np.isfinite(off))
     assert st_on["breakdown"] == st_off["breakdown"]
 
 

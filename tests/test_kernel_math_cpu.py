@@ -191,3 +191,9 @@ def test_modified_table_lanes(mode, baryon):
     rel, zr, zg = parity(got, ref, floor=1e-290)
     assert rel < 1e-8, rel
     assert zr == zg
+    # the Boltzmann-tail table lanes (variant 16, mod_quad_tab_tail_t: |sign e^chem 2^-k| < 2^-55, no denominators)
+    tail, _ = emu_spectra(spec, s, chains=1, variant=4 | 16)
+    rel, zr, zg = parity(tail, ref, floor=1e-290)
+    assert rel < 1e-8, rel
+    assert zr == zg
+    assert not np.array_equal(tail, got)
