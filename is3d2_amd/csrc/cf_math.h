@@ -1430,14 +1430,13 @@ IS3D_HD void sep_quad_pd_t(const SepLane& L, const dbl2* c, const dbl2* b, const
 // RTA-CE (SEP_CE) in the same launch also takes, per (cell, phi), pe = {TE, T2} with
 // TE = -(u^x pc + u^y ps) and T2 = LC pc + LS ps (cell-only lane coefficients, sep_cell_consts):
 //   E = E0 + TE,  a (L0 + Lc pc + Ls ps) = fma(a, T2, L0')   -- five ops per point instead of eight.
-// SC = false: a caller that knows escw == 1 for the whole wave (3+1D, no 2^-k lane scale) skips its multiply.
-template <int FL, bool REG, bool OUT, bool SC = true>
+template <int FL, bool REG, bool OUT>
 IS3D_HD void sep_quad_tb_t(const SepLane& L, double mT, const dbl2* b, const dbl2* pt, const dbl2* pe, double* v) {
   constexpr bool needE = FL == SEP_CE;
   double pb[4], q[4], E[4];
 #pragma unroll
   for (int i = 0; i < 4; i++) {
-    pb[i] = fma(L.D0, b[i].x, SC ? L.escw * pt[i].x : pt[i].x);
+    pb[i] = fma(L.D0, b[i].x, L.escw * pt[i].x);
     const double den = fma(L.ssc, b[i].x, L.a);
     E[i] = needE ? L.E0 + pe[i].x : 1.0;
     q[i] = needE ? den * E[i] : den;

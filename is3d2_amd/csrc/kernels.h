@@ -142,9 +142,6 @@ constexpr int kTbQ = 4;
 #ifndef IS3D_TAIL_WAVE
 #define IS3D_TAIL_WAVE 1      // the tail decision per wavefront: a wave mixing tail and other lanes runs one loop
 #endif
-#ifndef IS3D_SC1
-#define IS3D_SC1 1            // fast Grad / RTA-CE fours: a wave whose lanes all have escw == 1 (3+1D, no 2^-k scale)
-#endif                        // drops the escw multiply per point (sep_quad_tb_t / sep_quad_pd_t SC = false)
 #ifndef IS3D_TAIL_PDL
 #define IS3D_TAIL_PDL 1       // Boltzmann-tail lanes in the per-lane Grad / RTA-CE launches too (sep_quad_pd_tail_t)
 #endif
@@ -312,7 +309,7 @@ __device__ __forceinline__ void sep_phi_loop_pd(const SepLane& L, CSP CS, const 
 }
 
 // fast Grad lanes of an F_TB launch: fours from the {b', Phi} and {PD, T1} tables (sep_quad_tb_t)
-template <int MODE, int FLAGS, int KJ, bool SC = true>
+template <int MODE, int FLAGS, int KJ>
 __device__ __forceinline__ void sep_phi_loop_tb(const SepLane& L, double mT, const dbl2* BP, const dbl2* PT,
                                                 const dbl2* PE, double* acc) {
   constexpr int FL = (MODE == GRAD) ? SEP_GRAD : SEP_CE;
@@ -327,7 +324,7 @@ __device__ __forceinline__ void sep_phi_loop_tb(const SepLane& L, double mT, con
       b[i] = BP[jj + i]; pt[i] = PT[jj + i];
       if (FL == SEP_CE) pe[i] = PE[jj + i];
     }
-    sep_quad_tb_t<FL, REG, OUT, SC>(L, mT, b, pt, pe, v);
+    sep_quad_tb_t<FL, REG, OUT>(L, mT, b, pt, pe, v);
 #pragma unroll
     for (int i = 0; i < 4; i++) acc[jj + i] += v[i];
   }
@@ -497,14 +494,6 @@ __device__ __forceinline__ void fetch_tile(const double* rec, long cb, long c_en
                                        (__attribute__((address_space(3))) void*)(dst + 2 * wave0), 16, 0, 0);
     }
   }
-}
-
-// every live lane of the wavefront satisfies p (the result is kept in a VGPR: a wave-uniform SGPR branch made
-// the compiler restructure k_spectra's lane loops and spill, see sep_setup)
-__device__ __forceinline__ bool wave_all(bool p) {
-  int t = __all(p);
-  asm volatile("" : "+v"(t));
-  return t != 0;
 }
 
 __device__ __forceinline__ void wait_fetch() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
@@ -819,16 +808,12 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
               else
                 sep_phi_loop_tb_tail<MODE, FLAGS, KJ>(L, mT, BP, PT, pet + t * nphp + j0, acc);
             }
-            else if (L.fast) {
-              if (IS3D_SC1 && wave_all(L.escw == 1.0)) sep_phi_loop_tb<MODE, FLAGS, KJ, false>(L, mT, BP, PT, pet + t * nphp + j0, acc);
-              else sep_phi_loop_tb<MODE, FLAGS, KJ, true>(L, mT, BP, PT, pet + t * nphp + j0, acc);
-            }
+            else if (L.fast) sep_phi_loop_tb<MODE, FLAGS, KJ>(L, mT, BP, PT, pet + t * nphp + j0, acc);
             else sep_phi_loop<MODE, FLAGS, false, KJ>(L, CSl, BP, acc);
           } else if (IS3D_PD_TABLE && IS3D_CS_SCALAR && !MP && MODE <= CE && KJ % 4 == 0 && L.fast && A.njb == 1) {
             // one phi block: every lane reads the same {pc, ps}, so they come by scalar loads into SGPRs
             // (VALU operands) instead of LDS (not F_MP: a wavefront can straddle two pT blocks)
             if (PDT && L.tail) sep_phi_loop_pd_tail<MODE, FLAGS, KJ>(L, (cs_sptr)A.csg + 2L * ipt * nphp, BP, qvt + t * nphp, acc);
-            else if (IS3D_SC1 && wave_all(L.escw == 1.0)) sep_phi_loop_pd<MODE, FLAGS, KJ, false>(L, (cs_sptr)A.csg + 2L * ipt * nphp, BP, qvt + t * nphp, acc);
             else sep_phi_loop_pd<MODE, FLAGS, KJ, true>(L, (cs_sptr)A.csg + 2L * ipt * nphp, BP, qvt + t * nphp, acc);
           } else if (IS3D_PD_TABLE && MODE <= CE && KJ % 4 == 0 && L.fast) {
             if (PDT && L.tail) sep_phi_loop_pd_tail<MODE, FLAGS, KJ>(L, CSl, BP, qvt + tro, acc);
