@@ -1328,6 +1328,33 @@ IS3D_HD void sep_pair_t(const SepLane& L, dbl2 c0, dbl2 b0, dbl2 c1, dbl2 b1, do
   v1 = sep_fast_tail<FL, REG, OUT>(L, c1, b1, pds1, E1, r * q0);
 }
 
+// Two Boltzmann-tail points (sep_setup allow_tail: 1/a folded into D0 / Dc / Ds, delta-f coefficients
+// unscaled; k_dndx's pairs): pb = w p.dsigma f_eq = lin(D0, Dc, Ds) b', then as sep_quad_pd_tail_t
+//   Grad  pb (1 + S)        RTA-CE  pb (1 + L + S / E), one 1/E per pair
+template <int FL, bool REG, bool OUT>
+IS3D_HD void sep_pair_tail_t(const SepLane& L, dbl2 c0, dbl2 b0, dbl2 c1, dbl2 b1, double& v0, double& v1) {
+  constexpr bool needE = FL == SEP_CE;
+  double rE0 = 0.0, rE1 = 0.0;
+  if (needE) {
+    const double E0 = lin(L.E0, L.Ec, L.Es, c0), E1 = lin(L.E0, L.Ec, L.Es, c1);
+    const double r = rcp1(E0 * E1);
+    rE0 = r * E1; rE1 = r * E0;
+  }
+  const dbl2 c[2] = {c0, c1}, b[2] = {b0, b1};
+  const double rE[2] = {rE0, rE1};
+  double v[2];
+#pragma unroll
+  for (int i = 0; i < 2; i++) {
+    double pb = lin(L.D0, L.Dc, L.Ds, c[i]) * b[i].x;
+    if (OUT) pb = (pb <= 0.0) ? 0.0 : pb;
+    const double S = lin(L.S0, L.Sc, L.Ss, c[i]) + b[i].y;
+    const double dfv = needE ? fma(S, rE[i], lin(L.L0, L.Lc, L.Ls, c[i])) : S;
+    const double t = REG ? 1.0 + fmax(-1.0, fmin(dfv, 1.0)) : 1.0 + dfv;
+    v[i] = pb * t;
+  }
+  v0 = v[0]; v1 = v[1];
+}
+
 // Four fast-path points with one reciprocal: r = 1/(q0 q1 q2 q3), 1/(q0 q1) = r q2 q3, then as the pair
 template <int FL, bool REG, bool OUT>
 IS3D_HD void sep_quad_t(const SepLane& L, const dbl2* c, const dbl2* b, double* v) {

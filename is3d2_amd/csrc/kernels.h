@@ -108,6 +108,9 @@ constexpr int kTbQ = 4;
                                       // config2 PTM 467 -> 461 ms, PTB 437 -> 431, config4 3194 -> 3180 ms, Grad unchanged;
                                       // profiles/round3_r3j_ab_split.log)
 #endif
+#ifndef IS3D_SPLIT_BYTES_SEP
+#define IS3D_SPLIT_BYTES_SEP (2048L << 10)   // the same for Grad / RTA-CE (no renormalisation rows to keep in L2):
+#endif                                       // 4x fewer output-sized slabs written and re-read
 #ifndef IS3D_NOPF_MODES
 #define IS3D_NOPF_MODES 0     // bit m: mode m's fours skip the one-quad-ahead prefetch (register-starved builds)
 #endif
@@ -144,6 +147,9 @@ constexpr int kTbQ = 4;
 #endif
 #ifndef IS3D_TAIL_PDL
 #define IS3D_TAIL_PDL 1       // Boltzmann-tail lanes in the per-lane Grad / RTA-CE launches too (sep_quad_pd_tail_t)
+#endif
+#ifndef IS3D_TAIL_DNDX
+#define IS3D_TAIL_DNDX 1      // operation 0 (k_dndx): Boltzmann-tail Grad / RTA-CE lanes in pairs (sep_pair_tail_t)
 #endif
 #ifndef IS3D_TAIL_PD
 #define IS3D_TAIL_PD 0        // Grad tail lanes: PD table + scalar {pc, ps} instead of {PD, T1}: 2.2% slower (r2d A/B)
@@ -882,6 +888,22 @@ __device__ __forceinline__ double sep_phi_wsum(const SepLane& L, const dbl2* CS,
   return a0 + a1;
 }
 
+// sep_phi_wsum for a Boltzmann-tail lane (Grad / RTA-CE, sep_setup allow_tail): sep_pair_tail_t
+template <int MODE, int FLAGS, int KJ>
+__device__ __forceinline__ double sep_phi_wsum_tail(const SepLane& L, const dbl2* CS, const dbl2* BP, const dbl2* W) {
+  constexpr int FL = (MODE == GRAD) ? SEP_GRAD : SEP_CE;
+  constexpr bool REG = (FLAGS & F_REG) != 0, OUT = (FLAGS & F_OUT) != 0;
+  double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+  for (int jj = 0; jj < KJ; jj += 2) {
+    const dbl2 w = W[jj >> 1];
+    double v0, v1;
+    sep_pair_tail_t<FL, REG, OUT>(L, CS[jj], BP[jj], CS[jj + 1], BP[jj + 1], v0, v1);
+    a0 = fma(w.x, v0, a0); a1 = fma(w.y, v1, a1);
+  }
+  return a0 + a1;
+}
+
 template <int FLAGS, bool CLAMP, int KJ>
 __device__ __forceinline__ double mod_phi_wsum(const ModLane& M, const dbl2* CS, const dbl2* QV, const dbl2* W) {
   constexpr bool OUT = (FLAGS & F_OUT) != 0;
@@ -1018,10 +1040,13 @@ __global__ __launch_bounds__(kBlock, dndx_waves<MODE>()) void k_dndx(DndxArgs A)
           const bool sep = (MODE <= CE) || kind == 1.0 || Y[Y_NARROW] != 0.0;
           if (sep) {
             SepLane L;
-            sep_setup(sep_flavor(MODE), R, Y, mT, mT2, m2, mTb, pT, sign, baryon, s_etab, L);
+            // Boltzmann-tail lanes of Grad / RTA-CE (decided per wavefront, as in k_spectra)
+            constexpr bool TL = IS3D_TAIL_DNDX && MODE <= CE;
+            sep_setup(sep_flavor(MODE), R, Y, mT, mT2, m2, mTb, pT, sign, baryon, s_etab, L, TL ? 2 : 0);
             if (L.skip) continue;
-            cell += L.fast ? sep_phi_wsum<MODE, FLAGS, true, KJ>(L, s_cs + j0, BP, W)
-                           : sep_phi_wsum<MODE, FLAGS, false, KJ>(L, s_cs + j0, BP, W);
+            if (TL && L.tail) cell += sep_phi_wsum_tail<MODE, FLAGS, KJ>(L, s_cs + j0, BP, W);
+            else cell += L.fast ? sep_phi_wsum<MODE, FLAGS, true, KJ>(L, s_cs + j0, BP, W)
+                                : sep_phi_wsum<MODE, FLAGS, false, KJ>(L, s_cs + j0, BP, W);
           } else if (MODE >= PTM) {
             ModLane M;
             mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, s_etab, M, false);

@@ -147,7 +147,7 @@ extern "C" int emu_spectra_v(const orc_params* p, const orc_setup* su, const orc
   std::vector<double> QV(nphi + 1);
   std::vector<dbl2> PE(nphi), PTq((size_t)nq * nphi);
   const bool use_tb = (variant & 1) && op != 0 && mode <= CE && !p->include_baryon && nphi % 4 == 0;
-  const bool tail = (variant & 2) != 0 && op != 0;
+  const bool tail = (variant & 2) != 0;
   std::vector<double> acc((size_t)np * nk * nphi);
   for (int i = 0; i < npT; i++) {
     const double pT = su->pT[i];
@@ -198,7 +198,8 @@ extern "C" int emu_spectra_v(const orc_params* p, const orc_setup* su, const orc
             if (sep) {
               SepLane L;
               // tail lanes: the F_TB fours, or k_spectra's per-lane PD-table fours (Grad / RTA-CE, phi blocks of fours)
-              const bool pd_tail = tail && !use_tb && mode <= CE && spectra_kj(nphi) % 4 == 0;
+              // (operation 0: k_dndx's tail pairs, any phi block)
+              const bool pd_tail = tail && !use_tb && mode <= CE && (op == 0 || spectra_kj(nphi) % 4 == 0);
               sep_setup(sep_flavor(mode), R, Y, mT, mT * mT, m2, mT * baryon, pT, sign, baryon, kExp2Tab, L,
                         (use_tb || pd_tail) && tail);
               if (g_census) g_census[i * 3 + (L.skip ? 0 : (L.tail ? 1 : 2))]++;
@@ -226,6 +227,25 @@ extern "C" int emu_spectra_v(const orc_params* p, const orc_setup* su, const orc
 #undef EMU_TB
                     for (int i = 0; i < 4; i++) a[j4 + i] += v[i];
                   }
+                }
+                continue;
+              }
+              // k_dndx's tail pairs (phi rows padded to even length); variant 32: the same pairs for operation 1, whose
+              // per-y outputs show the pair arithmetic (in operation 0 the tail lanes' share of a cell yield is ~e^-24)
+              if (L.fast && L.tail && (op == 0 || (variant & 32))) {
+                const int rg = p->regulate_deltaf, of = p->outflow;
+                for (int j2 = 0; j2 < nphi; j2 += 2) {
+                  dbl2 z; z.x = 0.0; z.y = 0.0;
+                  const dbl2 c1 = (j2 + 1 < nphi) ? CS[j2 + 1] : z, b1 = (j2 + 1 < nphi) ? BP[j2 + 1] : z;
+                  double v0, v1;
+#define EMU_PRT(FLV, RG, OF) sep_pair_tail_t<FLV, RG, OF>(L, CS[j2], BP[j2], c1, b1, v0, v1)
+                  if (mode == GRAD) { if (rg) { if (of) EMU_PRT(SEP_GRAD, true, true); else EMU_PRT(SEP_GRAD, true, false); }
+                                      else { if (of) EMU_PRT(SEP_GRAD, false, true); else EMU_PRT(SEP_GRAD, false, false); } }
+                  else { if (rg) { if (of) EMU_PRT(SEP_CE, true, true); else EMU_PRT(SEP_CE, true, false); }
+                         else { if (of) EMU_PRT(SEP_CE, false, true); else EMU_PRT(SEP_CE, false, false); } }
+#undef EMU_PRT
+                  a[j2] += v0;
+                  if (j2 + 1 < nphi) a[j2 + 1] += v1;
                 }
                 continue;
               }

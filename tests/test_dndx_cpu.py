@@ -19,6 +19,29 @@ def test_cell_yield_math_matches_oracle(dim, mode):
     _, _, _, cy = O.dndx(spec, s, threads=1, return_cells=True)
     got, _ = emu_spectra(spec, s, op=0)
     assert parity(got, cy.ravel())[0] < 1e-12
+    if mode <= 2:   # k_dndx's Boltzmann-tail pairs (variant 2, sep_pair_tail_t)
+        tail, _ = emu_spectra(spec, s, op=0, variant=2)
+        assert parity(tail, cy.ravel())[0] < 1e-12
+
+
+@pytest.mark.parametrize("mode,reg_out", [(1, (1, 1)), (2, (1, 0)), (2, (0, 1))])
+def test_cell_yield_tail_pairs_smash(mode, reg_out):
+    """k_dndx's Boltzmann-tail pairs (sep_pair_tail_t) over the SMASH list, baryon on, regulate / outflow,
+    against the oracle's per-cell yields and, for the pair arithmetic itself, its spectra."""
+    s = synth.as_read(synth.surface(8, seed=29, dimension=3, baryon=True, full3d=True))
+    spec = make_spec(hrg_eos=2, chosen="smash", df_mode=mode, dimension=3, pT="pT24", phi="phi24",
+                     include_baryon=1, include_baryondiff_deltaf=1, regulate_deltaf=reg_out[0], outflow=reg_out[1])
+    _, _, _, cy = O.dndx(spec, s, threads=1, return_cells=True)
+    tail, _ = emu_spectra(spec, s, op=0, variant=2)
+    rel = parity(tail, cy.ravel(), floor=1e-290)[0]
+    assert rel < 1e-10, rel
+    # a tail lane's share of a cell yield is ~e^-24 of the lanes near the cell's rapidity, so the pair arithmetic
+    # shows in operation 1's per-y outputs (variant 32: the same pairs there) against the oracle's spectra
+    ref = O.spectra(spec, s, threads=1)
+    got, _ = emu_spectra(spec, s, variant=2 | 32)
+    base, _ = emu_spectra(spec, s)
+    assert parity(got, ref, floor=1e-290)[0] < 1e-8
+    assert not np.array_equal(got, base)      # the tail pairs really ran
 
 
 @pytest.mark.parametrize("mode", [1, 2, 3])
