@@ -1497,9 +1497,7 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   // splits cost config 1's shape 0.5 ms of a 4.7 ms pass -- Grad 4.7 -> 4.2 ms, RTA-CE 5.4 -> 5.0 ms with 2k,
   // while the F_LY launch of the modified modes lost 14% with it: profiles/round3_r3p_ab_fill.log)
   const long by_fill = ((P.mp ? IS3D_FILL_WGS_MP : IS3D_FILL_WGS) + wgs - 1) / wgs;
-  // (Grad / RTA-CE carry no renormalisation rows: their splits may hold 4x the records, a quarter of the slabs)
-  const long split_bytes = (mode <= CE) ? IS3D_SPLIT_BYTES_SEP : IS3D_SPLIT_BYTES;
-  const long by_l2 = ((long)NREC * 8 * nw + split_bytes - 1) / split_bytes;
+  const long by_l2 = ((long)NREC * 8 * nw + IS3D_SPLIT_BYTES - 1) / IS3D_SPLIT_BYTES;
   long nsplit = std::max(by_fill, std::min(by_l2, (long)IS3D_MAX_SPLITS));
   if (nsplit >= 8) nsplit = (nsplit + 7) / 8 * 8;
   nsplit = std::max(1L, std::min(nsplit, max_split));

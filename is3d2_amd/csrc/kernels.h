@@ -106,11 +106,10 @@ constexpr int kTbQ = 4;
 #ifndef IS3D_SPLIT_BYTES
 #define IS3D_SPLIT_BYTES (512L << 10) // record bytes per cell split (k_spectra grid sizing): 0.5 MB (2 MB before round 3:
                                       // config2 PTM 467 -> 461 ms, PTB 437 -> 431, config4 3194 -> 3180 ms, Grad unchanged;
-                                      // profiles/round3_r3j_ab_split.log)
+                                      // profiles/round3_r3j_ab_split.log; 2 MB for Grad / RTA-CE alone -- a quarter
+                                      // of the slabs -- measured again on the round-3 final kernels: Grad 195 -> 196 ms,
+                                      // RTA-CE 313 -> 321 ms, config4 3153 -> 3175 ms, round3_r3x_ab_split_dndx_tail.log)
 #endif
-#ifndef IS3D_SPLIT_BYTES_SEP
-#define IS3D_SPLIT_BYTES_SEP (2048L << 10)   // the same for Grad / RTA-CE (no renormalisation rows to keep in L2):
-#endif                                       // 4x fewer output-sized slabs written and re-read
 #ifndef IS3D_NOPF_MODES
 #define IS3D_NOPF_MODES 0     // bit m: mode m's fours skip the one-quad-ahead prefetch (register-starved builds)
 #endif
@@ -149,7 +148,7 @@ constexpr int kTbQ = 4;
 #define IS3D_TAIL_PDL 1       // Boltzmann-tail lanes in the per-lane Grad / RTA-CE launches too (sep_quad_pd_tail_t)
 #endif
 #ifndef IS3D_TAIL_DNDX
-#define IS3D_TAIL_DNDX 1      // operation 0 (k_dndx): Boltzmann-tail Grad / RTA-CE lanes in pairs (sep_pair_tail_t)
+#define IS3D_TAIL_DNDX 1      // operation 0 (k_dndx): Boltzmann-tail Grad lanes in pairs (sep_pair_tail_t)
 #endif
 #ifndef IS3D_TAIL_PD
 #define IS3D_TAIL_PD 0        // Grad tail lanes: PD table + scalar {pc, ps} instead of {PD, T1}: 2.2% slower (r2d A/B)
@@ -1041,7 +1040,9 @@ __global__ __launch_bounds__(kBlock, dndx_waves<MODE>()) void k_dndx(DndxArgs A)
           if (sep) {
             SepLane L;
             // Boltzmann-tail lanes of Grad / RTA-CE (decided per wavefront, as in k_spectra)
-            constexpr bool TL = IS3D_TAIL_DNDX && MODE <= CE;
+            // (Grad only: RTA-CE's tail pairs, one 1/E per pair, were slower -- 508 -> 560 ms at config 2 against
+            // Grad's 404 -> 333 ms, profiles/round3_r3x_ab_split_dndx_tail.log)
+            constexpr bool TL = IS3D_TAIL_DNDX && MODE == GRAD;
             sep_setup(sep_flavor(MODE), R, Y, mT, mT2, m2, mTb, pT, sign, baryon, s_etab, L, TL ? 2 : 0);
             if (L.skip) continue;
             if (TL && L.tail) cell += sep_phi_wsum_tail<MODE, FLAGS, KJ>(L, s_cs + j0, BP, W);
