@@ -1449,6 +1449,46 @@ IS3D_HD void sep_quad_pd_t(const SepLane& L, const dbl2* c, const dbl2* b, const
   v[3] = sep_fast_tail_pb<FL, REG, OUT>(L, c[3], b[3], pb[3], E[3], r23 * q[2]);
 }
 
+// RTA-CE fours of the per-lane launch with the cell's {TE, T2} table as well (pe[i], as in sep_quad_tb_t):
+// E = E0 + TE and the lane's linear delta-f part a (L0/a + Lc pc + Ls ps) = fma(a, T2, L0) -- two ops per point
+// fewer than the lane's own linear forms.  TAIL: a Boltzmann-tail lane (sep_setup allow_tail: unscaled
+// coefficients, 1/a in p.dsigma), acc += pb (1 + L0 + T2 + S / E), one 1/E per four points.
+template <bool REG, bool OUT, bool TAIL>
+IS3D_HD void sep_quad_pde_t(const SepLane& L, const dbl2* c, const dbl2* b, const double* pd, const dbl2* pe,
+                            double* acc) {
+  double pb[4], E[4], q[4];
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    pb[i] = fma(L.D0, b[i].x, L.escw * pd[i]);
+    E[i] = L.E0 + pe[i].x;
+    q[i] = TAIL ? E[i] : fma(L.ssc, b[i].x, L.a) * E[i];
+  }
+  const double q01 = q[0] * q[1], q23 = q[2] * q[3];
+  const double r = rcp1(q01 * q23);
+  const double r01 = r * q23, r23 = r * q01;
+  const double rq[4] = {r01 * q[1], r01 * q[0], r23 * q[3], r23 * q[2]};
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    if (TAIL) {   // rq = 1/E
+      double p = pb[i];
+      if (OUT) p = (p <= 0.0) ? 0.0 : p;
+      const double S = lin(L.S0, L.Sc, L.Ss, c[i]) + b[i].y;
+      double t;
+      if (REG) t = 1.0 + fmax(-1.0, fmin(fma(S, rq[i], L.L0 + pe[i].y), 1.0));
+      else t = fma(S, rq[i], (1.0 + L.L0) + pe[i].y);
+      acc[i] = fma(p, t, acc[i]);
+    } else {      // rq = 1/(den E), as sep_fast_tail_pb with lin(L0, Lc, Ls) = fma(a, T2, L0)
+      double in = fma(L.a, b[i].y, lin(L.S0, L.Sc, L.Ss, c[i]));
+      in = fma(E[i], fma(L.a, pe[i].y, L.L0), in);
+      double t;
+      if (REG) t = 1.0 + fmax(-1.0, fmin(rq[i] * in, 1.0));
+      else t = fma(rq[i], in, 1.0);
+      const double g = pb[i] * (E[i] * rq[i]) * t;
+      acc[i] += (OUT && pb[i] <= 0.0) ? 0.0 : g;
+    }
+  }
+}
+
 // Grad fours with the linear delta-f part from the (cell, q, phi) table as well.  Without baryon
 // terms (include_baryon = 0: c1 = c3 = 0 and V = 0, so R_SCB = R_SSB = 0 exactly) the lane's
 // Sc pc + Ss ps = a mT (SC1 pc + SS1 ps), and T1 = SC1 pc + SS1 ps depends on (cell, y, phi) only,

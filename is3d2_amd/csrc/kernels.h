@@ -147,6 +147,9 @@ constexpr int kTbQ = 4;
 #ifndef IS3D_TAIL_PDL
 #define IS3D_TAIL_PDL 1       // Boltzmann-tail lanes in the per-lane Grad / RTA-CE launches too (sep_quad_pd_tail_t)
 #endif
+#ifndef IS3D_CE_PE
+#define IS3D_CE_PE 1          // RTA-CE per-lane launch: E and the linear delta-f part from a {TE, T2} table (sep_quad_pde_t)
+#endif
 #ifndef IS3D_TAIL_DNDX
 #define IS3D_TAIL_DNDX 1      // operation 0 (k_dndx): Boltzmann-tail Grad lanes in pairs (sep_pair_tail_t)
 #endif
@@ -310,6 +313,21 @@ __device__ __forceinline__ void sep_phi_loop_pd(const SepLane& L, CSP CS, const 
     sep_quad_pd_t<FL, REG, OUT, SC>(L, c, b, pd, v);
 #pragma unroll
     for (int i = 0; i < 4; i++) { acc[jj + i] += v[i]; c[i] = nc[i]; b[i] = nb[i]; pd[i] = np[i]; }
+  }
+}
+
+// RTA-CE lanes of the per-lane launch with the {TE, T2} table (sep_quad_pde_t; TAIL: Boltzmann-tail lanes)
+template <int FLAGS, int KJ, bool TAIL, typename CSP>
+__device__ __forceinline__ void sep_phi_loop_pde(const SepLane& L, CSP CS, const dbl2* BP, const double* PD,
+                                                 const dbl2* PE, double* acc) {
+  constexpr bool REG = (FLAGS & F_REG) != 0, OUT = (FLAGS & F_OUT) != 0;
+#pragma unroll
+  for (int jj = 0; jj < KJ; jj += 4) {
+    dbl2 c[4], b[4], pe[4];
+    double pd[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) { c[i] = cs_at(CS, jj + i); b[i] = BP[jj + i]; pd[i] = PD[jj + i]; pe[i] = PE[jj + i]; }
+    sep_quad_pde_t<REG, OUT, TAIL>(L, c, b, pd, pe, acc + jj);
   }
 }
 
@@ -517,6 +535,8 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
   constexpr bool LY = (FLAGS & F_LY) != 0 || FB;
   // Boltzmann-tail lanes of the per-lane Grad / RTA-CE launches (PD-table fours, sep_quad_pd_tail_t)
   constexpr bool PDT = IS3D_TAIL_PDL && !TB && MODE <= CE && IS3D_PD_TABLE && KJ % 4 == 0;
+  // RTA-CE per-lane launch with the per-(cell, phi) {TE, T2} table (one pT per workgroup, workgroup y-term rows)
+  constexpr bool PDE = IS3D_CE_PE && MODE == CE && !TB && (FLAGS & F_MP) == 0 && !LY && IS3D_PD_TABLE && KJ % 4 == 0;
   constexpr bool MP = (FLAGS & F_MP) != 0;                  // several pT per workgroup, one phi block per lane
   const int npw = MP ? A.npw : 1;                           // pT values of this launch's workgroups
   // per-(cell, q, phi) tables built from the per-tile tables (phase C below): Grad / RTA-CE {PD, T1},
@@ -552,7 +572,7 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
   // at the same phi by the two halves of a wavefront that straddles a row boundary land in different
   // banks (a 512-B row stride is 128 dwords: the same bank, a 2-way conflict in every straddling wave)
   constexpr int prow = KJ + 1;
-  dbl2* s_pe = s_pt + kTile * nqm * prow;                 // TB, RTA-CE: [kTabBufs][kTile][nphp] {TE, T2}
+  dbl2* s_pe = s_pt + (TB ? kTile * nqm * prow : 0);     // TB / PDE, RTA-CE: [kTabBufs][kTile][nphp] {TE, T2}
   double* s_mt = (double*)s_pt;                           // modified path: [kTile][nqm][prow] T2 = 2 U_q . W
 
   const int tid = threadIdx.x;
@@ -674,7 +694,7 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
       } else {
         qvt[o] = sep_pd(R, csj, v.x);                     // PD table (sep_pd)
       }
-      if constexpr (TB && MODE == CE) {
+      if constexpr ((TB || PDE) && MODE == CE) {
         const dbl2 c = s_cs[j];
         dbl2 e;
         e.x = -fma(R[R_UX], c.x, R[R_UY] * c.y);
@@ -818,11 +838,21 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
           } else if (IS3D_PD_TABLE && IS3D_CS_SCALAR && !MP && MODE <= CE && KJ % 4 == 0 && L.fast && A.njb == 1) {
             // one phi block: every lane reads the same {pc, ps}, so they come by scalar loads into SGPRs
             // (VALU operands) instead of LDS (not F_MP: a wavefront can straddle two pT blocks)
-            if (PDT && L.tail) sep_phi_loop_pd_tail<MODE, FLAGS, KJ>(L, (cs_sptr)A.csg + 2L * ipt * nphp, BP, qvt + t * nphp, acc);
-            else sep_phi_loop_pd<MODE, FLAGS, KJ, true>(L, (cs_sptr)A.csg + 2L * ipt * nphp, BP, qvt + t * nphp, acc);
+            if constexpr (PDE) {
+              if (PDT && L.tail) sep_phi_loop_pde<FLAGS, KJ, true>(L, (cs_sptr)A.csg + 2L * ipt * nphp, BP, qvt + t * nphp, pet + t * nphp, acc);
+              else sep_phi_loop_pde<FLAGS, KJ, false>(L, (cs_sptr)A.csg + 2L * ipt * nphp, BP, qvt + t * nphp, pet + t * nphp, acc);
+            } else {
+              if (PDT && L.tail) sep_phi_loop_pd_tail<MODE, FLAGS, KJ>(L, (cs_sptr)A.csg + 2L * ipt * nphp, BP, qvt + t * nphp, acc);
+              else sep_phi_loop_pd<MODE, FLAGS, KJ, true>(L, (cs_sptr)A.csg + 2L * ipt * nphp, BP, qvt + t * nphp, acc);
+            }
           } else if (IS3D_PD_TABLE && MODE <= CE && KJ % 4 == 0 && L.fast) {
-            if (PDT && L.tail) sep_phi_loop_pd_tail<MODE, FLAGS, KJ>(L, CSl, BP, qvt + tro, acc);
-            else sep_phi_loop_pd<MODE, FLAGS, KJ, true>(L, CSl, BP, qvt + tro, acc);
+            if constexpr (PDE) {
+              if (PDT && L.tail) sep_phi_loop_pde<FLAGS, KJ, true>(L, CSl, BP, qvt + tro, pet + tro, acc);
+              else sep_phi_loop_pde<FLAGS, KJ, false>(L, CSl, BP, qvt + tro, pet + tro, acc);
+            } else {
+              if (PDT && L.tail) sep_phi_loop_pd_tail<MODE, FLAGS, KJ>(L, CSl, BP, qvt + tro, acc);
+              else sep_phi_loop_pd<MODE, FLAGS, KJ, true>(L, CSl, BP, qvt + tro, acc);
+            }
           }
           else if (L.fast) sep_phi_loop<MODE, FLAGS, true, KJ>(L, CSl, BP, acc);
           else sep_phi_loop<MODE, FLAGS, false, KJ>(L, CSl, BP, acc);

@@ -175,7 +175,7 @@ extern "C" int emu_spectra_v(const orc_params* p, const orc_setup* su, const orc
           }
         }
       }
-      if (use_tb && mode == CE)   // {TE, T2}
+      if ((use_tb || (variant & 64)) && mode == CE)   // {TE, T2} (F_TB launch; variant 64: the per-lane launch's)
         for (int j = 0; j < nphi; j++) {
           PE[j].x = -fma(R[R_UX], CS[j].x, R[R_UY] * CS[j].y);
           PE[j].y = fma(R[R_LC], CS[j].x, R[R_LS] * CS[j].y);
@@ -246,6 +246,28 @@ extern "C" int emu_spectra_v(const orc_params* p, const orc_setup* su, const orc
 #undef EMU_PRT
                   a[j2] += v0;
                   if (j2 + 1 < nphi) a[j2 + 1] += v1;
+                }
+                continue;
+              }
+              // variant 64: the per-lane RTA-CE launch's fours with the {TE, T2} table (sep_quad_pde_t), tail or not
+              if (L.fast && (variant & 64) && op != 0 && !use_tb && mode == CE && spectra_kj(nphi) % 4 == 0) {
+                const int rg = p->regulate_deltaf, of = p->outflow;
+                for (int j4 = 0; j4 < nphi; j4 += 4) {
+                  dbl2 c4[4], b4[4], e4[4];
+                  double P[4], a4[4];
+                  for (int i = 0; i < 4; i++) {
+                    const int jj = j4 + i;
+                    const bool in = jj < nphi;
+                    dbl2 z; z.x = 0.0; z.y = 0.0;
+                    c4[i] = in ? CS[jj] : z; b4[i] = in ? BP[jj] : z; e4[i] = in ? PE[jj] : z;
+                    P[i] = in ? sep_pd(R, CS[jj], BP[jj].x) : 0.0;
+                    a4[i] = in ? a[jj] : 0.0;
+                  }
+#define EMU_PDE(RG, OF) (L.tail ? sep_quad_pde_t<RG, OF, true>(L, c4, b4, P, e4, a4) : sep_quad_pde_t<RG, OF, false>(L, c4, b4, P, e4, a4))
+                  if (rg) { if (of) EMU_PDE(true, true); else EMU_PDE(true, false); }
+                  else { if (of) EMU_PDE(false, true); else EMU_PDE(false, false); }
+#undef EMU_PDE
+                  for (int i = 0; i < 4 && j4 + i < nphi; i++) a[j4 + i] = a4[i];
                 }
                 continue;
               }

@@ -178,6 +178,27 @@ def test_pd_tail_lanes(dim, mode, baryon, reg_out, phi):
     assert not np.array_equal(got, base)       # the tail arithmetic really ran
 
 
+@pytest.mark.parametrize("dim,baryon,reg_out,phi", [(3, 1, (0, 0), "phi32"), (3, 0, (1, 1), "phi32"),
+                                                      (3, 1, (1, 0), PHI30), (3, 1, (0, 1), "phi24"),
+                                                      (2, 0, (0, 0), "phi24")])
+def test_ce_te_table_lanes(dim, baryon, reg_out, phi):
+    """RTA-CE lanes of k_spectra's per-lane launch with the per-(cell, phi) {TE, T2} table (variant 64,
+    sep_quad_pde_t: E = E0 + TE, linear delta-f part fma(a, T2, L0)), normal and Boltzmann-tail (2), against the
+    oracle: baryon on, regulate / outflow, a 30-point phi row padded to the 32-point block, 2+1D."""
+    s = synth.as_read(synth.surface(6, seed=31, dimension=dim, baryon=bool(baryon), full3d=(dim == 3)))
+    spec = make_spec(hrg_eos=2, chosen="smash", df_mode=2, dimension=dim, pT="pT24", phi=phi,
+                     include_baryon=baryon, include_baryondiff_deltaf=baryon,
+                     regulate_deltaf=reg_out[0], outflow=reg_out[1])
+    ref = O.spectra(spec, s, threads=1)
+    base, _ = emu_spectra(spec, s)
+    for variant in (64, 64 | 2):
+        got, _ = emu_spectra(spec, s, variant=variant)
+        rel, zr, zg = parity(got, ref, floor=1e-290)
+        assert rel < 1e-8, (variant, rel)
+        assert zr == zg
+        assert not np.array_equal(got, base)
+
+
 @pytest.mark.parametrize("mode,baryon", [(3, 0), (4, 0), (5, 0), (3, 1), (5, 1)])
 def test_modified_table_lanes(mode, baryon):
     """k_spectra's modified-path table lanes (variant 4: mod_quad_tab_t in exp-table units -- e^(-E_mod/T_mod)
