@@ -1012,7 +1012,8 @@ static SpectraPlan spectra_plan(const is3d_engine* e) {
                              (P.tb ? 2 * tile * qrows * (P.KJ + 1) + 1 : 0) +
                              (P.tb && mode == CE ? tb * 2 * tile * nphp : 0) +
                              // the per-lane RTA-CE launch's {TE, T2} table (kernels.h PDE)
-                             (IS3D_CE_PE && mode == CE && !P.tb && !P.mp && qrows && P.KJ % 4 == 0 ? tb * 2 * tile * nphp : 0) +
+                             // (+ 1: s_pe starts at the 16-byte-aligned end of the y-term rows)
+                             (IS3D_CE_PE && mode == CE && !P.tb && !P.mp && qrows && P.KJ % 4 == 0 ? tb * 2 * tile * nphp + 1 : 0) +
                              (mode >= PTM && qrows ? tile * qrows * (P.KJ + 1) + 1 : 0));
   };
 #ifdef IS3D_FORCE_KJ
