@@ -148,7 +148,7 @@ constexpr int kTbQ = 4;
 #define IS3D_TAIL_PDL 1       // Boltzmann-tail lanes in the per-lane Grad / RTA-CE launches too (sep_quad_pd_tail_t)
 #endif
 #ifndef IS3D_CE_PE
-#define IS3D_CE_PE 0          // RTA-CE per-lane launch: E and the linear delta-f part from a {TE, T2} table (sep_quad_pde_t)
+#define IS3D_CE_PE 1          // RTA-CE per-lane launch: E and the linear delta-f part from a {TE, T2} table (sep_quad_pde_t)
 #endif
 #ifndef IS3D_TAIL_DNDX
 #define IS3D_TAIL_DNDX 1      // operation 0 (k_dndx): Boltzmann-tail Grad lanes in pairs (sep_pair_tail_t)
