@@ -135,7 +135,8 @@ int is3d_set_species(is3d_engine *e, int n, const double *mass, const double *si
  * reduction writes every member (prefactor x its degeneracy x the shared cell sum): the spectra are
  * bit-identical to integrating each species separately (on = 0) when both take the same launch plan (at the
  * BASELINE sizes), otherwise equal to rounding (the class count can change the cell-split grouping).
- * is3d_species_integrated returns the number of species the kernels integrate (SMASH 444 -> 193). */
+ * is3d_species_integrated returns the number of species the kernels integrate (SMASH 444 -> 193), or minus an
+ * IS3D_ERR_* code when the tables cannot be finalised (is3d_last_error says why). */
 int is3d_set_species_classes(is3d_engine *e, int on);
 int is3d_species_integrated(is3d_engine *e);
 int is3d_set_pdg(is3d_engine *e, int n, const double *mass, const double *sign,

@@ -201,17 +201,7 @@ static constexpr double kInvLn2x256 = 369.3299304675746;   // 256 / ln2
 #ifndef IS3D_EXP_TAB_BITS
 #define IS3D_EXP_TAB_BITS 8
 #endif
-#if IS3D_EXP_TAB_BITS == 10
-// 1024-entry table (8 KB of LDS), |c rs| <= ln2/2048, degree-3 Taylor (truncation 5.5e-16, ~2.5 ulp):
-// one FMA fewer per exp than the 256-entry table
-}  // namespace is3d
-#include "exp2_tab1024.h"
-namespace is3d {
-static constexpr int kExpTabN = 1024, kExpTabDeg = 3;
-#define kExp2Tab kExp2Tab1024
-#define kExpTabCoefs kExpTabA1024
-static constexpr double kInvLn2xN = kInvLn2x1024;
-#elif IS3D_EXP_TAB_BITS == 8
+#if IS3D_EXP_TAB_BITS == 8
 static constexpr int kExpTabN = 256, kExpTabDeg = 4;
 #define kExp2Tab kExp2Tab256
 #define kExpTabCoefs kExpTabA256
@@ -1208,6 +1198,18 @@ IS3D_HD void sep_setup(int flavor, const double* R, const double* Y, double mT, 
 
 IS3D_HD double lin(double c0, double cc, double cs, dbl2 p) { return fma(cc, p.x, fma(cs, p.y, c0)); }
 
+// fma(a, b, c) with c wave-uniform in an SGPR (an F_TS table operand, kernels.h): one VOP3 v_fma_f64.  Left to
+// the compiler, fma(vgpr, vgpr, sgpr) became v_fmac_f64 on a VGPR copy of c -- two v_mov_b32 per point
+IS3D_HD double fma_vvs(double a, double b, double c) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  double r;
+  asm("v_fma_f64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(c));
+  return r;
+#else
+  return fma(a, b, c);
+#endif
+}
+
 // Slow-path tail (per-point exp, unscaled coefficients): returns w * p.dsigma * f_eq (1 + delta-f)
 // (0 when outflow-cut), with 1 - sign f_eq and 1/E formed as in the reference.
 template <int FL, bool REG, bool OUT>
@@ -1497,7 +1499,8 @@ IS3D_HD void sep_quad_pde_t(const SepLane& L, const dbl2* c, const dbl2* b, cons
 // RTA-CE (SEP_CE) in the same launch also takes, per (cell, phi), pe = {TE, T2} with
 // TE = -(u^x pc + u^y ps) and T2 = LC pc + LS ps (cell-only lane coefficients, sep_cell_consts):
 //   E = E0 + TE,  a (L0 + Lc pc + Ls ps) = fma(a, T2, L0')   -- five ops per point instead of eight.
-template <int FL, bool REG, bool OUT>
+// SPHI: Phi (b[i].y) is an SGPR operand (F_TS), fma_vvs
+template <int FL, bool REG, bool OUT, bool SPHI = false>
 IS3D_HD void sep_quad_tb_t(const SepLane& L, double mT, const dbl2* b, const dbl2* pt, const dbl2* pe, double* v) {
   constexpr bool needE = FL == SEP_CE;
   double pb[4], q[4], E[4];
@@ -1514,7 +1517,7 @@ IS3D_HD void sep_quad_tb_t(const SepLane& L, double mT, const dbl2* b, const dbl
   const double rq[4] = {r01 * q[1], r01 * q[0], r23 * q[3], r23 * q[2]};
 #pragma unroll
   for (int i = 0; i < 4; i++) {
-    double in = fma(L.a, fma(mT, pt[i].y, b[i].y), L.S0);
+    double in = fma(L.a, SPHI ? fma_vvs(mT, pt[i].y, b[i].y) : fma(mT, pt[i].y, b[i].y), L.S0);
     if (needE) in = fma(E[i], fma(L.a, pe[i].y, L.L0), in);
     double t;
     if (REG) t = 1.0 + fmax(-1.0, fmin(rq[i] * in, 1.0));
@@ -1529,7 +1532,7 @@ IS3D_HD void sep_quad_tb_t(const SepLane& L, double mT, const dbl2* b, const dbl
 //   Grad    acc += pb (1 + S),            S = S0 + mT T1 + Phi                     5 ops per point
 //   RTA-CE  acc += pb (1 + L + S / E),    L = L0 + T2, E = E0 + TE, one 1/E per four points
 // (pb = w p.dsigma f_eq; regulate clamps delta-f to [-1, 1]; outflow drops points with pb <= 0).
-template <int FL, bool REG, bool OUT>
+template <int FL, bool REG, bool OUT, bool SPHI = false>
 IS3D_HD void sep_quad_tb_tail_t(const SepLane& L, double mT, const dbl2* b, const dbl2* pt, const dbl2* pe, double* acc) {
   constexpr bool needE = FL == SEP_CE;
   double rE[4] = {0.0, 0.0, 0.0, 0.0};
@@ -1546,7 +1549,7 @@ IS3D_HD void sep_quad_tb_tail_t(const SepLane& L, double mT, const dbl2* b, cons
   for (int i = 0; i < 4; i++) {
     double pb = fma(L.D0, b[i].x, L.escw * pt[i].x);
     if (OUT) pb = (pb <= 0.0) ? 0.0 : pb;
-    const double P = fma(mT, pt[i].y, b[i].y);
+    const double P = SPHI ? fma_vvs(mT, pt[i].y, b[i].y) : fma(mT, pt[i].y, b[i].y);
     double t;
     if (REG) {
       const double S = P + L.S0;

@@ -717,6 +717,12 @@ struct is3d_engine {
   long rec_cap = 0, aux_cap = 0, sol_cap = 0, renorm_cap = 0, slab_cap = 0, out_cap = 0;
   int* d_fb = nullptr;        // modified modes: [0] fallback cell count, [1..] k_fbscan's cell list
   long fb_cap = 0;
+  double* d_phtab = nullptr;  // F_TS launches: k_phitab's per-(cell, pT, phi) rows of one chunk of cells
+  long phtab_cap = 0;
+  double* d_phtab2 = nullptr; // ... and of the next chunk, integrated on the side stream meanwhile
+  long phtab2_cap = 0;
+  hipStream_t side = nullptr; // F_TS chunks alternate between the launch stream and this one
+  hipEvent_t fork = nullptr, join = nullptr;
   // operation 0
   double *d_ycell = nullptr, *d_part = nullptr; long ycell_cap = 0, part_cap = 0;
   int *d_keys = nullptr, *d_perm = nullptr; long keys_cap = 0, perm_cap = 0;
@@ -776,7 +782,10 @@ extern "C" void is3d_destroy(is3d_engine* e) {
   if (e->surf_owned) dfree(e->d_surf);
   dfree(e->d_chain);
   dfree(e->d_rec); dfree(e->d_aux); dfree(e->d_sol); dfree(e->d_renorm); dfree(e->d_slab); dfree(e->d_out);
-  dfree(e->d_fb);
+  dfree(e->d_fb); dfree(e->d_phtab); dfree(e->d_phtab2);
+  if (e->side) (void)hipStreamDestroy(e->side);
+  if (e->fork) (void)hipEventDestroy(e->fork);
+  if (e->join) (void)hipEventDestroy(e->join);
   dfree(e->d_ycell); dfree(e->d_part); dfree(e->d_keys); dfree(e->d_perm); dfree(e->d_offs);
   dfree(e->d_err); dfree(e->d_cnt);
   for (auto& v : e->ev) if (v) (void)hipEventDestroy(v);
@@ -800,7 +809,7 @@ extern "C" is3d_engine* is3d_create_devices(int n, const int* devices) {
 
 extern "C" int is3d_set_cell_window(is3d_engine* e, long lo, long hi) {
   if (!e) return IS3D_ERR_ARG;
-  if (e->grp) return e->fail(IS3D_ERR_UNSUPPORTED, "a device-list engine places its own windows");
+  if (e->grp) return is3d::group_fail(e->grp, IS3D_ERR_UNSUPPORTED, "a device-list engine places its own windows");
   if (lo < 0 || hi < 0) { e->win_lo = e->win_hi = -1; return IS3D_OK; }
   if (lo > hi || hi > e->ncell) return e->fail(IS3D_ERR_ARG, "cell window outside the surface");
   e->win_lo = lo; e->win_hi = hi;
@@ -851,9 +860,9 @@ extern "C" int is3d_set_species_classes(is3d_engine* e, int on) {
 
 extern "C" int is3d_species_integrated(is3d_engine* e) {
   if (e && e->grp) return is3d::group_species_integrated(e->grp);
-  if (!e) return IS3D_ERR_ARG;
+  if (!e) return -IS3D_ERR_ARG;
   const int rc = finalize_tables(e);
-  return rc ? rc : e->ncls;
+  return rc ? -rc : e->ncls;       // an error as minus its IS3D_ERR_* code (a count is >= 1)
 }
 
 extern "C" int is3d_set_pdg(is3d_engine* e, int n, const double* mass, const double* sign, const double* degeneracy,
@@ -973,6 +982,7 @@ static int device_jonah_table(is3d_engine* e, const double* r2, const double* w2
 // pT sin} table finalize_tables builds for KJ-padded phi rows)
 struct SpectraPlan {
   int KJ, njb, nq, nqmax, tb, ly, t8, tile;
+  int ts;                     // F_TS: the F_TB launch with the per-(cell, phi) operands from k_phitab's table
   int mp, npw;                // F_MP: pT values per workgroup (1 otherwise)
   size_t shmem;
   size_t shmem_fb;            // modified modes: the F_FB launch (8-cell tiles, per-lane y-term rows, no q tables)
@@ -1000,8 +1010,16 @@ static SpectraPlan spectra_plan(const is3d_engine* e) {
   };
   int kTile = (mode >= PTM) ? IS3D_KTILE_MOD : is3d::kern::kTile;   // spectra_tile<MODE, FLAGS>()
   // k_spectra's LDS layout (kernels.h): record tiles x kRecBufs, per-tile tables x kTabBufs
+  // F_TS (kernels.h TS): an F_TB launch with one phi block of 24 or 32 points
+  auto ts_ok = [&]() { return IS3D_TS && P.tb && P.njb == 1 && (P.KJ == 24 || P.KJ == 32); };
   auto lds_bytes = [&](int qrows) {     // qrows = 0: F_LY layout (one y-term row per lane)
     const size_t nphp = (size_t)P.njb * P.KJ, tile = (size_t)kTile;
+    if (ts_ok()) {
+      // records x 3, trig + {pc, ps}, grid, y-term rows x 2, exp table, T1 rows [tile][qrows][KJ + 2] (+ 1: alignment)
+      return sizeof(double) * (3 * tile * NREC + 4 * nphp + (size_t)(nk + 2 * nl) +
+                               2 * tile * std::min(qrows, P.nq) * kYRow + kExpTabN + tile * qrows * (P.KJ + 2) + 1 +
+                               (IS3D_TS_PF ? 128 : 0));
+    }
     // pipelined launches (F_TB, the modified path's 16-cell tiles): 3 record tiles, 2 table buffers
     const bool pipe = IS3D_PIPE && (P.tb || (mode >= PTM && qrows && !P.t8 && !P.ly));
     const size_t rb = pipe ? 3 : 2, tb = pipe ? 2 : 1, qvf = (mode >= PTM || !pipe) ? 2 : 1;
@@ -1076,6 +1094,7 @@ static SpectraPlan spectra_plan(const is3d_engine* e) {
     }
   }
   P.tile = kTile;
+  P.ts = ts_ok() ? F_TS : 0;
   if (mode >= PTM) {
     const int t = kTile, ly = P.ly, tb = P.tb, t8 = P.t8;
     kTile = is3d::kern::kTile;
@@ -1528,15 +1547,60 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   sa.npw = P.npw;
   sa.regulate = e->p.regulate_deltaf; sa.outflow = e->p.outflow; sa.dim = dim; sa.op = 1;
   const size_t shmem = P.shmem;
-  const int tb = P.tb | P.ly | P.t8 | P.mp;
-  const dim3 grid((unsigned)(wgs * nsplit));
+  const int tb = P.tb | P.ly | P.t8 | P.mp | P.ts;
   const int kflags = (e->p.regulate_deltaf ? F_REG : 0) | (e->p.outflow ? F_OUT : 0) | tb;
-  switch (mode) {
-    case GRAD: launch_spectra<GRAD>(grid, shmem, st, sa, kflags, KJ); break;
-    case CE: launch_spectra<CE>(grid, shmem, st, sa, kflags, KJ); break;
-    case PTM: launch_spectra<PTM>(grid, shmem, st, sa, kflags, KJ); break;
-    case PTB: launch_spectra<PTB>(grid, shmem, st, sa, kflags, KJ); break;
-    default: launch_spectra<PTMA>(grid, shmem, st, sa, kflags, KJ); break;
+  if (P.ts) {
+    // F_TS: k_phitab writes the per-(cell, pT, phi) rows of a chunk of whole cell splits (at most
+    // IS3D_PHITAB_BYTES), then k_spectra integrates that chunk's splits; one chunk at config 2 (3.7 GB).  Several
+    // chunks (config 4: 61 GB of rows) alternate between the launch stream and a side stream with a table buffer
+    // each, so the next chunk's k_phitab and the first workgroups of its k_spectra fill the CUs the previous
+    // launch's last workgroups leave idle (config 4: 11 chunks ran 2811 ms back to back, one 61 GB chunk 2739 ms)
+    const long rw = phitab_row(mode, KJ);
+    const long per_split = cps * (long)npT * rw;
+    const long spc = std::max(1L, std::min(nsplit, (long)(IS3D_PHITAB_BYTES / 8) / per_split));
+    const long phn = spc * cps, nchunk = (nsplit + spc - 1) / spc;
+    if (!ensure(e->d_phtab, e->phtab_cap, phn * npT * rw)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(phi tables) failed");
+    if (nchunk > 1) {
+      if (!ensure(e->d_phtab2, e->phtab2_cap, phn * npT * rw)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(phi tables) failed");
+      if (!e->side) HIPCHK(e, hipStreamCreateWithFlags(&e->side, hipStreamNonBlocking));
+      if (!e->fork) HIPCHK(e, hipEventCreateWithFlags(&e->fork, hipEventDisableTiming));
+      if (!e->join) HIPCHK(e, hipEventCreateWithFlags(&e->join, hipEventDisableTiming));
+      HIPCHK(e, hipEventRecord(e->fork, st));
+      HIPCHK(e, hipStreamWaitEvent(e->side, e->fork, 0));
+    }
+    for (long ic = 0; ic < nchunk; ic++) {
+      const long s0 = ic * spc, ns = std::min(spc, nsplit - s0);
+      const long c0 = s0 * cps, ncc = std::min(nw, (s0 + ns) * cps) - c0;
+      hipStream_t cs = (ic & 1) ? e->side : st;
+      double* tab = (ic & 1) ? e->d_phtab2 : e->d_phtab;
+      PhiTabArgs ta{};
+      ta.rec = rec_w; ta.c0 = c0; ta.nc = ncc; ta.pT = e->d_pT; ta.cphi = e->d_cphi; ta.sphi = e->d_sphi;
+      ta.npT = npT; ta.nphi = nphi; ta.nphp = KJ; ta.tab = tab; ta.phn = phn;
+      SpecArgs sc = sa;
+      sc.split0 = (int)s0; sc.nsplit = (int)ns; sc.phtab = tab; sc.phn = phn; sc.phc0 = c0; sc.phrow = (int)rw;
+      const dim3 grid((unsigned)(wgs * ns));
+      if (mode == GRAD) {
+        launch_phitab<GRAD>(cs, ta);
+        launch_spectra<GRAD>(grid, shmem, cs, sc, kflags, KJ);
+      } else {
+        launch_phitab<CE>(cs, ta);
+        launch_spectra<CE>(grid, shmem, cs, sc, kflags, KJ);
+      }
+      HIPCHK(e, hipGetLastError());
+    }
+    if (nchunk > 1) {
+      HIPCHK(e, hipEventRecord(e->join, e->side));
+      HIPCHK(e, hipStreamWaitEvent(st, e->join, 0));
+    }
+  } else {
+    const dim3 grid((unsigned)(wgs * nsplit));
+    switch (mode) {
+      case GRAD: launch_spectra<GRAD>(grid, shmem, st, sa, kflags, KJ); break;
+      case CE: launch_spectra<CE>(grid, shmem, st, sa, kflags, KJ); break;
+      case PTM: launch_spectra<PTM>(grid, shmem, st, sa, kflags, KJ); break;
+      case PTB: launch_spectra<PTB>(grid, shmem, st, sa, kflags, KJ); break;
+      default: launch_spectra<PTMA>(grid, shmem, st, sa, kflags, KJ); break;
+    }
   }
   HIPCHK(e, hipGetLastError());
   if (mode >= PTM) {

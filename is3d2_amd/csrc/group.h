@@ -23,6 +23,8 @@ int group_set_params(Group* g, const is3d_params* p);
 int group_set_species(Group* g, int n, const double* mass, const double* sign, const double* degen, const double* baryon);
 int group_set_species_classes(Group* g, int on);
 int group_species_integrated(Group* g);
+// record an error on the group (is3d_last_error of a device-list engine reads the group's message)
+int group_fail(Group* g, int code, const char* msg);
 int group_set_pdg(Group* g, int n, const double* mass, const double* sign, const double* degen, const double* baryon);
 int group_set_momentum_grid(Group* g, int npT, const double* pT, int nphi, const double* phi, int ny, const double* y,
                             int neta, const double* eta, const double* eta_w);

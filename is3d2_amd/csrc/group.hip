@@ -63,6 +63,11 @@ struct Group {
 };
 
 static bool needs_full(const Group* g) { return g->have_params && g->p.df_mode == 5 && g->p.famod_chains > 0; }
+// the surface was split for other params (PTMA warm-start chains on / off since is3d_set_surface): the windows
+// and what each shard holds no longer match what the params need
+static bool stale_split(const Group* g) { return g->sh.size() > 1 && g->ncell > 0 && g->full != needs_full(g); }
+static const char* kStaleSplit = "the params changed whether every device needs the whole surface (PTMA warm-start "
+                                 "chains): set the surface again";
 
 Group* group_create(int n, const int* devices, std::string& err) {
   if (n <= 0 || !devices) { err = "empty device list"; return nullptr; }
@@ -167,7 +172,11 @@ int group_set_species(Group* g, int n, const double* m, const double* s, const d
 int group_set_species_classes(Group* g, int on) {
   return each(g, [&](is3d_engine* e) { return is3d_set_species_classes(e, on); });
 }
-int group_species_integrated(Group* g) { return is3d_species_integrated(g->sh[0]); }
+int group_species_integrated(Group* g) {
+  const int n = is3d_species_integrated(g->sh[0]);
+  return n < 0 ? -g->shard_fail(0, -n) : n;
+}
+int group_fail(Group* g, int code, const char* msg) { return g->fail(code, msg); }
 int group_set_pdg(Group* g, int n, const double* m, const double* s, const double* d, const double* b) {
   return each(g, [&](is3d_engine* e) { return is3d_set_pdg(e, n, m, s, d, b); });
 }
@@ -266,9 +275,7 @@ long group_output_size(const Group* g) { return g->sh.empty() ? -1 : is3d_output
 
 int group_launch(Group* g, double* dev_out, void* stream) {
   if (!dev_out) return g->fail(IS3D_ERR_ARG, "null output buffer");
-  if (needs_full(g) && !g->full && g->sh.size() > 1)
-    return g->fail(IS3D_ERR_STATE, "PTMA warm-start chains need the whole surface on every device: set the params "
-                                   "(famod_chains > 0) before the surface");
+  if (stale_split(g)) return g->fail(IS3D_ERR_STATE, kStaleSplit);
   const int K = (int)g->sh.size();
   const long out_n = group_output_size(g);
   if (out_n <= 0) return g->fail(IS3D_ERR_STATE, "species / grids / params not set");
@@ -395,6 +402,7 @@ int group_calculate_dN_dX(Group* g, double* tau, double* r, double* phi) {
   const int K = (int)g->sh.size();
   if (K > 1 && g->bins.threads > 0)
     return g->fail(IS3D_ERR_UNSUPPORTED, "spacetime threads > 0 (the reference's thread-slice carry) runs on one device");
+  if (stale_split(g)) return g->fail(IS3D_ERR_STATE, kStaleSplit);
   if (g->full && K > 1)
     return g->fail(IS3D_ERR_UNSUPPORTED, "calculate_spectra error: no spacetime distribution routine for famod yet");
   const long nt = (long)g->np * g->bins.tau_bins, nr = (long)g->np * g->bins.r_bins, nph = (long)g->np * g->bins.phip_bins;
@@ -450,6 +458,7 @@ int group_evaluate_df_coefficients(Group* g, double T, double muB, double E, dou
 
 int group_total_yield(Group* g, const double* plasma, double y_cut, double* n_total, double* densities) {
   if (!plasma || !n_total) return g->fail(IS3D_ERR_ARG, "null argument");
+  if (stale_split(g)) return g->fail(IS3D_ERR_STATE, kStaleSplit);
   const int K = (int)g->sh.size();
   std::vector<double> nt(K, 0.0);
   const int rc = each_parallel(g, [&](int k) -> int {

@@ -84,6 +84,9 @@ struct SpecArgs {
   int op;                     // 1 spectra / 0 spacetime (yterms variants)
   const int* fbcells;         // F_FB launch: ascending indices of the cells with separable-fallback lanes
   const int* fbcount;         //   (k_fbscan, device-side) and their number
+  int split0;                 // first cell split of this launch (F_TS launches cover the splits chunk by chunk)
+  // F_TS: the per-(cell, pT, phi) tables k_phitab wrote for this chunk of cells, rows [pT][cell - phc0][phrow]
+  const double* phtab; long phn, phc0; int phrow;
 };
 
 // flag bits of the spectra kernel instantiation
@@ -100,8 +103,21 @@ struct SpecArgs {
 // phi row (one block of KJ >= nphi) and a workgroup holds npw = 256 / (np nq) pT values, whose {b', Phi} /
 // PD / {pc, ps} tables it builds side by side; the lane setup is amortised over every phi point instead of
 // an 8-point block
-constexpr int F_REG = 1, F_OUT = 2, F_TB = 4, F_LY = 8, F_T8 = 16, F_FB = 32, F_MP = 64;
+// F_TS (with F_TB, one phi block): the wave-uniform per-(cell, phi) operands {b', Phi}, PD (and RTA-CE's {TE, T2})
+// come by scalar loads from a per-(cell, pT) global table that k_phitab writes before the launch, straight into
+// SGPRs, instead of broadcast ds_read_b128s from LDS tables the workgroup builds; LDS keeps only the per-(cell, q
+// row, phi) T1 rows (one ds_read_b128 per two points).  The F_TB tail loop read two ds_read_b128 (8 LDS-array
+// cycles) per 5 VALU ops, so four SIMDs in it were bound by the CU's LDS array, not by the FP64 pipe
+constexpr int F_REG = 1, F_OUT = 2, F_TB = 4, F_LY = 8, F_T8 = 16, F_FB = 32, F_MP = 64, F_TS = 128;
 constexpr int kTbQ = 4;
+// doubles per F_TS table row of one (cell, pT): {b', Phi}[nphp] | PD[nphp] | RTA-CE {TE, T2}[nphp]
+__host__ __device__ constexpr int phitab_row(int mode, int nphp) { return (mode == CE ? 5 : 3) * nphp; }
+#ifndef IS3D_TS
+#define IS3D_TS 1             // F_TB launches with one phi block take the scalar-table form (F_TS)
+#endif
+#ifndef IS3D_PHITAB_BYTES
+#define IS3D_PHITAB_BYTES (6L << 30)   // F_TS table budget: larger surfaces run chunk by chunk (whole cell splits)
+#endif
 
 #ifndef IS3D_SPLIT_BYTES
 #define IS3D_SPLIT_BYTES (512L << 10) // record bytes per cell split (k_spectra grid sizing): 0.5 MB (2 MB before round 3:
@@ -153,6 +169,9 @@ constexpr int kTbQ = 4;
 #ifndef IS3D_TAIL_DNDX
 #define IS3D_TAIL_DNDX 1      // operation 0 (k_dndx): Boltzmann-tail Grad lanes in pairs (sep_pair_tail_t)
 #endif
+#ifndef IS3D_TS_PF
+#define IS3D_TS_PF 1          // F_TS: the table rows of tile i + 2 are touched into L2 (LDS-DMA of one dword per 128 B)
+#endif
 #ifndef IS3D_TAIL_PD
 #define IS3D_TAIL_PD 0        // Grad tail lanes: PD table + scalar {pc, ps} instead of {PD, T1}: 2.2% slower (r2d A/B)
 #endif
@@ -188,10 +207,20 @@ struct DndxArgs {
   int dim;
 };
 
+// k_phitab: the F_TS tables of one chunk of cells (every pT), rows [pT][cell - c0][phitab_row]
+struct PhiTabArgs {
+  const double* rec; long c0, nc;           // records of the launch window, first cell and cells of the chunk
+  const double *pT, *cphi, *sphi;
+  int npT, nphi, nphp;
+  double* tab; long phn;                    // rows per pT plane (>= nc)
+};
+
 template <int MODE>
 void launch_spectra(dim3 grid, size_t shmem, hipStream_t st, const SpecArgs& a, int flags, int kj);
 template <int MODE>
 void launch_dndx(dim3 grid, size_t shmem, hipStream_t st, const DndxArgs& a, int flags, int kj);
+template <int MODE>
+void launch_phitab(hipStream_t st, const PhiTabArgs& a);
 
 // phi blocks launch_spectra has an instantiation for (the host plan must pick one of these)
 __host__ __device__ constexpr bool spectra_kj_supported(int kj) {
@@ -372,6 +401,36 @@ __device__ __forceinline__ void sep_phi_loop_tb_tail(const SepLane& L, double mT
   }
 }
 
+// F_TS lanes: the F_TB fours (sep_quad_tb_t / sep_quad_tb_tail_t, the same arithmetic) with {b', Phi}, PD and
+// RTA-CE's {TE, T2} by scalar loads from the cell's k_phitab row G (wave-uniform address: SGPR operands) and T1
+// from the lane's LDS row (16-byte aligned pairs: one ds_read_b128 per two points)
+template <int MODE, int FLAGS, int KJ, bool TAIL>
+__device__ __forceinline__ void sep_phi_loop_ts(const SepLane& L, double mT, cs_sptr G, const dbl2* T1, double* acc) {
+  constexpr int FL = (MODE == GRAD) ? SEP_GRAD : SEP_CE;
+  constexpr bool REG = (FLAGS & F_REG) != 0, OUT = (FLAGS & F_OUT) != 0;
+  static_assert(KJ % 4 == 0, "F_TS needs phi blocks of fours");
+#pragma unroll
+  for (int jj = 0; jj < KJ; jj += 4) {
+    dbl2 b[4], pt[4], pe[4];
+    const dbl2 t01 = T1[jj >> 1], t23 = T1[(jj >> 1) + 1];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      b[i].x = G[2 * (jj + i)]; b[i].y = G[2 * (jj + i) + 1];
+      pt[i].x = G[2 * KJ + jj + i];
+      if (FL == SEP_CE) { pe[i].x = G[3 * KJ + 2 * (jj + i)]; pe[i].y = G[3 * KJ + 2 * (jj + i) + 1]; }
+    }
+    pt[0].y = t01.x; pt[1].y = t01.y; pt[2].y = t23.x; pt[3].y = t23.y;
+    if (TAIL) {
+      sep_quad_tb_tail_t<FL, REG, OUT, true>(L, mT, b, pt, pe, acc + jj);
+    } else {
+      double v[4];
+      sep_quad_tb_t<FL, REG, OUT, true>(L, mT, b, pt, pe, v);
+#pragma unroll
+      for (int i = 0; i < 4; i++) acc[jj + i] += v[i];
+    }
+  }
+}
+
 // Boltzmann-tail Grad lanes of an F_TB launch, PD-table form: {b', Phi} and PD from LDS, {pc, ps} by scalar
 // loads (sep_quad_pd_tail_t; 6 LDS-array cycles per point instead of 8)
 template <int MODE, int FLAGS, int KJ, typename CSP>
@@ -530,6 +589,8 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
   extern __shared__ double smem[];
   const int nphp = A.njb * KJ;                            // phi rows padded to KJ multiples
   constexpr bool TB = (MODE == GRAD || MODE == CE) && (FLAGS & F_TB) != 0 && KJ % 4 == 0;
+  // F_TS: per-(cell, phi) operands from the k_phitab rows by scalar loads; LDS holds the T1 rows only
+  constexpr bool TS = TB && (FLAGS & F_TS) != 0;
   constexpr bool FB = MODE >= PTM && (FLAGS & F_FB) != 0;   // separable-fallback launch of a modified mode
   constexpr bool MODMAIN = MODE >= PTM && !FB;              // modified launch: separable lanes left to F_FB
   constexpr bool LY = (FLAGS & F_LY) != 0 || FB;
@@ -550,7 +611,7 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
   constexpr int kRecBufs = PIPE ? 3 : 2, kTabBufs = PIPE ? 2 : 1;
   constexpr int kQvF = (MODE >= PTM || !PIPE) ? 2 : 1;    // doubles per (cell, phi) of s_qv
   const int nqm = A.nqmax;                                // rows per cell (>= every workgroup's nqw)
-  const long recsz = (long)kTile * NREC, bpsz = (long)npw * kTile * nphp, qvsz = kQvF * bpsz;
+  const long recsz = (long)kTile * NREC, bpsz = TS ? 0L : (long)npw * kTile * nphp, qvsz = kQvF * bpsz;
   // y-term rows per cell: per row, or per q once the rows cover every q (nyr below): min(nqm, nq);
   // LY launches: one y-term row per lane instead ([kBlock][kYRowLY], single; odd row stride: no conflicts)
   const long ysz = LY ? (long)kBlock * kYRowLY : (long)kTile * min(nqm, A.nq) * kYRow;
@@ -572,8 +633,12 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
   // at the same phi by the two halves of a wavefront that straddles a row boundary land in different
   // banks (a 512-B row stride is 128 dwords: the same bank, a 2-way conflict in every straddling wave)
   constexpr int prow = KJ + 1;
-  dbl2* s_pe = s_pt + (TB ? kTile * nqm * prow : 0);     // TB / PDE, RTA-CE: [kTabBufs][kTile][nphp] {TE, T2}
+  dbl2* s_pe = s_pt + (TB && !TS ? kTile * nqm * prow : 0);   // TB / PDE, RTA-CE: [kTabBufs][kTile][nphp] {TE, T2}
   double* s_mt = (double*)s_pt;                           // modified path: [kTile][nqm][prow] T2 = 2 U_q . W
+  // F_TS: [kTile][nqm][prow2] T1 rows; an even stride keeps every row 16-byte aligned for the ds_read_b128 pairs,
+  // and 2 (KJ + 2) dwords put the same phi of two rows of a straddling wavefront 4 banks apart
+  constexpr int prow2 = KJ + 2;
+  double* s_t1 = (double*)s_pt;
 
   const int tid = threadIdx.x;
   for (int i = tid; i < kExpTabN; i += kBlock) s_etab[i] = kExp2Tab[i];
@@ -588,7 +653,7 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
   const long lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
   const int lane_group = (int)(lid % A.nbx);
   const int pg = (int)((lid / A.nbx) % npg);
-  const int split = (int)(lid / ((long)A.nbx * npg));
+  const int split = A.split0 + (int)(lid / ((long)A.nbx * npg));
   const int lp = MP ? tid / (int)A.ntask : 0;
   const int ipt = MP ? min(pg * npw + lp, A.npT - 1) : pg;
   const double pT = A.pT[ipt];
@@ -673,7 +738,7 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
     dbl2* pe = s_pe + tb * bpsz;
     double* yb = s_y + tb * ysz;
     // F_MP: npw pT blocks of [kTile][nphp]; o = the entry's offset in its block, csj = its {pc, ps}
-    for (int idx = tid; idx < npw * ntx * nphp; idx += kBlock) {
+    for (int idx = tid; idx < (TS ? 0 : npw * ntx * nphp); idx += kBlock) {
       const int l2 = MP ? idx / (ntx * nphp) : 0, ix = MP ? idx % (ntx * nphp) : idx;
       const int t = ix / nphp, j = ix % nphp;
       const int o = (l2 * kTile + t) * nphp + j;
@@ -694,7 +759,7 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
       } else {
         qvt[o] = sep_pd(R, csj, v.x);                     // PD table (sep_pd)
       }
-      if constexpr ((TB || PDE) && MODE == CE) {
+      if constexpr ((TB || PDE) && MODE == CE && !TS) {
         const dbl2 c = s_cs[j];
         dbl2 e;
         e.x = -fma(R[R_UX], c.x, R[R_UY] * c.y);
@@ -728,7 +793,15 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
         s_mt[((long)t * nqw + qq) * prow + jj] = modt2(R, yb + ((long)t * nyr + yr) * kYRow, s_cs[j]);
       }
     }
-    if constexpr (TB) {
+    if constexpr (TS) {
+      // T1 = SC1 pc + SS1 ps per (cell, q row, phi) (one phi block: phi slot jj)
+      for (int idx = tid; idx < ntx * nqw * KJ; idx += kBlock) {
+        const int jj = idx % KJ, r = idx / KJ, qq = r % nqw, t = r / nqw;
+        const double* Y = yb + ((long)t * nyr + (allq ? (int)((r0 + qq) % A.nq) : qq)) * kYRow;
+        const dbl2 c = s_cs[jj];
+        s_t1[((long)t * nqw + qq) * prow2 + jj] = fma(Y[Y_SC1], c.x, Y[Y_SS1] * c.y);
+      }
+    } else if constexpr (TB) {
       // {PD, T1 = SC1 pc + SS1 ps} per (cell, q, phi) (rows of skipped cells are never read)
       for (int idx = tid; idx < ntx * nqw * KJ; idx += kBlock) {
         const int jj = idx % KJ, r = idx / KJ, qq = r % nqw, t = r / nqw;
@@ -768,8 +841,21 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
     const int ntx = tile_nt(i), tb = PIPE ? (i & 1) : 0;
     wait_fetch();
     lds_barrier();     // X: this tile's records (and, pipelined, its A / B tables) visible; the last tile is done
-    if (i + kRecBufs - 1 < ntiles)
+    if (i + kRecBufs - 1 < ntiles) {
       fetch_tile<kTile>(A.rec, tile_cb(i + kRecBufs - 1), c_end, recbuf(i + kRecBufs - 1), fbl);
+      if constexpr (TS && IS3D_TS_PF) {
+        // the k_phitab rows of that tile (contiguous: cells x RW doubles of this pT) into L2, so the scalar loads of
+        // its first points miss the K$ into L2 instead of HBM; one dword per 128-byte line, landing in a dummy LDS row
+        constexpr int RW = phitab_row(MODE, KJ);
+        const long cbp = tile_cb(i + kRecBufs - 1);
+        const long nb = (min(c_end, cbp + kTile) - cbp) * RW * 8;
+        const char* src = (const char*)(A.phtab + ((long)ipt * A.phn + (cbp - A.phc0)) * RW);
+        double* pfd = s_t1 + (long)kTile * nqm * prow2;
+        for (long off = (long)tid * 128; off < nb; off += (long)kBlock * 128)
+          __builtin_amdgcn_global_load_lds((const void*)(src + off),
+                                           (__attribute__((address_space(3))) void*)(pfd + 32 * (tid >> 6)), 4, 0, 0);
+      }
+    }
     if (!PIPE) {
       tables_ab(s_rec, ntx, 0);
       lds_barrier();
@@ -823,9 +909,17 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
           if ((IS3D_EARLY_SKIP & 1) && sep_skips(R, Y, mT, pT, baryon)) continue;
           SepLane L;
           sep_setup(sep_flavor(MODE), R, Y, mT, mT2, m2, mTb, pT, sign, baryon, s_etab, L,
-                    ((TB && IS3D_TAIL && (MODE == GRAD || IS3D_TAIL_CE)) || PDT) ? (IS3D_TAIL_WAVE ? 2 : 1) : 0);
+                    ((TB && IS3D_TAIL && (MODE == GRAD || IS3D_TAIL_CE || TS)) || PDT) ? (IS3D_TAIL_WAVE ? 2 : 1) : 0);
           if (L.skip) continue;
-          if constexpr (TB) {
+          if constexpr (TS) {
+            // this cell's k_phitab row (wave-uniform: ipt, the tile and t are) and the lane's T1 row
+            constexpr int RW = phitab_row(MODE, KJ);          // one phi block: nphp = KJ
+            const long go = ((long)ipt * A.phn + (cbx - A.phc0)) * RW + t * RW;
+            const dbl2* T1 = (const dbl2*)(s_t1 + ((long)t * nqw + row) * prow2);
+            if (IS3D_TAIL && L.tail) sep_phi_loop_ts<MODE, FLAGS, KJ, true>(L, mT, (cs_sptr)A.phtab + go, T1, acc);
+            else if (L.fast) sep_phi_loop_ts<MODE, FLAGS, KJ, false>(L, mT, (cs_sptr)A.phtab + go, T1, acc);
+            else sep_phi_loop<MODE, FLAGS, false, KJ>(L, CSl, (const dbl2*)(A.phtab + go), acc);
+          } else if constexpr (TB) {
             const dbl2* PT = s_pt + ((long)t * nqw + row) * prow;
             if (IS3D_TAIL && L.tail) {
               if (MODE == GRAD && IS3D_TAIL_PD)
@@ -1104,7 +1198,46 @@ __global__ __launch_bounds__(kBlock, dndx_waves<MODE>()) void k_dndx(DndxArgs A)
   }
 }
 
+// F_TS tables of one chunk of cells: per (pT, cell, phi slot) the values k_spectra's F_TB launch builds per tile
+// in LDS -- {b', Phi} (phiterms), PD (sep_pd) and RTA-CE's {TE, T2} -- by the same expressions, so the F_TS lanes
+// see the same operands.  One thread per entry, phi slot fastest (a cell's row is written by consecutive lanes);
+// padding slots and cells with u.dsigma <= 0 get zeros, as in the LDS tables.
+template <int MODE>
+__global__ __launch_bounds__(256) void k_phitab(PhiTabArgs A) {
+  __shared__ double s_etab[kExpTabN];
+  for (int i = threadIdx.x; i < kExpTabN; i += 256) s_etab[i] = kExp2Tab[i];
+  __syncthreads();
+  const int rw = phitab_row(MODE, A.nphp);
+  const long total = (long)A.npT * A.nc * A.nphp;
+  for (long idx = (long)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
+    const int j = (int)(idx % A.nphp);
+    const long r = idx / A.nphp, c = r % A.nc;
+    const int ipt = (int)(r / A.nc);
+    const double* R = A.rec + (A.c0 + c) * NREC;
+    double* row = A.tab + ((long)ipt * A.phn + c) * rw;
+    const bool in = j < A.nphi;
+    const double pT = A.pT[ipt], co = in ? A.cphi[j] : 0.0, sn = in ? A.sphi[j] : 0.0;
+    dbl2 cs; cs.x = pT * co; cs.y = pT * sn;
+    dbl2 v; v.x = 0.0; v.y = 0.0;
+    if (in && R[R_KIND] != 0.0) v = phiterms(MODE, R, pT, co, sn, s_etab);
+    row[2 * j] = v.x;
+    row[2 * j + 1] = v.y;
+    row[2 * A.nphp + j] = sep_pd(R, cs, v.x);
+    if constexpr (MODE == CE) {
+      row[3 * A.nphp + 2 * j] = -fma(R[R_UX], cs.x, R[R_UY] * cs.y);
+      row[3 * A.nphp + 2 * j + 1] = fma(R[R_LC], cs.x, R[R_LS] * cs.y);
+    }
+  }
+}
+
 }  // namespace
+
+template <int MODE>
+void launch_phitab(hipStream_t st, const PhiTabArgs& a) {
+  const long total = (long)a.npT * a.nc * a.nphp;
+  const long blocks = std::max(1L, std::min((total + 255) / 256, 256L * 32));
+  hipLaunchKernelGGL((k_phitab<MODE>), dim3((unsigned)blocks), dim3(256), 0, st, a);
+}
 
 template <int MODE, int KJ>
 void launch_spectra_kj(dim3 grid, size_t shmem, hipStream_t st, const SpecArgs& a, int flags) {
@@ -1146,6 +1279,17 @@ void launch_spectra_kj(dim3 grid, size_t shmem, hipStream_t st, const SpecArgs& 
         case 1: hipLaunchKernelGGL((k_spectra<MODE, 65, KJ>), grid, dim3(kBlock), shmem, st, a); break;
         case 2: hipLaunchKernelGGL((k_spectra<MODE, 66, KJ>), grid, dim3(kBlock), shmem, st, a); break;
         default: hipLaunchKernelGGL((k_spectra<MODE, 67, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+      }
+      return;
+    }
+  }
+  if constexpr ((MODE == GRAD || MODE == CE) && (KJ == 24 || KJ == 32)) {
+    if ((flags & F_TS) && (flags & F_TB)) {
+      switch (flags & 3) {
+        case 0: hipLaunchKernelGGL((k_spectra<MODE, 132, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+        case 1: hipLaunchKernelGGL((k_spectra<MODE, 133, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+        case 2: hipLaunchKernelGGL((k_spectra<MODE, 134, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+        default: hipLaunchKernelGGL((k_spectra<MODE, 135, KJ>), grid, dim3(kBlock), shmem, st, a); break;
       }
       return;
     }

@@ -16,6 +16,8 @@ template void launch_spectra<GRAD>(dim3, size_t, hipStream_t, const SpecArgs&, i
 template void launch_spectra<CE>(dim3, size_t, hipStream_t, const SpecArgs&, int, int);
 template void launch_dndx<GRAD>(dim3, size_t, hipStream_t, const DndxArgs&, int, int);
 template void launch_dndx<CE>(dim3, size_t, hipStream_t, const DndxArgs&, int, int);
+template void launch_phitab<GRAD>(hipStream_t, const PhiTabArgs&);
+template void launch_phitab<CE>(hipStream_t, const PhiTabArgs&);
 #elif IS3D_TU == 3 || IS3D_TU == 4
 template void launch_spectra<IS3D_TU>(dim3, size_t, hipStream_t, const SpecArgs&, int, int);
 template void launch_dndx<IS3D_TU>(dim3, size_t, hipStream_t, const DndxArgs&, int, int);

@@ -96,7 +96,7 @@ class Engine:
     def species_integrated(self):
         n = self.lib.is3d_species_integrated(self._e)
         if n < 0:
-            self._chk(n)
+            self._chk(-n)     # an error comes back as minus its IS3D_ERR_* code
         return n
 
     def set_pdg(self, mass, sign, degen, baryon):

@@ -15,8 +15,7 @@ EMU_LIB = os.path.join(HERE, "native", "libcf_emulator.so")
 def emulator():
     """Host build of the kernels' math (test-only), see tests/native/cf_emulator.cpp."""
     srcs = [EMU_SRC] + [os.path.join(HERE, "..", p) for p in (
-        "is3d2_amd/csrc/cf_math.h", "is3d2_amd/csrc/aniso_math.h", "is3d2_amd/csrc/spline_host.h",
-        "is3d2_amd/csrc/exp2_tab1024.h")]
+        "is3d2_amd/csrc/cf_math.h", "is3d2_amd/csrc/aniso_math.h", "is3d2_amd/csrc/spline_host.h")]
     if not os.path.exists(EMU_LIB) or any(os.path.getmtime(s) > os.path.getmtime(EMU_LIB) for s in srcs):
         subprocess.check_call(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-o", EMU_LIB, EMU_SRC])
     lib = C.CDLL(EMU_LIB)

@@ -135,3 +135,42 @@ def test_group_surface_from_device():
 def test_group_bad_device_list():
     with pytest.raises(Exception):
         Engine(devices=[0, 97])
+
+
+def test_group_stale_split_after_params_change():
+    """Surface split for PTMA warm-start chains (every shard holds the whole surface), then params without
+    chains: the launch refuses until the surface is set again (it would double-count cells otherwise), and
+    then matches one engine."""
+    s = synth.as_read(synth.surface(300, seed=103, dimension=2))
+    spec5 = make_spec(hrg_eos=2, chosen="pikp", df_mode=5, dimension=2, famod_chains=1)
+    spec1 = make_spec(hrg_eos=2, chosen="pikp", df_mode=1, dimension=2)
+    one, _ = spectra(spec1, s)
+    e = build_engine(spec5, s, devices=[0, 0])
+    e.set_params(**spec1["params"])
+    with pytest.raises(Exception, match="set the surface again"):
+        e.calculate_spectra()
+    e.set_surface(s)
+    got = e.calculate_spectra()
+    e.close()
+    assert parity(got, one)[0] < 1e-12
+
+
+def test_group_window_error_message():
+    e = Engine(devices=[0, 0])
+    with pytest.raises(Exception, match="places its own windows"):
+        e.set_cell_window(0, 1)
+    e.close()
+
+
+@pytest.mark.skipif(not __import__("torch").cuda.is_available() or __import__("torch").cuda.device_count() < 2,
+                    reason="needs two GPUs: the distinct-device RCCL all-reduce and peer-copy reduction")
+@pytest.mark.parametrize("reduce", ["rccl", "copy"])
+def test_group_distinct_devices(monkeypatch, reduce):
+    """devices = [0, 1]: ncclCommInitAll over distinct GPUs + grouped in-place ncclAllReduce (IS3D_REDUCE unset
+    or rccl), or hipMemcpyPeerAsync + fixed-order add (copy).  Skipped on a one-GPU box."""
+    monkeypatch.setenv("IS3D_REDUCE", reduce)
+    s = synth.as_read(synth.surface(400, seed=107, dimension=3, full3d=True))
+    spec = make_spec(hrg_eos=2, chosen="pikp", df_mode=2, dimension=3)
+    one, _ = spectra(spec, s)
+    grp, _ = spectra(spec, s, devices=[0, 1])
+    assert parity(grp, one)[0] < 1e-12
