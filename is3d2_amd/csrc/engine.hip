@@ -180,9 +180,17 @@ struct ChainArgs {
   double* sstart;        // [4][nseg] the start state of each segment's stored run
   int* changed;          // [kChainPasses] pass j changed some segment's end state
   long n, C, L, nspc;    // cells, chains, positions per segment, segments per chain
+  // positions [q0, q1) of every chain (cells [q0 C, q1 C)): the whole chain on one engine; a device group's shard
+  // solves its own range, starting each chain from the end state its predecessor shard pushes into bin
+  long q0, q1;
+  int has_pred;          // q0 > 0: chain position q0 - 1 lives on the previous shard
+  int npass;             // passes enqueued (<= kChainPasses)
+  double* bin;           // [3][4 C + 1] boundary in: end states of position q0 - 1 by pass parity, [2] = final + walk flag
+  double* bout;          // [3][4 C + 1] boundary out: this range's end states (position q1 - 1), same slots
   Hadrons h;
   double fp2;
 };
+constexpr int kBndSlots = 3;   // bin / bout slots: pass parity 0, 1 and the finisher's
 
 __device__ __forceinline__ bool state_eq(const double* a, const double* b) {
   bool eq = true;
@@ -196,8 +204,8 @@ __device__ __forceinline__ bool state_eq(const double* a, const double* b) {
 __device__ bool chain_segment_run(const ChainArgs& A, long seg, double* state, bool sync) {
   const int lane = threadIdx.x;
   const long c = seg / A.nspc, s = seg % A.nspc;
-  const long P = (A.n - c + A.C - 1) / A.C;                 // positions of chain c
-  const long p0 = s * A.L, p1 = min(P, p0 + A.L);
+  const long P = min((A.n - c + A.C - 1) / A.C, A.q1);      // positions of chain c in this range's end
+  const long p0 = A.q0 + s * A.L, p1 = min(P, p0 + A.L);
   for (long pos = p0; pos < p1; pos++) {
     const long cell = c + pos * A.C;
     if (A.rec[cell * NREC + R_KIND] == 0.0) continue;       // u.dsigma <= 0: not in the chain (:1146)
@@ -225,61 +233,87 @@ __device__ bool chain_segment_run(const ChainArgs& A, long seg, double* state, b
 
 __global__ __launch_bounds__(64) void k_chain_pass(ChainArgs A, int pass) {
   const long seg = blockIdx.x, nseg = A.C * A.nspc;
+  const long c = seg / A.nspc, s = seg % A.nspc;
   const int lane = threadIdx.x;
-  if (pass > 0 && A.changed[pass - 1] == 0) return;         // converged: the remaining passes are no-ops
+  const long bw = 4 * A.C + 1;
+  // converged: the remaining passes are no-ops (a shard with a predecessor always checks its starts: the boundary
+  // pushed in may still move)
+  if (pass > 0 && A.changed[pass - 1] == 0 && !A.has_pred) return;
   const double* prev = A.send + (long)((pass + 1) & 1) * 4 * nseg;
   double* cur = A.send + (long)(pass & 1) * 4 * nseg;
   double state[4] = {0.0, 0.0, 0.0, 0.0};                   // cold: no previous success in this chain
+  bool done = false;
   if (pass > 0) {
     double st0[4], used[4];
 #pragma unroll
     for (int f = 0; f < 4; f++) used[f] = A.sstart[f * nseg + seg];
-    if (seg % A.nspc == 0) {
+    if (s == 0) {
+      const double* b = A.bin + (long)((pass - 1) & 1) * bw;
 #pragma unroll
-      for (int f = 0; f < 4; f++) st0[f] = 0.0;
+      for (int f = 0; f < 4; f++) st0[f] = A.has_pred ? b[f * A.C + c] : 0.0;
     } else {
 #pragma unroll
       for (int f = 0; f < 4; f++) st0[f] = prev[f * nseg + seg - 1];
     }
     if (state_eq(st0, used)) {                              // same start: the stored run stands
       if (lane == 0) for (int f = 0; f < 4; f++) cur[f * nseg + seg] = prev[f * nseg + seg];
-      return;
-    }
-#pragma unroll
-    for (int f = 0; f < 4; f++) state[f] = st0[f];
-  }
-  if (lane == 0) for (int f = 0; f < 4; f++) A.sstart[f * nseg + seg] = state[f];
-  const bool synced = chain_segment_run(A, seg, state, pass > 0);
-  if (lane == 0) {
-    if (synced) {
-      for (int f = 0; f < 4; f++) cur[f * nseg + seg] = prev[f * nseg + seg];
+      done = true;
     } else {
-      bool moved = pass == 0;
-      for (int f = 0; f < 4; f++) {
-        moved = moved || __double_as_longlong(state[f]) != __double_as_longlong(prev[f * nseg + seg]);
-        cur[f * nseg + seg] = state[f];
-      }
-      if (moved && pass > 0) atomicOr(&A.changed[pass], 1);
+#pragma unroll
+      for (int f = 0; f < 4; f++) state[f] = st0[f];
     }
   }
-  if (pass == 0 && lane == 0 && A.nspc > 1) atomicOr(&A.changed[0], 1);
+  if (!done) {
+    if (lane == 0) for (int f = 0; f < 4; f++) A.sstart[f * nseg + seg] = state[f];
+    const bool synced = chain_segment_run(A, seg, state, pass > 0);
+    if (lane == 0) {
+      if (synced) {
+        for (int f = 0; f < 4; f++) cur[f * nseg + seg] = prev[f * nseg + seg];
+      } else {
+        bool moved = pass == 0;
+        for (int f = 0; f < 4; f++) {
+          moved = moved || __double_as_longlong(state[f]) != __double_as_longlong(prev[f * nseg + seg]);
+          cur[f * nseg + seg] = state[f];
+        }
+        if (moved && pass > 0) atomicOr(&A.changed[pass], 1);
+      }
+    }
+    if (pass == 0 && lane == 0 && A.nspc > 1) atomicOr(&A.changed[0], 1);
+  }
+  // the range's last segment of chain c: its end state is the next shard's boundary in
+  if (s == A.nspc - 1 && lane == 0) {
+    double* b = A.bout + (long)(pass & 1) * bw;
+    for (int f = 0; f < 4; f++) b[f * A.C + c] = cur[f * nseg + seg];
+  }
 }
 
-// Serial completion after kChainPasses passes (one wavefront; normally returns at once): segments in chain
-// order, each from its predecessor's current end state -- exact by induction.
+// Serial completion after the passes (one wavefront; normally returns at once): segments in chain order, each
+// from its predecessor's current end state -- exact by induction.  It walks when this range's last pass changed
+// something or the predecessor shard walked (bin[2] flag); either way it leaves the range's final end states and
+// its walk flag in bout[2] for the next shard.
 __global__ __launch_bounds__(64) void k_chain_finish(ChainArgs A) {
-  if (A.changed[kChainPasses - 1] == 0) return;
-  const long nseg = A.C * A.nspc;
-  double* cur = A.send + (long)((kChainPasses - 1) & 1) * 4 * nseg;
+  const long nseg = A.C * A.nspc, bw = 4 * A.C + 1;
+  double* cur = A.send + (long)((A.npass - 1) & 1) * 4 * nseg;
+  const double* bfin = A.bin + 2 * bw;
+  double* bo = A.bout + 2 * bw;
   const int lane = threadIdx.x;
+  const bool walk = A.changed[A.npass - 1] != 0 || (A.has_pred && bfin[4 * A.C] != 0.0);
+  if (!walk) {
+    if (lane == 0) {
+      for (long c = 0; c < A.C; c++)
+        for (int f = 0; f < 4; f++) bo[f * A.C + c] = cur[f * nseg + c * A.nspc + A.nspc - 1];
+      bo[4 * A.C] = 0.0;
+    }
+    return;
+  }
   // the running end state stays in registers (uniform over the wavefront): no memory round trip between
   // segments, and every array element this kernel reads was written by an earlier launch or not at all
   double carry[4] = {0.0, 0.0, 0.0, 0.0};
   for (long seg = 0; seg < nseg; seg++) {
-    if (seg % A.nspc == 0) {
+    const long c = seg / A.nspc, s = seg % A.nspc;
+    if (s == 0) {
 #pragma unroll
-      for (int f = 0; f < 4; f++) carry[f] = cur[f * nseg + seg];
-      continue;
+      for (int f = 0; f < 4; f++) carry[f] = A.has_pred ? bfin[f * A.C + c] : 0.0;
     }
     double used[4];
 #pragma unroll
@@ -287,27 +321,30 @@ __global__ __launch_bounds__(64) void k_chain_finish(ChainArgs A) {
     if (state_eq(carry, used)) {
 #pragma unroll
       for (int f = 0; f < 4; f++) carry[f] = cur[f * nseg + seg];
-      continue;
-    }
-    if (lane == 0) for (int f = 0; f < 4; f++) A.sstart[f * nseg + seg] = carry[f];
-    double state[4] = {carry[0], carry[1], carry[2], carry[3]};
-    if (chain_segment_run(A, seg, state, true)) {
-#pragma unroll
-      for (int f = 0; f < 4; f++) carry[f] = cur[f * nseg + seg];
     } else {
+      if (lane == 0) for (int f = 0; f < 4; f++) A.sstart[f * nseg + seg] = carry[f];
+      double state[4] = {carry[0], carry[1], carry[2], carry[3]};
+      if (chain_segment_run(A, seg, state, true)) {
 #pragma unroll
-      for (int f = 0; f < 4; f++) carry[f] = state[f];
-      if (lane == 0) for (int f = 0; f < 4; f++) cur[f * nseg + seg] = state[f];
+        for (int f = 0; f < 4; f++) carry[f] = cur[f * nseg + seg];
+      } else {
+#pragma unroll
+        for (int f = 0; f < 4; f++) carry[f] = state[f];
+        if (lane == 0) for (int f = 0; f < 4; f++) cur[f * nseg + seg] = state[f];
+      }
     }
+    if (s == A.nspc - 1 && lane == 0) for (int f = 0; f < 4; f++) bo[f * A.C + c] = carry[f];
   }
+  if (lane == 0) bo[4 * A.C] = 1.0;
 }
 
 // the serial chain's counters from the per-cell records: [1] pl/pt < 0, [2] reconstruction failures,
 // [3] Newton iterations
-__global__ __launch_bounds__(256) void k_chain_count(const double* rec, const int* info, long n, unsigned long long* cnt) {
+__global__ __launch_bounds__(256) void k_chain_count(const double* rec, const int* info, long c_lo, long c_hi,
+                                                     unsigned long long* cnt) {
   __shared__ unsigned long long s[3][256];
   unsigned long long a = 0, b = 0, it = 0;
-  for (long c = (long)blockIdx.x * 256 + threadIdx.x; c < n; c += (long)gridDim.x * 256) {
+  for (long c = c_lo + (long)blockIdx.x * 256 + threadIdx.x; c < c_hi; c += (long)gridDim.x * 256) {
     if (rec[c * NREC + R_KIND] == 0.0) continue;
     const int v = info[c];
     it += (unsigned)(v & 0xffff); a += (v >> 16) & 1; b += (v >> 17) & 1;
@@ -653,6 +690,16 @@ T* dalloc(size_t count) {
 // ------------------------------------------------------------------------------------------
 // engine
 // ------------------------------------------------------------------------------------------
+// one launch's state between the stages of a staged launch (launch_begin .. launch_end)
+struct LaunchCtx {
+  hipStream_t st = nullptr;
+  double* dev_out = nullptr;
+  long wlo = 0, whi = 0, nw = 0, p0 = 0, p1 = 0;
+  bool chained = false, empty = false;
+  PrepArgs pa{};
+  ChainArgs ca{};
+};
+
 struct is3d_engine {
   int device = 0;
   std::string err;
@@ -731,6 +778,7 @@ struct is3d_engine {
   int* d_err = nullptr;
   unsigned long long* d_cnt = nullptr;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  LaunchCtx lc;               // the launch in flight (staged launches)
   is3d_stats st{};
   bool launched = false;
 
@@ -1093,8 +1141,12 @@ static SpectraPlan spectra_plan(const is3d_engine* e) {
       }
     }
   }
-  P.tile = kTile;
   P.ts = ts_ok() ? F_TS : 0;
+  if (P.ts && kTile != IS3D_KTILE_TS) {     // spectra_tile<MODE, F_TB | F_TS>()
+    kTile = IS3D_KTILE_TS;
+    P.shmem = lds_bytes(P.nqmax);
+  }
+  P.tile = kTile;
   if (mode >= PTM) {
     const int t = kTile, ly = P.ly, tb = P.tb, t8 = P.t8;
     kTile = is3d::kern::kTile;
@@ -1392,42 +1444,44 @@ static PrepConsts make_consts(const is3d_engine* e) {
   return k;
 }
 
-extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
-  if (e && e->grp) return is3d::group_launch(e->grp, dev_out, stream);
-  if (!e) return IS3D_ERR_ARG;
+// A launch in stages: launch_begin (prepass up to PTMA's warm-start chains), chain_pass x npass + chain_end (the
+// chains), launch_end (PTMA C/B matrices, PTM renormalisation, the integral, the reduction).  is3d_launch runs them
+// back to back; a device group whose shards solve their own ranges of the chains (group.hip) interleaves the
+// shards' passes with the boundary hand-offs between them.
+static int launch_begin(is3d_engine* e, double* dev_out, void* stream, long q0, long q1, int has_pred) {
   int rc = finalize_tables(e);
   if (rc) return rc;
   if (!dev_out) return e->fail(IS3D_ERR_ARG, "null output buffer");
   HIPCHK(e, hipSetDevice(e->device));
+  LaunchCtx& L = e->lc;
+  L = LaunchCtx{};
   hipStream_t st = (hipStream_t)stream;
+  L.st = st; L.dev_out = dev_out;
   const long n = e->ncell;
-  const int mode = e->p.df_mode, dim = e->p.dimension;
+  const int mode = e->p.df_mode;
   const long outsize = is3d_output_size(e);
-  const int np = (int)e->mass.size(), npT = (int)e->pT.size(), nphi = (int)e->phi.size();
-  const int ny_out = (dim == 3) ? (int)e->y.size() : 1;
-  const int nk = ny_out, nl = (dim == 3) ? 1 : (int)e->eta.size();
   // cell window (group shards holding the whole surface): k_spectra integrates [wlo, whi); the prepass covers
-  // the window too, except for PTMA's warm-start chains, which walk every cell (MomentumSpectra.cpp:1308-1364)
+  // the window too, except for PTMA's warm-start chains, which walk every cell (MomentumSpectra.cpp:1308-1364) --
+  // or, when a device group splits the chains (q1 >= 0), the cells of this shard's positions, which are its window
   const long wlo = e->win_hi >= 0 ? e->win_lo : 0, whi = e->win_hi >= 0 ? e->win_hi : n, nw = whi - wlo;
   const bool chained = mode == PTMA && e->p.famod_chains > 0;
-  const long p0 = chained ? 0 : wlo, p1 = chained ? n : whi;
+  const bool split_chain = chained && q1 >= 0;
+  const long p0 = chained && !split_chain ? 0 : wlo, p1 = chained && !split_chain ? n : whi;
+  L.wlo = wlo; L.whi = whi; L.nw = nw; L.p0 = p0; L.p1 = p1; L.chained = chained;
   e->st = is3d_stats{};
   e->st.cells = nw;
   HIPCHK(e, hipMemsetAsync(e->d_err, 0, sizeof(int), st));
   HIPCHK(e, hipMemsetAsync(e->d_cnt, 0, 8 * sizeof(unsigned long long), st));
   HIPCHK(e, hipEventRecord(e->ev[0], st));
   if (nw == 0) {
+    L.empty = true;
     HIPCHK(e, hipMemsetAsync(dev_out, 0, outsize * sizeof(double), st));
-    HIPCHK(e, hipEventRecord(e->ev[1], st));
-    HIPCHK(e, hipEventRecord(e->ev[2], st));
-    HIPCHK(e, hipEventRecord(e->ev[3], st));
-    e->launched = true;
     return IS3D_OK;
   }
   if (!ensure(e->d_rec, e->rec_cap, (long)NREC * n)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(records) failed");
   if (!ensure(e->d_aux, e->aux_cap, 9L * n)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(aux) failed");
   if (mode == PTMA && !ensure(e->d_sol, e->sol_cap, 6L * n)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(sol) failed");
-  PrepArgs pa{};
+  PrepArgs& pa = L.pa;
   pa.k = make_consts(e); pa.tb = e->dtb; pa.surf = e->d_surf; pa.rec = e->d_rec; pa.aux = e->d_aux; pa.n = n;
   pa.c0 = p0; pa.c1 = p1;
   pa.err = e->d_err; pa.cnt = e->d_cnt;
@@ -1453,26 +1507,77 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
       hipLaunchKernelGGL(k_aniso, dim3((unsigned)aa.chains), dim3(64), 0, st, aa);
       HIPCHK(e, hipGetLastError());
     } else {
-      // warm-start chains in parallel segments (k_chain_pass): ~16k segments keep the GPU full
-      ChainArgs ca{};
+      // warm-start chains in parallel segments (k_chain_pass): ~16k segments of this engine's positions keep the
+      // GPU full
+      ChainArgs& ca = L.ca;
       ca.rec = e->d_rec; ca.ain = e->d_aux; ca.sol = e->d_sol; ca.n = n; ca.C = aa.chains; ca.h = aa.h; ca.fp2 = aa.fp2;
       const long P = (n + ca.C - 1) / ca.C;
-      ca.L = std::max((long)IS3D_CHAIN_L, (n + 16383) / 16384);
-      ca.nspc = (P + ca.L - 1) / ca.L;
-      const long nseg = ca.C * ca.nspc;
-      const long need = 4 * n + (n + 1) / 2 + 12 * nseg + kChainPasses;
+      ca.q0 = split_chain ? q0 : 0;
+      ca.q1 = split_chain ? std::min(q1, P) : P;
+      ca.has_pred = split_chain && has_pred && ca.q0 > 0;
+      const long npos = std::max(1L, ca.q1 - ca.q0);
+      ca.L = std::max((long)IS3D_CHAIN_L, (npos * ca.C + 16383) / 16384);
+      ca.nspc = (npos + ca.L - 1) / ca.L;
+      ca.npass = kChainPasses;
+      if (const char* v = std::getenv("IS3D_CHAIN_PASSES")) ca.npass = std::max(1, std::min(kChainPasses, std::atoi(v)));
+      const long nseg = ca.C * ca.nspc, bw = 4 * ca.C + 1;
+      const long need = 4 * n + (n + 1) / 2 + 12 * nseg + kChainPasses + 2 * kBndSlots * bw;
       if (!ensure(e->d_chain, e->chain_cap, need)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(chain state) failed");
       ca.sta = e->d_chain; ca.info = (int*)(e->d_chain + 4 * n);
       ca.send = e->d_chain + 4 * n + (n + 1) / 2; ca.sstart = ca.send + 8 * nseg;
       ca.changed = (int*)(ca.sstart + 4 * nseg);
+      ca.bin = ca.sstart + 4 * nseg + kChainPasses;
+      ca.bout = ca.bin + kBndSlots * bw;
       HIPCHK(e, hipMemsetAsync(ca.changed, 0, kChainPasses * sizeof(int), st));
-      for (int pass = 0; pass < kChainPasses; pass++)
-        hipLaunchKernelGGL(k_chain_pass, dim3((unsigned)nseg), dim3(64), 0, st, ca, pass);
-      hipLaunchKernelGGL(k_chain_finish, dim3(1), dim3(64), 0, st, ca);
-      hipLaunchKernelGGL(k_chain_count, dim3((unsigned)std::min(1024L, (n + 255) / 256)), dim3(256), 0, st,
-                         (const double*)e->d_rec, (const int*)ca.info, n, e->d_cnt);
-      HIPCHK(e, hipGetLastError());
     }
+  }
+  return IS3D_OK;
+}
+
+static int chain_pass(is3d_engine* e, int pass) {
+  LaunchCtx& L = e->lc;
+  if (L.empty || !L.chained) return IS3D_OK;
+  HIPCHK(e, hipSetDevice(e->device));
+  hipLaunchKernelGGL(k_chain_pass, dim3((unsigned)(L.ca.C * L.ca.nspc)), dim3(64), 0, L.st, L.ca, pass);
+  HIPCHK(e, hipGetLastError());
+  return IS3D_OK;
+}
+
+static int chain_end(is3d_engine* e) {
+  LaunchCtx& L = e->lc;
+  if (L.empty || !L.chained) return IS3D_OK;
+  HIPCHK(e, hipSetDevice(e->device));
+  const long c_lo = L.ca.q0 * L.ca.C, c_hi = std::min(e->ncell, L.ca.q1 * L.ca.C);
+  hipLaunchKernelGGL(k_chain_finish, dim3(1), dim3(64), 0, L.st, L.ca);
+  hipLaunchKernelGGL(k_chain_count, dim3((unsigned)std::min(1024L, std::max(1L, (c_hi - c_lo + 255) / 256))), dim3(256), 0,
+                     L.st, (const double*)e->d_rec, (const int*)L.ca.info, c_lo, c_hi, e->d_cnt);
+  HIPCHK(e, hipGetLastError());
+  return IS3D_OK;
+}
+
+static int launch_end(is3d_engine* e) {
+  LaunchCtx& L = e->lc;
+  hipStream_t st = L.st;
+  double* dev_out = L.dev_out;
+  HIPCHK(e, hipSetDevice(e->device));
+  if (L.empty) {
+    HIPCHK(e, hipEventRecord(e->ev[1], st));
+    HIPCHK(e, hipEventRecord(e->ev[2], st));
+    HIPCHK(e, hipEventRecord(e->ev[3], st));
+    e->launched = true;
+    return IS3D_OK;
+  }
+  const long n = e->ncell;
+  const int mode = e->p.df_mode, dim = e->p.dimension;
+  const long outsize = is3d_output_size(e);
+  const int np = (int)e->mass.size(), npT = (int)e->pT.size(), nphi = (int)e->phi.size();
+  const int ny_out = (dim == 3) ? (int)e->y.size() : 1;
+  const int nk = ny_out, nl = (dim == 3) ? 1 : (int)e->eta.size();
+  const long wlo = L.wlo, nw = L.nw;
+  const PrepArgs& pa = L.pa;
+  const dim3 g1((unsigned)std::max(1L, (L.p1 - L.p0 + 255) / 256)), b1(256);
+  (void)np;
+  if (mode == PTMA) {
     hipLaunchKernelGGL(k_famod_b, g1, b1, 0, st, pa, (const double*)e->d_sol);
     HIPCHK(e, hipGetLastError());
   }
@@ -1557,7 +1662,9 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
     // launch's last workgroups leave idle (config 4: 11 chunks ran 2811 ms back to back, one 61 GB chunk 2739 ms)
     const long rw = phitab_row(mode, KJ);
     const long per_split = cps * (long)npT * rw;
-    const long spc = std::max(1L, std::min(nsplit, (long)(IS3D_PHITAB_BYTES / 8) / per_split));
+    const long whole = per_split * nsplit * 8;          // bytes of the whole surface's rows
+    const long budget = whole <= IS3D_PHITAB_ONE ? whole : (long)IS3D_PHITAB_BYTES;
+    const long spc = std::max(1L, std::min(nsplit, budget / 8 / per_split));
     const long phn = spc * cps, nchunk = (nsplit + spc - 1) / spc;
     if (!ensure(e->d_phtab, e->phtab_cap, phn * npT * rw)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(phi tables) failed");
     if (nchunk > 1) {
@@ -1636,6 +1743,31 @@ extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   e->launched = true;
   return IS3D_OK;
 }
+
+extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
+  if (e && e->grp) return is3d::group_launch(e->grp, dev_out, stream);
+  if (!e) return IS3D_ERR_ARG;
+  int rc = launch_begin(e, dev_out, stream, 0, -1, 0);
+  for (int pass = 0; !rc && e->lc.chained && pass < e->lc.ca.npass; pass++) rc = chain_pass(e, pass);
+  if (!rc) rc = chain_end(e);
+  return rc ? rc : launch_end(e);
+}
+
+// staged launch for the device group (group.h)
+int is3d_internal_launch_begin(is3d_engine* e, double* dev_out, void* stream, long q0, long q1, int has_pred) {
+  return launch_begin(e, dev_out, stream, q0, q1, has_pred);
+}
+int is3d_internal_chain_pass(is3d_engine* e, int pass) { return chain_pass(e, pass); }
+int is3d_internal_chain_end(is3d_engine* e) { return chain_end(e); }
+int is3d_internal_launch_end(is3d_engine* e) { return launch_end(e); }
+int is3d_internal_chain_npass(const is3d_engine* e) { return e->lc.chained && !e->lc.empty ? e->lc.ca.npass : 0; }
+// boundary slot k (0, 1: pass parity, 2: final) of this engine's chain range: in (from the previous shard) or out
+double* is3d_internal_chain_bnd(is3d_engine* e, int out, int slot) {
+  if (!e->lc.chained || e->lc.empty) return nullptr;
+  const long bw = 4 * e->lc.ca.C + 1;
+  return (out ? e->lc.ca.bout : e->lc.ca.bin) + slot * bw;
+}
+long is3d_internal_chain_bnd_bytes(const is3d_engine* e) { return (4 * e->lc.ca.C + 1) * (long)sizeof(double); }
 
 extern "C" int is3d_finish(is3d_engine* e) {
   if (e && e->grp) return is3d::group_finish(e->grp);

@@ -47,6 +47,16 @@ int group_get_jonah_table(const Group* g, double* l2, double* z, double* bp, dou
 }  // namespace is3d
 
 // engine.hip internals the group uses on its shard engines (not part of the public ABI)
+// staged launch (engine.hip launch_begin / chain_pass / chain_end / launch_end): a shard solves positions
+// [q0, q1) of PTMA's warm-start chains (q1 < 0: the whole chains), its first segments starting from the end
+// states the previous shard pushes into its boundary slots (has_pred)
+int is3d_internal_launch_begin(is3d_engine* e, double* dev_out, void* stream, long q0, long q1, int has_pred);
+int is3d_internal_chain_pass(is3d_engine* e, int pass);
+int is3d_internal_chain_end(is3d_engine* e);
+int is3d_internal_launch_end(is3d_engine* e);
+int is3d_internal_chain_npass(const is3d_engine* e);
+double* is3d_internal_chain_bnd(is3d_engine* e, int out, int slot);
+long is3d_internal_chain_bnd_bytes(const is3d_engine* e);
 extern "C" {
 // engine-owned copy of cells [lo, lo + n) of a field-major device surface (25 x src_n doubles) on src_device
 int is3d_internal_copy_surface(is3d_engine* e, long n, const double* src, long src_n, int src_device, long lo);

@@ -2,10 +2,13 @@
 //
 // Partitioning: contiguous cell windows, one per device, balanced by an estimated cost --
 // a cell with u.dsigma <= 0 is skipped by every kernel (MomentumSpectra.cpp:132; it costs only its record
-// prep), any other cell costs one unit.  PTMA with the reference's warm-start chains (famod_chains > 0,
-// MomentumSpectra.cpp:1308-1364) is a serial recurrence over the whole surface: every device then holds the
-// whole surface and walks the chains itself (the Newton prepass is duplicated, the momentum integral is
-// still split by window), so the solutions are the single-device ones.
+// prep), any other cell costs one unit.  PTMA with the reference's warm-start chains (famod_chains = C > 0,
+// MomentumSpectra.cpp:1308-1364) is a serial recurrence over the whole surface (chain c = cells c, c + C, ...):
+// every device holds the whole surface, its window is a range of chain positions [q0, q1) (cells [q0 C, q1 C)),
+// and it solves only those positions' Newton steps -- the segmented solve of engine.hip k_chain_pass, with the
+// first segment of each chain starting from the end state the previous device pushes after every pass (a peer
+// copy of 4 C + 1 doubles) and a sequential finisher hand-off -- so the solutions are the single-device ones
+// bit for bit while each device does 1/K of the prepass (IS3D_CHAIN_DIST=0: every device walks every chain).
 // Reduction: one ncclAllReduce of the N_s x N_pT x N_phi x N_y float64 spectra over the device outputs on
 // the shard streams (RCCL over xGMI), or peer copy + fixed-order add on the first device when the list
 // repeats a GPU.
@@ -40,6 +43,9 @@ struct Group {
   bool nccl = false;
   std::vector<long> lo, hi;           // cell window of each shard
   bool full = false;                  // every shard holds the whole surface (PTMA warm-start chains)
+  std::vector<long> q0, q1;           // full: chain positions of each shard's window (cells [q0 C, q1 C))
+  std::vector<hipEvent_t> evE, evF;   // distributed chains: boundary pushed (E) / pass done (F), per shard
+  bool dist_chain = false;            // the launch in flight split the chains over the shards
   long ncell = 0;
   is3d_params p{};
   bool have_params = false;
@@ -91,6 +97,15 @@ Group* group_create(int n, const int* devices, std::string& err) {
     }
     g->st.push_back(s);
     g->done.push_back(ev);
+    hipEvent_t e1 = nullptr, e2 = nullptr;
+    if (hipEventCreateWithFlags(&e1, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&e2, hipEventDisableTiming) != hipSuccess) {
+      err = "event creation failed on device " + std::to_string(devices[k]);
+      group_destroy(g);
+      return nullptr;
+    }
+    g->evE.push_back(e1);
+    g->evF.push_back(e2);
   }
   (void)hipSetDevice(devices[0]);
   (void)hipEventCreate(&g->ev0);
@@ -122,6 +137,8 @@ void group_destroy(Group* g) {
     (void)hipSetDevice(g->dev[k]);
     if (g->st[k]) (void)hipStreamDestroy(g->st[k]);
     if (g->done[k]) (void)hipEventDestroy(g->done[k]);
+    if (k < g->evE.size() && g->evE[k]) (void)hipEventDestroy(g->evE[k]);
+    if (k < g->evF.size() && g->evF[k]) (void)hipEventDestroy(g->evF[k]);
   }
   if (!g->dev.empty()) {
     (void)hipSetDevice(g->dev[0]);
@@ -225,6 +242,21 @@ static void balance(Group* g, long n, const double* tau, const double* dat, cons
   }
 }
 
+// full (PTMA warm-start chains): windows of whole chain positions -- each boundary rounded to a multiple of the
+// chain count C, so a shard's cells are positions [q0, q1) of every chain
+static void chain_windows(Group* g, long n) {
+  const int K = (int)g->sh.size();
+  const long C = std::max(1L, std::min<long>(g->p.famod_chains, n)), P = (n + C - 1) / C;
+  g->q0.assign(K, 0);
+  g->q1.assign(K, 0);
+  for (int k = 0; k < K; k++) {
+    g->q0[k] = k ? g->q1[k - 1] : 0;
+    g->q1[k] = (k == K - 1) ? P : std::max(g->q0[k], std::min(P, (g->hi[k] + C / 2) / C));
+    g->lo[k] = std::min(n, g->q0[k] * C);
+    g->hi[k] = std::min(n, g->q1[k] * C);
+  }
+}
+
 int group_set_surface(Group* g, long n, const is3d_surface* s) {
   if (!s || n < 0) return g->fail(IS3D_ERR_ARG, "bad surface");
   if (n > 0 && (!s->tau || !s->dat || !s->dax || !s->day || !s->dan || !s->ux || !s->uy || !s->un))
@@ -232,6 +264,7 @@ int group_set_surface(Group* g, long n, const is3d_surface* s) {
   g->ncell = n;
   balance(g, n, s->tau, s->dat, s->dax, s->day, s->dan, s->ux, s->uy, s->un);
   g->full = needs_full(g);
+  if (g->full) chain_windows(g, n);
   return each_parallel(g, [&](int k) -> int {
     is3d_engine* e = g->sh[k];
     if (g->full) {
@@ -262,6 +295,7 @@ int group_set_surface_device(Group* g, long n, const double* dev_fields) {
   balance(g, n, h.data(), h.data() + n, h.data() + 2 * n, h.data() + 3 * n, h.data() + 4 * n, h.data() + 5 * n,
           h.data() + 6 * n, h.data() + 7 * n);
   g->full = needs_full(g);
+  if (g->full) chain_windows(g, n);
   return each_parallel(g, [&](int k) -> int {
     is3d_engine* e = g->sh[k];
     const long o = g->full ? 0 : g->lo[k], m = g->full ? n : g->hi[k] - g->lo[k];
@@ -272,6 +306,62 @@ int group_set_surface_device(Group* g, long n, const double* dev_fields) {
 }
 
 long group_output_size(const Group* g) { return g->sh.empty() ? -1 : is3d_output_size(g->sh[0]); }
+
+// PTMA warm-start chains split over the shards (see the file comment).  Every pass j of every shard is enqueued
+// in reverse shard order, so a shard's pass j waits (event E of its predecessor) for exactly the predecessor's push
+// of its pass j - 1 end states, and a shard pushes its pass j end states into its successor's parity-j slot only
+// after the successor's pass j (event F), the last reader of that slot (its pass j - 1 read it).  The finishers
+// then run in shard order, each handing its final end states (and whether it walked) to the next.
+template <class S>
+static int launch_split_chains(Group* g, S stream_of) {
+  const int K = (int)g->sh.size();
+  std::vector<int> act;                 // shards with chain positions, in order
+  for (int k = 0; k < K; k++) {
+    const int rc = is3d_internal_launch_begin(g->sh[k], g->buf[k], (void*)stream_of(k), g->q0[k], g->q1[k],
+                                              act.empty() ? 0 : 1);
+    if (rc) return g->shard_fail(k, rc);
+    if (g->q1[k] > g->q0[k]) act.push_back(k);
+  }
+  const int na = (int)act.size();
+  const int npass = na ? is3d_internal_chain_npass(g->sh[act[0]]) : 0;
+  auto bad = [&](const char* what) { return g->fail(IS3D_ERR_DEVICE, std::string("chain hand-off: ") + what); };
+  for (int j = 0; j < npass; j++) {
+    for (int i = na - 1; i >= 0; i--) {
+      const int k = act[i], kp = i ? act[i - 1] : -1, kn = i + 1 < na ? act[i + 1] : -1;
+      if (hipSetDevice(g->dev[k]) != hipSuccess) return bad("hipSetDevice");
+      if (kp >= 0 && j > 0 && hipStreamWaitEvent(stream_of(k), g->evE[kp], 0) != hipSuccess) return bad("wait");
+      const int rc = is3d_internal_chain_pass(g->sh[k], j);
+      if (rc) return g->shard_fail(k, rc);
+      if (hipEventRecord(g->evF[k], stream_of(k)) != hipSuccess) return bad("record");
+      if (kn >= 0) {
+        if (hipStreamWaitEvent(stream_of(k), g->evF[kn], 0) != hipSuccess) return bad("wait");
+        if (hipMemcpyPeerAsync(is3d_internal_chain_bnd(g->sh[kn], 0, j & 1), g->dev[kn],
+                               is3d_internal_chain_bnd(g->sh[k], 1, j & 1), g->dev[k],
+                               is3d_internal_chain_bnd_bytes(g->sh[k]), stream_of(k)) != hipSuccess)
+          return bad("hipMemcpyPeerAsync");
+        if (hipEventRecord(g->evE[k], stream_of(k)) != hipSuccess) return bad("record");
+      }
+    }
+  }
+  for (int i = 0; i < na; i++) {
+    const int k = act[i], kp = i ? act[i - 1] : -1, kn = i + 1 < na ? act[i + 1] : -1;
+    if (hipSetDevice(g->dev[k]) != hipSuccess) return bad("hipSetDevice");
+    if (kp >= 0 && hipStreamWaitEvent(stream_of(k), g->evE[kp], 0) != hipSuccess) return bad("wait");
+    const int rc = is3d_internal_chain_end(g->sh[k]);
+    if (rc) return g->shard_fail(k, rc);
+    if (kn >= 0) {
+      if (hipMemcpyPeerAsync(is3d_internal_chain_bnd(g->sh[kn], 0, 2), g->dev[kn], is3d_internal_chain_bnd(g->sh[k], 1, 2),
+                             g->dev[k], is3d_internal_chain_bnd_bytes(g->sh[k]), stream_of(k)) != hipSuccess)
+        return bad("hipMemcpyPeerAsync");
+      if (hipEventRecord(g->evE[k], stream_of(k)) != hipSuccess) return bad("record");
+    }
+  }
+  for (int k = 0; k < K; k++) {
+    const int rc = is3d_internal_launch_end(g->sh[k]);
+    if (rc) return g->shard_fail(k, rc);
+  }
+  return IS3D_OK;
+}
 
 int group_launch(Group* g, double* dev_out, void* stream) {
   if (!dev_out) return g->fail(IS3D_ERR_ARG, "null output buffer");
@@ -297,11 +387,18 @@ int group_launch(Group* g, double* dev_out, void* stream) {
   g->cur0 = (hipStream_t)stream;
   (void)hipSetDevice(g->dev[0]);
   if (hipEventRecord(g->ev0, g->cur0) != hipSuccess) return g->fail(IS3D_ERR_DEVICE, "hipEventRecord failed");
-  for (int k = 0; k < K; k++) {
-    const int rc = is3d_launch(g->sh[k], g->buf[k], k ? (void*)g->st[k] : stream);
-    if (rc) return g->shard_fail(k, rc);
-  }
   auto stream_of = [&](int k) { return k ? g->st[k] : g->cur0; };
+  const char* dc = std::getenv("IS3D_CHAIN_DIST");
+  g->dist_chain = g->full && K > 1 && !(dc && !std::strcmp(dc, "0"));
+  if (!g->dist_chain) {
+    for (int k = 0; k < K; k++) {
+      const int rc = is3d_launch(g->sh[k], g->buf[k], k ? (void*)g->st[k] : stream);
+      if (rc) return g->shard_fail(k, rc);
+    }
+  } else {
+    const int rc = launch_split_chains(g, stream_of);
+    if (rc) return rc;
+  }
   if (g->nccl) {
     if (ncclGroupStart() != ncclSuccess) return g->fail(IS3D_ERR_DEVICE, "ncclGroupStart failed");
     for (int k = 0; k < K; k++) {
@@ -362,7 +459,7 @@ int group_finish(Group* g) {
   if (hipEventSynchronize(g->ev1) != hipSuccess) return g->fail(IS3D_ERR_DEVICE, "group synchronisation failed");
   float ms = 0.f;
   if (hipEventElapsedTime(&ms, g->ev0, g->ev1) == hipSuccess) agg.ms_total = ms;
-  if (g->full) {
+  if (g->full && !g->dist_chain) {
     // every shard walked the whole PTMA chain and prepared every cell: count that work once (shard 0's, the
     // same solves everywhere)
     is3d_stats s0{};

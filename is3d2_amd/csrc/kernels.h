@@ -22,8 +22,13 @@ constexpr int kTile = IS3D_KTILE;   // cells per LDS tile
 // cells per k_spectra tile of one delta-f mode and launch (8 for Grad / RTA-CE: 16 costs them 18% / 11%,
 // r2t; the modified path's F_T8 and F_LY launches keep 8 where 16 cells' q-row tables would not fit:
 // config 1's shape in F_LY ran 11.2 ms with 8-cell tiles, 13.6 ms with 16)
+#ifndef IS3D_KTILE_TS
+#define IS3D_KTILE_TS 8       // F_TS launches (LDS: records, y-terms and T1 rows only)
+#endif
 template <int MODE, int FLAGS>
-constexpr int spectra_tile() { return (MODE >= PTM && !(FLAGS & (32 | 16 | 8))) ? IS3D_KTILE_MOD : kTile; }
+constexpr int spectra_tile() {
+  return (MODE >= PTM && !(FLAGS & (32 | 16 | 8))) ? IS3D_KTILE_MOD : ((FLAGS & 128) && (FLAGS & 4)) ? IS3D_KTILE_TS : kTile;
+}
 // waves per SIMD the spectra kernel is register-allocated for (measured on MI355X, config2):
 // Grad and RTA-CE run best at 3 (168 VGPRs), the modified-momentum modes at 2
 #ifndef IS3D_SPECTRA_WAVES_SEP
@@ -115,8 +120,13 @@ __host__ __device__ constexpr int phitab_row(int mode, int nphp) { return (mode 
 #ifndef IS3D_TS
 #define IS3D_TS 1             // F_TB launches with one phi block take the scalar-table form (F_TS)
 #endif
+#ifndef IS3D_PHITAB_ONE
+#define IS3D_PHITAB_ONE (8L << 30)     // F_TS tables up to this size are written and integrated in one chunk
+#endif
 #ifndef IS3D_PHITAB_BYTES
-#define IS3D_PHITAB_BYTES (6L << 30)   // F_TS table budget: larger surfaces run chunk by chunk (whole cell splits)
+#define IS3D_PHITAB_BYTES (2L << 30)   // larger ones in chunks of whole cell splits of about this size, alternating
+                                       // over two streams (config 4: 2 GB chunks 2738 ms, 6 GB 2770 ms, one 61 GB
+                                       // chunk 2734 ms; config 2 RTA-CE in one 6.1 GB chunk 249 ms, 2 GB chunks 254 ms)
 #endif
 
 #ifndef IS3D_SPLIT_BYTES

@@ -50,9 +50,13 @@ def test_group_smash_grid_grad_table_launch():
     assert parity(grp, one)[0] < 1e-10
 
 
-def test_group_ptma_chain_walks_whole_surface():
-    """PTMA with the reference's warm-start chain: every shard holds the whole surface and walks the chain,
-    integrating only its window -- same Newton solves (iteration count) as one device."""
+@pytest.mark.parametrize("dist", ["1", "0"])
+def test_group_ptma_chain_walks_whole_surface(monkeypatch, dist):
+    """PTMA with the reference's warm-start chain: every shard holds the whole surface; with the chains split
+    (default) each shard solves only its window's chain positions from its predecessor's boundary states, with
+    IS3D_CHAIN_DIST=0 each walks the whole chain -- either way the same Newton solves (iteration count) as one
+    device."""
+    monkeypatch.setenv("IS3D_CHAIN_DIST", dist)
     s = synth.as_read(synth.surface(900, seed=73, dimension=2))
     spec = make_spec(hrg_eos=2, chosen="pikp", df_mode=5, dimension=2, famod_chains=1)
     one, st1 = spectra(spec, s)
@@ -60,6 +64,31 @@ def test_group_ptma_chain_walks_whole_surface():
     assert stg["iterations"] == st1["iterations"]
     assert stg["breakdown"] == st1["breakdown"]
     assert parity(grp, one)[0] < 1e-12
+
+
+@pytest.mark.parametrize("chains,ndev,passes", [(1, 3, None), (3, 2, None), (1, 5, None), (16, 3, None),
+                                                 (1, 4, "1"), (3, 3, "2")])
+def test_group_ptma_distributed_chains(monkeypatch, chains, ndev, passes):
+    """Chains split over the shards on a breakdown-heavy surface (failed solves reset the state, p_L < 0 cells pass
+    it through) with u.dsigma <= 0 runs: the iteration / failure counts equal one device's, which equal the
+    oracle's serial chains.  IS3D_CHAIN_PASSES = 1 or 2 leaves most of the ripple to the finishers, which hand the
+    final boundary states from shard to shard."""
+    if passes:
+        monkeypatch.setenv("IS3D_CHAIN_PASSES", passes)
+    s = synth.as_read(synth.surface(2400, seed=109, dimension=3, full3d=True))
+    s["bulkPi"] = s["bulkPi"].copy()
+    s["bulkPi"][::2] *= 10.0
+    s["dat"] = s["dat"].copy()
+    s["dat"][700:900] *= -20.0
+    spec = make_spec(hrg_eos=2, chosen="pikp", df_mode=5, dimension=3, famod_chains=chains)
+    one, st1 = spectra(spec, s)
+    grp, stg = spectra(spec, s, devices=[0] * ndev)
+    for k in ("iterations", "breakdown", "pl_negative", "recon_fail", "cells"):
+        assert stg[k] == st1[k], (k, stg[k], st1[k])
+    assert np.array_equal(np.isnan(grp), np.isnan(one))
+    assert parity(np.nan_to_num(grp), np.nan_to_num(one))[0] < 1e-12
+    _, rst = O.spectra(spec, s, threads=chains, return_stats=True)
+    assert stg["iterations"] == rst[3]
 
 
 def test_group_rccl_one_rank(monkeypatch):
