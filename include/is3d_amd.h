@@ -163,6 +163,15 @@ int is3d_set_surface_device(is3d_engine *e, long n_cells, const double *dev_fiel
  * solutions (MomentumSpectra.cpp:1308-1364), which cell shards could not. */
 int is3d_set_cell_window(is3d_engine *e, long lo, long hi);
 
+/* Estimated k_spectra cost of every cell of the surface set last, relative to a live cell of the mode's main
+ * launch (no reference counterpart: the shard cost model of SURVEY.md 8(e), used by is3d_create_devices' windows
+ * and by one-process-per-GPU callers): 0.02 for u.dsigma <= 0 (skipped by every kernel,
+ * MomentumSpectra.cpp:132; its record prep only); PTM / PTB cells that break down or have narrow rapidity
+ * windows take the separable fallback launch (MomentumSpectra.cpp:863-929) at 1.4 / 1.8 (measured on MI355X,
+ * tools/fb_cost_probe.py); every other cell 1 (PTMA's breakdowns are only known after its Newton solves).
+ * Runs the record prepass on the engine's GPU (synchronous); cost holds n_cells doubles. */
+int is3d_cell_costs(is3d_engine *e, double *cost);
+
 /* Full call: kernels + device->host copy of dN/(pT dpT dphi dy) into dN_out. */
 int is3d_calculate_spectra(is3d_engine *e, double *dN_out);
 

@@ -17,7 +17,7 @@ IS3D_OK, IS3D_ERR_ARG, IS3D_ERR_STATE, IS3D_ERR_DEVICE, IS3D_ERR_DF_RANGE, IS3D_
 # every symbol include/is3d_amd.h declares
 EXPORTS = ["is3d_abi_version", "is3d_build_id", "is3d_create", "is3d_create_devices", "is3d_destroy", "is3d_last_error", "is3d_set_params",
            "is3d_set_species", "is3d_set_species_classes", "is3d_species_integrated", "is3d_set_pdg", "is3d_set_momentum_grid", "is3d_set_gauss_laguerre",
-           "is3d_set_df_tables", "is3d_set_surface", "is3d_set_surface_device", "is3d_set_cell_window", "is3d_calculate_spectra",
+           "is3d_set_df_tables", "is3d_set_surface", "is3d_set_surface_device", "is3d_set_cell_window", "is3d_cell_costs", "is3d_calculate_spectra",
            "is3d_launch", "is3d_finish", "is3d_get_stats", "is3d_output_size", "is3d_evaluate_df_coefficients",
            "is3d_surface_averages", "is3d_get_jonah_table", "is3d_set_momentum_weights", "is3d_set_spacetime_bins",
            "is3d_calculate_dN_dX", "is3d_get_cell_yields", "is3d_total_yield"]
@@ -79,6 +79,7 @@ def load():
     lib.is3d_set_surface.argtypes = [C.c_void_p, C.c_long, P(Surface)]
     lib.is3d_set_surface_device.argtypes = [C.c_void_p, C.c_long, C.c_void_p]
     lib.is3d_set_cell_window.argtypes = [C.c_void_p, C.c_long, C.c_long]
+    lib.is3d_cell_costs.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
     lib.is3d_calculate_spectra.argtypes = [C.c_void_p, pd]
     lib.is3d_launch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     lib.is3d_finish.argtypes = [C.c_void_p]

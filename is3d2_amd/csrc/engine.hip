@@ -401,6 +401,15 @@ __global__ __launch_bounds__(256) void k_renorm(RenormArgs A) {
   A.renorm[idx] = ptm_renorm(A.k, aux, A.mass[s], A.sign[s], A.degen[s], A.baryon[s]);
 }
 
+// per-cell cost estimate (is3d_cell_costs) from the prepared records
+__global__ __launch_bounds__(256) void k_cell_cost(const double* rec, long n, double fb_cost, double* cost) {
+  const long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  const double* R = rec + c * NREC;
+  const bool fb = R[R_KIND] == 1.0 || (R[R_KIND] == 2.0 && R[R_NARROW] != 0.0);
+  cost[c] = R[R_KIND] == 0.0 ? kSkipCost : (fb_cost > 0.0 && fb) ? fb_cost : 1.0;
+}
+
 // Modified modes: the cells whose lanes may take the separable fallback (breakdown: R_KIND == 1; narrow
 // rapidity windows: R_NARROW != 0, MomentumSpectra.cpp:863-871), listed in ascending order for the F_FB
 // launch.  One workgroup: each thread counts a contiguous chunk, an LDS scan gives the offsets, the chunks
@@ -1768,6 +1777,44 @@ double* is3d_internal_chain_bnd(is3d_engine* e, int out, int slot) {
   return (out ? e->lc.ca.bout : e->lc.ca.bin) + slot * bw;
 }
 long is3d_internal_chain_bnd_bytes(const is3d_engine* e) { return (4 * e->lc.ca.C + 1) * (long)sizeof(double); }
+
+extern "C" int is3d_cell_costs(is3d_engine* e, double* cost) {
+  if (e && e->grp) return is3d::group_fail(e->grp, IS3D_ERR_UNSUPPORTED, "is3d_cell_costs: call it on a one-device engine");
+  if (!e || !cost) return IS3D_ERR_ARG;
+  int rc = finalize_tables(e);
+  if (rc) return rc;
+  const long n = e->ncell;
+  if (n <= 0) return IS3D_OK;
+  HIPCHK(e, hipSetDevice(e->device));
+  const int mode = e->p.df_mode;
+  if (!ensure(e->d_rec, e->rec_cap, (long)NREC * n)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(records) failed");
+  if (!ensure(e->d_aux, e->aux_cap, 9L * n)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(aux) failed");
+  double* d_cost = nullptr;
+  HIPCHK(e, hipMalloc(&d_cost, n * sizeof(double)));
+  PrepArgs pa{};
+  pa.k = make_consts(e); pa.tb = e->dtb; pa.surf = e->d_surf; pa.rec = e->d_rec; pa.aux = e->d_aux; pa.n = n;
+  pa.c0 = 0; pa.c1 = n;
+  pa.err = e->d_err; pa.cnt = e->d_cnt;
+  const dim3 g1((unsigned)((n + 255) / 256)), b1(256);
+  hipError_t er = hipMemsetAsync(e->d_err, 0, sizeof(int), nullptr);
+  if (er == hipSuccess) er = hipMemsetAsync(e->d_cnt, 0, 8 * sizeof(unsigned long long), nullptr);
+  switch (mode) {
+    case GRAD: hipLaunchKernelGGL(k_prep<GRAD>, g1, b1, 0, nullptr, pa); break;
+    case CE: hipLaunchKernelGGL(k_prep<CE>, g1, b1, 0, nullptr, pa); break;
+    case PTM: hipLaunchKernelGGL(k_prep<PTM>, g1, b1, 0, nullptr, pa); break;
+    case PTB: hipLaunchKernelGGL(k_prep<PTB>, g1, b1, 0, nullptr, pa); break;
+    default: hipLaunchKernelGGL(k_prep<PTMA>, g1, b1, 0, nullptr, pa); break;
+  }
+  // separable-fallback cells of PTM / PTB relative to a modified cell (config-2 shape, MI355X,
+  // tools/fb_cost_probe.py: PTM 1.37-1.43, PTB 1.58-1.80)
+  const double fb_cost = mode == PTM ? 1.4 : mode == PTB ? 1.8 : 0.0;
+  hipLaunchKernelGGL(k_cell_cost, g1, b1, 0, nullptr, (const double*)e->d_rec, n, fb_cost, d_cost);
+  if (er == hipSuccess) er = hipGetLastError();
+  if (er == hipSuccess) er = hipMemcpy(cost, d_cost, n * sizeof(double), hipMemcpyDeviceToHost);
+  (void)hipFree(d_cost);
+  if (er != hipSuccess) return e->fail(IS3D_ERR_DEVICE, std::string("is3d_cell_costs: ") + hipGetErrorString(er));
+  return IS3D_OK;
+}
 
 extern "C" int is3d_finish(is3d_engine* e) {
   if (e && e->grp) return is3d::group_finish(e->grp);

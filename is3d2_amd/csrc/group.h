@@ -14,6 +14,8 @@
 
 namespace is3d {
 struct Group;
+// shard cost of a cell with u.dsigma <= 0 (skipped by every kernel, MomentumSpectra.cpp:132): its record prep only
+constexpr double kSkipCost = 0.02;
 
 Group* group_create(int n, const int* devices, std::string& err);
 void group_destroy(Group* g);

@@ -31,7 +31,6 @@ namespace {
 __global__ __launch_bounds__(256) void k_accum(double* __restrict__ out, const double* __restrict__ add, long n) {
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) out[i] += add[i];
 }
-constexpr double kSkipCost = 0.02;   // a u.dsigma <= 0 cell: record prep only
 }  // namespace
 
 struct Group {
@@ -216,12 +215,15 @@ int group_set_df_tables(Group* g, int nT, int nmuB, const double* T, const doubl
   return each(g, [&](is3d_engine* e) { return is3d_set_df_tables(e, nT, nmuB, T, muB, tab, T_avg); });
 }
 
-// contiguous windows of ~equal estimated cost (u.dsigma <= 0 cells cost kSkipCost, the rest 1)
+// contiguous windows of ~equal estimated cost: u.dsigma <= 0 cells cost kSkipCost, the rest 1 -- or, when
+// `cost` is given (is3d_cell_costs on the whole surface: PTM / PTB separable-fallback cells), those costs
 static void balance(Group* g, long n, const double* tau, const double* dat, const double* dax, const double* day,
-                    const double* dan, const double* ux, const double* uy, const double* un) {
+                    const double* dan, const double* ux, const double* uy, const double* un,
+                    const double* cost = nullptr) {
   const int K = (int)g->sh.size();
   std::vector<double> pre((size_t)n + 1, 0.0);
   for (long c = 0; c < n; c++) {
+    if (cost) { pre[c + 1] = pre[c] + cost[c]; continue; }
     const double t2 = tau[c] * tau[c];
     const double ut = std::sqrt(1.0 + ux[c] * ux[c] + uy[c] * uy[c] + t2 * un[c] * un[c]);
     const bool live = ut * dat[c] + ux[c] * dax[c] + uy[c] * day[c] + un[c] * dan[c] > 0.0;
@@ -241,6 +243,9 @@ static void balance(Group* g, long n, const double* tau, const double* dat, cons
     g->hi[k] = c;
   }
 }
+
+// the modes whose cell costs differ beyond u.dsigma <= 0 (separable fallback of PTM / PTB)
+static bool cost_prepass(const Group* g) { return g->have_params && (g->p.df_mode == 3 || g->p.df_mode == 4); }
 
 // full (PTMA warm-start chains): windows of whole chain positions -- each boundary rounded to a multiple of the
 // chain count C, so a shard's cells are positions [q0, q1) of every chain
@@ -262,7 +267,14 @@ int group_set_surface(Group* g, long n, const is3d_surface* s) {
   if (n > 0 && (!s->tau || !s->dat || !s->dax || !s->day || !s->dan || !s->ux || !s->uy || !s->un))
     return g->fail(IS3D_ERR_ARG, "surface field missing");
   g->ncell = n;
-  balance(g, n, s->tau, s->dat, s->dax, s->day, s->dan, s->ux, s->uy, s->un);
+  // PTM / PTB: the separable-fallback cells cost 1.4 / 1.8 of a modified one; the prepass on shard 0 knows which
+  // cells they are (the tables must be set: otherwise the u.dsigma model)
+  std::vector<double> cost;
+  if (g->sh.size() > 1 && n > 0 && cost_prepass(g) && is3d_set_surface(g->sh[0], n, s) == IS3D_OK) {
+    cost.resize((size_t)n);
+    if (is3d_cell_costs(g->sh[0], cost.data()) != IS3D_OK) cost.clear();
+  }
+  balance(g, n, s->tau, s->dat, s->dax, s->day, s->dan, s->ux, s->uy, s->un, cost.empty() ? nullptr : cost.data());
   g->full = needs_full(g);
   if (g->full) chain_windows(g, n);
   return each_parallel(g, [&](int k) -> int {
@@ -292,8 +304,14 @@ int group_set_surface_device(Group* g, long n, const double* dev_fields) {
     if (hipMemcpy(h.data() + (size_t)i * n, dev_fields + (size_t)fidx[i] * n, n * sizeof(double), hipMemcpyDeviceToHost) != hipSuccess)
       return g->fail(IS3D_ERR_DEVICE, "surface read-back failed");
   g->ncell = n;
+  std::vector<double> cost;
+  if (g->sh.size() > 1 && n > 0 && cost_prepass(g) &&
+      is3d_internal_copy_surface(g->sh[0], n, dev_fields, n, g->dev[0], 0) == IS3D_OK) {
+    cost.resize((size_t)n);
+    if (is3d_cell_costs(g->sh[0], cost.data()) != IS3D_OK) cost.clear();
+  }
   balance(g, n, h.data(), h.data() + n, h.data() + 2 * n, h.data() + 3 * n, h.data() + 4 * n, h.data() + 5 * n,
-          h.data() + 6 * n, h.data() + 7 * n);
+          h.data() + 6 * n, h.data() + 7 * n, cost.empty() ? nullptr : cost.data());
   g->full = needs_full(g);
   if (g->full) chain_windows(g, n);
   return each_parallel(g, [&](int k) -> int {

@@ -42,9 +42,21 @@ def balanced_ranges(costs, world):
     return [(bounds[k], bounds[k + 1]) for k in range(world)]
 
 
-def shard_bounds(surf, rank, world):
-    """This rank's cost-balanced contiguous cell range of `surf`."""
-    return balanced_ranges(cell_costs(surf), world)[rank]
+def device_cell_costs(spec, surf, T_avg=None, device=0):
+    """Per-cell costs from the engine's prepass (is3d_cell_costs: PTM / PTB separable-fallback cells cost
+    1.4 / 1.8 of a modified one, u.dsigma <= 0 cells 0.02) -- the model is3d_create_devices balances with."""
+    from .engine import build_engine
+    e = build_engine(spec, surf, T_avg=T_avg, device=device)
+    try:
+        return e.cell_costs()
+    finally:
+        e.close()
+
+
+def shard_bounds(surf, rank, world, costs=None):
+    """This rank's cost-balanced contiguous cell range of `surf` (costs: e.g. device_cell_costs; default the
+    u.dsigma model of cell_costs)."""
+    return balanced_ranges(cell_costs(surf) if costs is None else np.asarray(costs), world)[rank]
 
 
 def average_sums(surf, include_baryon=0):

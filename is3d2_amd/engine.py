@@ -143,6 +143,14 @@ class Engine:
         self._chk(self.lib.is3d_set_cell_window(self._e, int(lo), int(hi)))
 
     # --- compute -----------------------------------------------------------------------
+    def cell_costs(self):
+        """Per-cell shard cost estimate of the surface set last (is3d_cell_costs: 0.02 skipped, PTM / PTB
+        separable-fallback cells 1.4 / 1.8, else 1)."""
+        n = self.ncell
+        out = np.zeros(max(n, 1))
+        self._chk(self.lib.is3d_cell_costs(self._e, _dp(out)))
+        return out[:n]
+
     def output_size(self):
         return self.lib.is3d_output_size(self._e)
 

@@ -47,3 +47,13 @@ def parity(got, ref, floor=1e-300):
     m = np.abs(ref) > floor
     rel = np.abs(got[m] - ref[m]) / np.abs(ref[m]) if m.any() else np.zeros(1)
     return float(rel.max()), int((~m).sum()), int((np.abs(got) <= floor).sum())
+
+
+def rel_quantile(got, ref, q=0.99, floor=1e-300):
+    """q-quantile of |got-ref|/|ref| over |ref| > floor: a drift guard far below the max-error bar (typical
+    errors are ~1e-13, the 1e-8 bar sits 1e4-1e5x above them)."""
+    got = np.asarray(got); ref = np.asarray(ref)
+    m = np.abs(ref) > floor
+    if not m.any():
+        return 0.0
+    return float(np.quantile(np.abs(got[m] - ref[m]) / np.abs(ref[m]), q))

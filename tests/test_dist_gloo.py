@@ -76,3 +76,17 @@ def test_cost_balanced_ranges():
         # equal counts would have given rank 0 only free cells
         assert cost[0] > 0.5 * c.sum() / world
     assert D.balanced_ranges(np.ones(3), 8)[-1] == (3, 3)     # more ranks than cells: empty tail ranges
+
+
+def test_cost_balanced_ranges_with_fallback_costs():
+    """Given per-cell costs (is3d_cell_costs: PTB separable-fallback cells 1.8, modified 1, free 0.02) the ranges
+    balance those instead of counting cells: a fallback-heavy first half gets fewer cells."""
+    from is3d2_amd import dist as D, synth
+    s = synth.as_read(synth.surface(1000, seed=5))
+    costs = np.r_[np.full(500, 1.8), np.full(500, 1.0)]
+    costs[::97] = D.SKIP_COST
+    for world in (2, 4):
+        r = [D.shard_bounds(s, k, world, costs=costs) for k in range(world)]
+        cost = [costs[lo:hi].sum() for lo, hi in r]
+        assert max(cost) - min(cost) <= 2 * 1.8 + 1e-9, cost     # each boundary within one cell
+    assert D.shard_bounds(s, 0, 2, costs=costs)[1] < 450

@@ -203,3 +203,26 @@ def test_group_distinct_devices(monkeypatch, reduce):
     one, _ = spectra(spec, s)
     grp, _ = spectra(spec, s, devices=[0, 1])
     assert parity(grp, one)[0] < 1e-12
+
+
+def test_group_balances_breakdown_cluster():
+    """PTB with the separable-fallback cells (breakdown, 1.8x a modified cell) clustered in the first half of the
+    surface: is3d_cell_costs sees them, the cost-balanced split moves below n / 2, and the device group (which
+    balances with the same costs) still equals one engine."""
+    from is3d2_amd import dist as D
+    n = 1200
+    s = synth.as_read(synth.surface(n, seed=113, dimension=2))
+    s["bulkPi"] = s["bulkPi"].copy()
+    s["bulkPi"][: n // 2] *= 30.0
+    spec = make_spec(hrg_eos=2, chosen="pikp", df_mode=4, dimension=2)
+    costs = D.device_cell_costs(spec, s)
+    assert costs.shape == (n,)
+    fb = costs > 1.0
+    assert fb[: n // 2].sum() > 0.3 * (n // 2) and fb[n // 2:].sum() < 0.05 * (n // 2)
+    assert set(np.unique(costs)) <= {0.02, 1.0, 1.8}
+    lo, hi = D.shard_bounds(s, 0, 2, costs=costs)
+    assert lo == 0 and hi < n // 2
+    one, st1 = spectra(spec, s)
+    grp, stg = spectra(spec, s, devices=[0, 0])
+    assert stg["breakdown"] == st1["breakdown"] > 0
+    assert parity(grp, one)[0] < 1e-12

@@ -5,12 +5,13 @@ allows."""
 import numpy as np
 import pytest
 
-from helpers import parity
+from helpers import parity, rel_quantile
 from is3d2_amd import IS3DError, build_engine, make_spec, surface_averages, synth
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-8   # measured 1e-13..2e-9 (cancellation in tiny high-pT entries); north_star bar is 1e-6
+P99 = 1e-11  # 99th-percentile relative error: a drift guard beside the max bar (typical ~1e-13)
 
 
 def run_gpu(spec, surf, T_avg=None):
@@ -30,6 +31,7 @@ def test_spectra_parity(dim, mode):
     got, st = run_gpu(spec, s)
     rel, zr, zg = parity(got, ref)
     assert rel < TOL, (rel, zr, zg)
+    assert rel_quantile(got, ref) < P99
     assert zr == zg
     assert st["breakdown"] == rst[0]
     if mode == 5:
@@ -46,6 +48,7 @@ def test_smash_3d_grad_subset(mode, reg_out):
     ref = O.spectra(spec, s, threads=8)
     got, _ = run_gpu(spec, s)
     assert parity(got, ref)[0] < TOL
+    assert rel_quantile(got, ref) < P99
 
 
 @pytest.mark.parametrize("mode", [1, 2, 3])
@@ -197,6 +200,7 @@ def test_phi_grid_blocks(phi, dim, mode):
     got, _ = run_gpu(spec, s)
     rel, zr, zg = parity(got, ref)
     assert rel < TOL, (rel, zr, zg)
+    assert rel_quantile(got, ref) < P99
     assert zr == zg
 
 
