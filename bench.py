@@ -168,7 +168,7 @@ def executed_roofline(args, mode, ms_spectra, ms_total, neta, units_local, n_loc
             stale.append("traffic: %s (build %s)" % (traffic.get("tag"), traffic.get("build_id")))
             traffic = None
         else:
-            traffic = traffic["hbm_bytes_per_launch"]
+            traffic = traffic.get("hbm_bytes_per_pass", traffic["hbm_bytes_per_launch"])
     elif traffic is not None:
         stale.append("traffic: untagged")
         traffic = None
@@ -191,11 +191,15 @@ def executed_roofline(args, mode, ms_spectra, ms_total, neta, units_local, n_loc
         r["stale_profiles"] = "counter summaries of another build, not used: " + "; ".join(stale)
     if ex is not None:
         if "fp64_flops_per_launch" in ex:
-            r["achieved"] = ex["fp64_flops_per_launch"] / t / 1e12
+            # per pass: an F_TS launch over more than one table chunk runs k_spectra once per chunk
+            flops = ex.get("fp64_flops_per_pass", ex["fp64_flops_per_launch"])
+            r["achieved"] = flops / t / 1e12
             r["frac"] = r["achieved"] / FP64_PEAK_TFLOPS
-            r["executed_flops_per_unit"] = ex["fp64_flops_per_launch"] / units_local
+            r["executed_flops_per_unit"] = flops / units_local
+            r["launches_per_pass"] = ex.get("launches_per_pass", 1.0)
         if "fma_f64_insts_per_launch" in ex:
-            ins = sum(ex.get(c + "_insts_per_launch", 0.0) for c in ("add_f64", "mul_f64", "fma_f64", "trans_f64"))
+            ins = ex.get("launches_per_pass", 1.0) * sum(ex.get(c + "_insts_per_launch", 0.0)
+                                                          for c in ("add_f64", "mul_f64", "fma_f64", "trans_f64"))
             r["fp64_pipe_frac"] = 64.0 * ins / (t * FP64_LANE_OPS_PEAK)
         r["executed"] = dict(ex, note="rocprofv3 PMC passes of this workload (tag); counts per k_spectra launch")
     return r

@@ -34,7 +34,12 @@
 #define IS3D_CHAIN_L 32       // PTMA warm-start chains: positions per segment (k_chain_pass), at least
 #endif
 #ifndef IS3D_MAX_SPLITS
-#define IS3D_MAX_SPLITS 256   // cap on k_spectra's cell splits (one output-sized slab each; config 4: 256 x 50 MB)
+#define IS3D_MAX_SPLITS 1024  // cap on k_spectra's cell splits (one output-sized slab each)
+#endif
+#ifndef IS3D_SLAB_BYTES
+#define IS3D_SLAB_BYTES (48L << 30)   // ... and on their slabs' memory: config 4 (10^6 cells, 50 MB slabs) runs 880 splits
+                                      // of 0.5 MB of records (44 GB of slabs): 2569 ms per pass, 512 splits 2679 ms,
+                                      // 256 splits 2751 ms (profiles/round4_r4a_ab_ts.log)
 #endif
 #include <hip/hip_runtime.h>
 
@@ -1634,7 +1639,9 @@ static int launch_end(is3d_engine* e) {
   // while the F_LY launch of the modified modes lost 14% with it: profiles/round3_r3p_ab_fill.log)
   const long by_fill = ((P.mp ? IS3D_FILL_WGS_MP : IS3D_FILL_WGS) + wgs - 1) / wgs;
   const long by_l2 = ((long)NREC * 8 * nw + IS3D_SPLIT_BYTES - 1) / IS3D_SPLIT_BYTES;
-  long nsplit = std::max(by_fill, std::min(by_l2, (long)IS3D_MAX_SPLITS));
+  const long sstride0 = (long)npT * bx * KJ * kBlock;
+  const long max_slabs = std::max(8L, std::min((long)IS3D_MAX_SPLITS, (long)(IS3D_SLAB_BYTES / 8) / std::max(1L, sstride0)));
+  long nsplit = std::max(by_fill, std::min(by_l2, max_slabs));
   if (nsplit >= 8) nsplit = (nsplit + 7) / 8 * 8;
   nsplit = std::max(1L, std::min(nsplit, max_split));
   long cps = std::max(1L, (nw + nsplit - 1) / nsplit);

@@ -51,9 +51,14 @@ constexpr int spectra_waves() {
 #endif
 template <int MODE, int KJ>
 constexpr int spectra_waves_kj() { return (KJ == 16 && MODE == GRAD) ? IS3D_SPECTRA_WAVES_KJ16 : spectra_waves<MODE>(); }
+#ifndef IS3D_WAVES_TS
+#define IS3D_WAVES_TS 0       // F_TS launches: waves per SIMD (0: as the mode's other launches)
+#endif
 // the F_FB launch (separable lanes of a modified mode: per-point exp, RTA-CE-like lane setup) stays at 2
 template <int MODE, int FLAGS, int KJ>
-constexpr int spectra_waves_f() { return (MODE >= PTM && (FLAGS & 32)) ? 2 : spectra_waves_kj<MODE, KJ>(); }
+constexpr int spectra_waves_f() {
+  return (MODE >= PTM && (FLAGS & 32)) ? 2 : (IS3D_WAVES_TS && (FLAGS & 128)) ? IS3D_WAVES_TS : spectra_waves_kj<MODE, KJ>();
+}
 // k_dndx keeps RTA-CE and the modified modes at 2 (its pT loop holds more live state: 215 VGPRs; it keeps
 // the separable fallback inline)
 template <int MODE>

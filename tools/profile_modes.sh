@@ -5,6 +5,7 @@
 #   pmcE  : FP64 VALU instruction mix (ADD / MUL / FMA / TRANS), INT32 / INT64 / CVT, FP64 flops
 #   pmcD  : wave-cycle breakdown and LDS (bank conflicts, LDS waits)
 #   pmcB/C: FETCH_SIZE / WRITE_SIZE in separate passes (TCC slot limits, MI355X_MICROARCH.md)
+#   pmcK  : scalar-cache requests / misses (the F_TS launches read their per-(cell, phi) operands by scalar loads)
 # Every pass is its own process under its own time limit; the script stops at the first failure.
 # usage: tools/profile_modes.sh <tag> <config> "<modes>" [bench args...]
 set -e
@@ -22,5 +23,6 @@ for M in $MODES; do
   timeout -s KILL 240 rocprofv3 --kernel-trace --output-format csv --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_SALU SQ_ACTIVE_INST_LDS -d "$OUT/pmcD" -o run -- "$PY" $B > "$OUT/pmcD.log" 2>&1
   timeout -s KILL 240 rocprofv3 --kernel-trace --output-format csv --pmc FETCH_SIZE -d "$OUT/pmcB" -o run -- "$PY" $B > "$OUT/pmcB.log" 2>&1
   timeout -s KILL 240 rocprofv3 --kernel-trace --output-format csv --pmc WRITE_SIZE -d "$OUT/pmcC" -o run -- "$PY" $B > "$OUT/pmcC.log" 2>&1
+  timeout -s KILL 240 rocprofv3 --kernel-trace --output-format csv --pmc SQC_DCACHE_HITS SQC_DCACHE_MISSES SQC_DCACHE_REQ -d "$OUT/pmcK" -o run -- "$PY" $B > "$OUT/pmcK.log" 2>&1
   echo "mode $M profiled"
 done

@@ -64,7 +64,7 @@ def main():
     os.makedirs(prof, exist_ok=True)
     shutil.copy(os.path.join(d, "trace", "run_kernel_stats.csv"), os.path.join(prof, "%s_kernel_stats.csv" % tag))
     out = {}
-    for sub in ("pmcA", "pmcB", "pmcC", "pmcD", "pmcE"):
+    for sub in ("pmcA", "pmcB", "pmcC", "pmcD", "pmcE", "pmcK"):
         p = os.path.join(d, sub, "run_counter_collection.csv")
         if not os.path.exists(p):
             continue
@@ -88,13 +88,22 @@ def main():
             e["clock_ghz"] = cyc / e["avg_ns_pmc_pass"]
             e["valu_issue_frac"] = 4.0 * e["SQ_ACTIVE_INST_VALU"] / (1024.0 * cyc)
     json.dump(out, open(os.path.join(prof, "%s_pmc.json" % tag), "w"), indent=1, sort_keys=True)
-    # the dominant k_spectra launch (the modified modes also run the short F_FB fallback launch)
+    # the dominant k_spectra kernel (the modified modes also run the short F_FB fallback launch); an F_TS launch
+    # over a surface whose tables exceed one chunk runs it several times per pass (engine.hip): per-pass totals =
+    # per-launch averages x launches per pass, passes = the reduction launches (one per pass)
     spec = sorted((k for k in out if k.startswith("k_spectra")), key=lambda k: -out[k].get("avg_ns_pmc_pass", 0.0))
+    passes = sum(out[k].get("launches", 0) for k in out if k.startswith("k_reduce") or k.startswith("k_dndx"))
+    if any(k.startswith("k_dndx") for k in out):
+        passes = sum(out[k].get("launches", 0) for k in out if k.startswith("k_dndx"))
     key = "%s_mode%d" % (config, mode)
+    lpp = 1.0
+    if spec and passes:
+        lpp = out[spec[0]]["launches"] / float(passes)
     if spec and "hbm_bytes_per_launch" in out[spec[0]]:
         tp = os.path.join(prof, "pmc_traffic.json")
         t = json.load(open(tp)) if os.path.exists(tp) else {}
-        t[key] = {"hbm_bytes_per_launch": out[spec[0]]["hbm_bytes_per_launch"], "tag": tag, "build_id": bid}
+        t[key] = {"hbm_bytes_per_launch": out[spec[0]]["hbm_bytes_per_launch"], "launches_per_pass": lpp,
+                  "hbm_bytes_per_pass": out[spec[0]]["hbm_bytes_per_launch"] * lpp, "tag": tag, "build_id": bid}
         json.dump(t, open(tp, "w"), indent=1, sort_keys=True)
     if spec and "valu_issue_frac" in out[spec[0]]:
         vp = os.path.join(prof, "pmc_valu.json")
@@ -109,12 +118,16 @@ def main():
             # the counter adds FMA x 2 + ADD + MUL + TRANS per WAVE-instruction (it equals that sum of the
             # per-type counters); x 64 lanes = flops (rocprofv3's derived FLOP metrics scale it the same way)
             v[key]["fp64_flops_per_launch"] = 64.0 * e["SQ_INSTS_VALU_FLOPS_FP64"]
+            v[key]["fp64_flops_per_pass"] = 64.0 * e["SQ_INSTS_VALU_FLOPS_FP64"] * lpp
         if "SQ_LDS_BANK_CONFLICT" in e:
             v[key]["lds_bank_conflict_cycles"] = e["SQ_LDS_BANK_CONFLICT"]
         if "SQ_LDS_IDX_ACTIVE" in e and "clock_ghz" in e:
             # LDS-array cycles summed over the 256 CUs / (256 x kernel cycles)
             v[key]["lds_busy_frac"] = e["SQ_LDS_IDX_ACTIVE"] / (256.0 * e["avg_ns_pmc_pass"] * e["clock_ghz"])
+        if "SQC_DCACHE_REQ" in e and e["SQC_DCACHE_REQ"] > 0:
+            v[key]["scalar_cache_miss_frac"] = e.get("SQC_DCACHE_MISSES", 0.0) / e["SQC_DCACHE_REQ"]
         v[key]["kernel_ns_pmc_pass"] = e["avg_ns_pmc_pass"]
+        v[key]["launches_per_pass"] = lpp
         json.dump(v, open(vp, "w"), indent=1, sort_keys=True)
     for k, e in sorted(out.items()):
         print(k, {c: round(v, 3) for c, v in e.items()})
