@@ -33,6 +33,12 @@
 #ifndef IS3D_CHAIN_L
 #define IS3D_CHAIN_L 32       // PTMA warm-start chains: positions per segment (k_chain_pass), at least
 #endif
+#ifndef IS3D_CHAIN_SLOTS
+#define IS3D_CHAIN_SLOTS 16384   // PTMA chain segments per pass (one wavefront each)
+#endif
+#ifndef IS3D_NEWTON_WAVES
+#define IS3D_NEWTON_WAVES 0   // PTMA Newton kernels (k_aniso, k_chain_pass): waves per SIMD to allocate for (0: compiler)
+#endif
 #ifndef IS3D_MAX_SPLITS
 #define IS3D_MAX_SPLITS 1024  // cap on k_spectra's cell splits (one output-sized slab each)
 #endif
@@ -135,7 +141,7 @@ struct AnisoArgs {
 };
 
 // one wavefront per warm-start chain: cells chain, chain + C, chain + 2C, ... (MomentumSpectra.cpp:98-107)
-__global__ __launch_bounds__(64) void k_aniso(AnisoArgs A) {
+__global__ __launch_bounds__(64, IS3D_NEWTON_WAVES ? IS3D_NEWTON_WAVES : 1) void k_aniso(AnisoArgs A) {
   const long chain = blockIdx.x;
   const int lane = threadIdx.x;
   double state[4] = {0.0, 0.0, 0.0, 0.0};
@@ -236,7 +242,7 @@ __device__ bool chain_segment_run(const ChainArgs& A, long seg, double* state, b
   return false;
 }
 
-__global__ __launch_bounds__(64) void k_chain_pass(ChainArgs A, int pass) {
+__global__ __launch_bounds__(64, IS3D_NEWTON_WAVES ? IS3D_NEWTON_WAVES : 1) void k_chain_pass(ChainArgs A, int pass) {
   const long seg = blockIdx.x, nseg = A.C * A.nspc;
   const long c = seg / A.nspc, s = seg % A.nspc;
   const int lane = threadIdx.x;
@@ -1530,7 +1536,10 @@ static int launch_begin(is3d_engine* e, double* dev_out, void* stream, long q0, 
       ca.q1 = split_chain ? std::min(q1, P) : P;
       ca.has_pred = split_chain && has_pred && ca.q0 > 0;
       const long npos = std::max(1L, ca.q1 - ca.q0);
-      ca.L = std::max((long)IS3D_CHAIN_L, (npos * ca.C + 16383) / 16384);
+      // ~IS3D_CHAIN_SLOTS segments of at least IS3D_CHAIN_L positions (sized to the GPU's resident k_chain_pass
+      // wavefronts instead -- 2048, L = 49 at 10^5 cells -- measured the same: profiles/round4_r4b_ab_newton.log)
+      const long spc_max = std::max(1L, (long)IS3D_CHAIN_SLOTS / ca.C);
+      ca.L = std::max((long)IS3D_CHAIN_L, (npos + spc_max - 1) / spc_max);
       ca.nspc = (npos + ca.L - 1) / ca.L;
       ca.npass = kChainPasses;
       if (const char* v = std::getenv("IS3D_CHAIN_PASSES")) ca.npass = std::max(1, std::min(kChainPasses, std::atoi(v)));
