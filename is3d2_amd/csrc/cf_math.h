@@ -1499,9 +1499,10 @@ IS3D_HD void sep_quad_pde_t(const SepLane& L, const dbl2* c, const dbl2* b, cons
 // RTA-CE (SEP_CE) in the same launch also takes, per (cell, phi), pe = {TE, T2} with
 // TE = -(u^x pc + u^y ps) and T2 = LC pc + LS ps (cell-only lane coefficients, sep_cell_consts):
 //   E = E0 + TE,  a (L0 + Lc pc + Ls ps) = fma(a, T2, L0')   -- five ops per point instead of eight.
-// SPHI: Phi (b[i].y) is an SGPR operand (F_TS), fma_vvs
-template <int FL, bool REG, bool OUT, bool SPHI = false>
-IS3D_HD void sep_quad_tb_t(const SepLane& L, double mT, const dbl2* b, const dbl2* pt, const dbl2* pe, double* v) {
+// SPHI: Phi (b[i].y) is an SGPR operand (F_TS), fma_vvs; BY: the baryon part b T3 (F_BY) joins the linear part
+template <int FL, bool REG, bool OUT, bool SPHI = false, bool BY = false>
+IS3D_HD void sep_quad_tb_t(const SepLane& L, double mT, const dbl2* b, const dbl2* pt, const dbl2* pe, double* v,
+                           double bary = 0.0, const double* t3 = nullptr) {
   constexpr bool needE = FL == SEP_CE;
   double pb[4], q[4], E[4];
 #pragma unroll
@@ -1517,7 +1518,9 @@ IS3D_HD void sep_quad_tb_t(const SepLane& L, double mT, const dbl2* b, const dbl
   const double rq[4] = {r01 * q[1], r01 * q[0], r23 * q[3], r23 * q[2]};
 #pragma unroll
   for (int i = 0; i < 4; i++) {
-    double in = fma(L.a, SPHI ? fma_vvs(mT, pt[i].y, b[i].y) : fma(mT, pt[i].y, b[i].y), L.S0);
+    double P = SPHI ? fma_vvs(mT, pt[i].y, b[i].y) : fma(mT, pt[i].y, b[i].y);
+    if (BY) P = fma(bary, t3[i], P);
+    double in = fma(L.a, P, L.S0);
     if (needE) in = fma(E[i], fma(L.a, pe[i].y, L.L0), in);
     double t;
     if (REG) t = 1.0 + fmax(-1.0, fmin(rq[i] * in, 1.0));
@@ -1532,8 +1535,9 @@ IS3D_HD void sep_quad_tb_t(const SepLane& L, double mT, const dbl2* b, const dbl
 //   Grad    acc += pb (1 + S),            S = S0 + mT T1 + Phi                     5 ops per point
 //   RTA-CE  acc += pb (1 + L + S / E),    L = L0 + T2, E = E0 + TE, one 1/E per four points
 // (pb = w p.dsigma f_eq; regulate clamps delta-f to [-1, 1]; outflow drops points with pb <= 0).
-template <int FL, bool REG, bool OUT, bool SPHI = false>
-IS3D_HD void sep_quad_tb_tail_t(const SepLane& L, double mT, const dbl2* b, const dbl2* pt, const dbl2* pe, double* acc) {
+template <int FL, bool REG, bool OUT, bool SPHI = false, bool BY = false>
+IS3D_HD void sep_quad_tb_tail_t(const SepLane& L, double mT, const dbl2* b, const dbl2* pt, const dbl2* pe, double* acc,
+                                double bary = 0.0, const double* t3 = nullptr) {
   constexpr bool needE = FL == SEP_CE;
   double rE[4] = {0.0, 0.0, 0.0, 0.0};
   if (needE) {
@@ -1549,7 +1553,8 @@ IS3D_HD void sep_quad_tb_tail_t(const SepLane& L, double mT, const dbl2* b, cons
   for (int i = 0; i < 4; i++) {
     double pb = fma(L.D0, b[i].x, L.escw * pt[i].x);
     if (OUT) pb = (pb <= 0.0) ? 0.0 : pb;
-    const double P = SPHI ? fma_vvs(mT, pt[i].y, b[i].y) : fma(mT, pt[i].y, b[i].y);
+    double P = SPHI ? fma_vvs(mT, pt[i].y, b[i].y) : fma(mT, pt[i].y, b[i].y);
+    if (BY) P = fma(bary, t3[i], P);
     double t;
     if (REG) {
       const double S = P + L.S0;

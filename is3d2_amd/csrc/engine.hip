@@ -1051,6 +1051,7 @@ static int device_jonah_table(is3d_engine* e, const double* r2, const double* w2
 struct SpectraPlan {
   int KJ, njb, nq, nqmax, tb, ly, t8, tile;
   int ts;                     // F_TS: the F_TB launch with the per-(cell, phi) operands from k_phitab's table
+  int by;                     // F_BY: ... with include_baryon (T3 rows)
   int mp, npw;                // F_MP: pT values per workgroup (1 otherwise)
   size_t shmem;
   size_t shmem_fb;            // modified modes: the F_FB launch (8-cell tiles, per-lane y-term rows, no q tables)
@@ -1073,7 +1074,10 @@ static SpectraPlan spectra_plan(const is3d_engine* e) {
     // V^mu and alphaB are only packed when include_baryon && include_baryondiff_deltaf (prep_grad_ce), and
     // df_eval leaves c1 = c3 = 0 without baryons); needs phi blocks of fours and at most kTbQ rows per
     // workgroup
-    P.tb = (IS3D_GRAD_TB && (mode == GRAD || (mode == CE && IS3D_CE_TB)) && !e->p.include_baryon &&
+    // with include_baryon only as F_TS + F_BY (one phi block of 24 or 32 points: the baryon part of the linear
+    // coefficients comes from the table as T3)
+    const bool ts_shape = IS3D_TS && IS3D_TS_BY && P.njb == 1 && (KJ == 24 || KJ == 32);
+    P.tb = (IS3D_GRAD_TB && (mode == GRAD || (mode == CE && IS3D_CE_TB)) && (!e->p.include_baryon || ts_shape) &&
             KJ % 4 == 0 && P.nqmax <= kTbQ) ? F_TB : 0;
   };
   int kTile = (mode >= PTM) ? IS3D_KTILE_MOD : is3d::kern::kTile;   // spectra_tile<MODE, FLAGS>()
@@ -1162,6 +1166,7 @@ static SpectraPlan spectra_plan(const is3d_engine* e) {
     }
   }
   P.ts = ts_ok() ? F_TS : 0;
+  P.by = (P.ts && e->p.include_baryon) ? F_BY : 0;
   if (P.ts && kTile != IS3D_KTILE_TS) {     // spectra_tile<MODE, F_TB | F_TS>()
     kTile = IS3D_KTILE_TS;
     P.shmem = lds_bytes(P.nqmax);
@@ -1677,7 +1682,7 @@ static int launch_end(is3d_engine* e) {
   sa.npw = P.npw;
   sa.regulate = e->p.regulate_deltaf; sa.outflow = e->p.outflow; sa.dim = dim; sa.op = 1;
   const size_t shmem = P.shmem;
-  const int tb = P.tb | P.ly | P.t8 | P.mp | P.ts;
+  const int tb = P.tb | P.ly | P.t8 | P.mp | P.ts | P.by;
   const int kflags = (e->p.regulate_deltaf ? F_REG : 0) | (e->p.outflow ? F_OUT : 0) | tb;
   if (P.ts) {
     // F_TS: k_phitab writes the per-(cell, pT, phi) rows of a chunk of whole cell splits (at most
@@ -1685,7 +1690,7 @@ static int launch_end(is3d_engine* e) {
     // chunks (config 4: 61 GB of rows) alternate between the launch stream and a side stream with a table buffer
     // each, so the next chunk's k_phitab and the first workgroups of its k_spectra fill the CUs the previous
     // launch's last workgroups leave idle (config 4: 11 chunks ran 2811 ms back to back, one 61 GB chunk 2739 ms)
-    const long rw = phitab_row(mode, KJ);
+    const long rw = phitab_row(mode, KJ, P.by != 0);
     const long per_split = cps * (long)npT * rw;
     const long whole = per_split * nsplit * 8;          // bytes of the whole surface's rows
     const long budget = whole <= IS3D_PHITAB_ONE ? whole : (long)IS3D_PHITAB_BYTES;
@@ -1707,7 +1712,7 @@ static int launch_end(is3d_engine* e) {
       double* tab = (ic & 1) ? e->d_phtab2 : e->d_phtab;
       PhiTabArgs ta{};
       ta.rec = rec_w; ta.c0 = c0; ta.nc = ncc; ta.pT = e->d_pT; ta.cphi = e->d_cphi; ta.sphi = e->d_sphi;
-      ta.npT = npT; ta.nphi = nphi; ta.nphp = KJ; ta.tab = tab; ta.phn = phn;
+      ta.npT = npT; ta.nphi = nphi; ta.nphp = KJ; ta.tab = tab; ta.phn = phn; ta.by = P.by != 0;
       SpecArgs sc = sa;
       sc.split0 = (int)s0; sc.nsplit = (int)ns; sc.phtab = tab; sc.phn = phn; sc.phc0 = c0; sc.phrow = (int)rw;
       const dim3 grid((unsigned)(wgs * ns));

@@ -118,12 +118,18 @@ struct SpecArgs {
 // SGPRs, instead of broadcast ds_read_b128s from LDS tables the workgroup builds; LDS keeps only the per-(cell, q
 // row, phi) T1 rows (one ds_read_b128 per two points).  The F_TB tail loop read two ds_read_b128 (8 LDS-array
 // cycles) per 5 VALU ops, so four SIMDs in it were bound by the CU's LDS array, not by the FP64 pipe
-constexpr int F_REG = 1, F_OUT = 2, F_TB = 4, F_LY = 8, F_T8 = 16, F_FB = 32, F_MP = 64, F_TS = 128;
+// F_BY (with F_TS, include_baryon = 1): the lanes' baryon part of the linear delta-f coefficients,
+// b (SCB pc + SSB ps) per (cell, phi) (R_SCB / R_SSB: c1 / c3 and V^mu terms, prep_grad_ce), comes as one more table
+// operand T3: a S = fma(a, fma(b, T3, fma(mT, T1, Phi)), S0') -- the F_TB factorisation needed R_SCB = R_SSB = 0
+constexpr int F_REG = 1, F_OUT = 2, F_TB = 4, F_LY = 8, F_T8 = 16, F_FB = 32, F_MP = 64, F_TS = 128, F_BY = 256;
 constexpr int kTbQ = 4;
-// doubles per F_TS table row of one (cell, pT): {b', Phi}[nphp] | PD[nphp] | RTA-CE {TE, T2}[nphp]
-__host__ __device__ constexpr int phitab_row(int mode, int nphp) { return (mode == CE ? 5 : 3) * nphp; }
+// doubles per F_TS table row of one (cell, pT): {b', Phi}[nphp] | PD[nphp] | RTA-CE {TE, T2}[nphp] | F_BY T3[nphp]
+__host__ __device__ constexpr int phitab_row(int mode, int nphp, bool by = false) { return ((mode == CE ? 5 : 3) + (by ? 1 : 0)) * nphp; }
 #ifndef IS3D_TS
 #define IS3D_TS 1             // F_TB launches with one phi block take the scalar-table form (F_TS)
+#endif
+#ifndef IS3D_TS_BY
+#define IS3D_TS_BY 1          // ... with include_baryon too (F_BY); otherwise the per-lane launch
 #endif
 #ifndef IS3D_PHITAB_ONE
 #define IS3D_PHITAB_ONE (8L << 30)     // F_TS tables up to this size are written and integrated in one chunk
@@ -228,6 +234,7 @@ struct PhiTabArgs {
   const double *pT, *cphi, *sphi;
   int npT, nphi, nphp;
   double* tab; long phn;                    // rows per pT plane (>= nc)
+  int by;                                   // F_BY: rows carry T3
 };
 
 template <int MODE>
@@ -420,26 +427,30 @@ __device__ __forceinline__ void sep_phi_loop_tb_tail(const SepLane& L, double mT
 // RTA-CE's {TE, T2} by scalar loads from the cell's k_phitab row G (wave-uniform address: SGPR operands) and T1
 // from the lane's LDS row (16-byte aligned pairs: one ds_read_b128 per two points)
 template <int MODE, int FLAGS, int KJ, bool TAIL>
-__device__ __forceinline__ void sep_phi_loop_ts(const SepLane& L, double mT, cs_sptr G, const dbl2* T1, double* acc) {
+__device__ __forceinline__ void sep_phi_loop_ts(const SepLane& L, double mT, double bary, cs_sptr G, const dbl2* T1,
+                                                double* acc) {
   constexpr int FL = (MODE == GRAD) ? SEP_GRAD : SEP_CE;
-  constexpr bool REG = (FLAGS & F_REG) != 0, OUT = (FLAGS & F_OUT) != 0;
+  constexpr bool REG = (FLAGS & F_REG) != 0, OUT = (FLAGS & F_OUT) != 0, BY = (FLAGS & F_BY) != 0;
   static_assert(KJ % 4 == 0, "F_TS needs phi blocks of fours");
+  constexpr int O3 = (MODE == CE ? 5 : 3) * KJ;        // T3 slot of the row (F_BY)
 #pragma unroll
   for (int jj = 0; jj < KJ; jj += 4) {
     dbl2 b[4], pt[4], pe[4];
+    double t3[4];
     const dbl2 t01 = T1[jj >> 1], t23 = T1[(jj >> 1) + 1];
 #pragma unroll
     for (int i = 0; i < 4; i++) {
       b[i].x = G[2 * (jj + i)]; b[i].y = G[2 * (jj + i) + 1];
       pt[i].x = G[2 * KJ + jj + i];
       if (FL == SEP_CE) { pe[i].x = G[3 * KJ + 2 * (jj + i)]; pe[i].y = G[3 * KJ + 2 * (jj + i) + 1]; }
+      t3[i] = BY ? G[O3 + jj + i] : 0.0;
     }
     pt[0].y = t01.x; pt[1].y = t01.y; pt[2].y = t23.x; pt[3].y = t23.y;
     if (TAIL) {
-      sep_quad_tb_tail_t<FL, REG, OUT, true>(L, mT, b, pt, pe, acc + jj);
+      sep_quad_tb_tail_t<FL, REG, OUT, true, BY>(L, mT, b, pt, pe, acc + jj, bary, t3);
     } else {
       double v[4];
-      sep_quad_tb_t<FL, REG, OUT, true>(L, mT, b, pt, pe, v);
+      sep_quad_tb_t<FL, REG, OUT, true, BY>(L, mT, b, pt, pe, v, bary, t3);
 #pragma unroll
       for (int i = 0; i < 4; i++) acc[jj + i] += v[i];
     }
@@ -861,7 +872,7 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
       if constexpr (TS && IS3D_TS_PF) {
         // the k_phitab rows of that tile (contiguous: cells x RW doubles of this pT) into L2, so the scalar loads of
         // its first points miss the K$ into L2 instead of HBM; one dword per 128-byte line, landing in a dummy LDS row
-        constexpr int RW = phitab_row(MODE, KJ);
+        constexpr int RW = phitab_row(MODE, KJ, (FLAGS & F_BY) != 0);
         const long cbp = tile_cb(i + kRecBufs - 1);
         const long nb = (min(c_end, cbp + kTile) - cbp) * RW * 8;
         const char* src = (const char*)(A.phtab + ((long)ipt * A.phn + (cbp - A.phc0)) * RW);
@@ -928,11 +939,11 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
           if (L.skip) continue;
           if constexpr (TS) {
             // this cell's k_phitab row (wave-uniform: ipt, the tile and t are) and the lane's T1 row
-            constexpr int RW = phitab_row(MODE, KJ);          // one phi block: nphp = KJ
+            constexpr int RW = phitab_row(MODE, KJ, (FLAGS & F_BY) != 0);   // one phi block: nphp = KJ
             const long go = ((long)ipt * A.phn + (cbx - A.phc0)) * RW + t * RW;
             const dbl2* T1 = (const dbl2*)(s_t1 + ((long)t * nqw + row) * prow2);
-            if (IS3D_TAIL && L.tail) sep_phi_loop_ts<MODE, FLAGS, KJ, true>(L, mT, (cs_sptr)A.phtab + go, T1, acc);
-            else if (L.fast) sep_phi_loop_ts<MODE, FLAGS, KJ, false>(L, mT, (cs_sptr)A.phtab + go, T1, acc);
+            if (IS3D_TAIL && L.tail) sep_phi_loop_ts<MODE, FLAGS, KJ, true>(L, mT, baryon, (cs_sptr)A.phtab + go, T1, acc);
+            else if (L.fast) sep_phi_loop_ts<MODE, FLAGS, KJ, false>(L, mT, baryon, (cs_sptr)A.phtab + go, T1, acc);
             else sep_phi_loop<MODE, FLAGS, false, KJ>(L, CSl, (const dbl2*)(A.phtab + go), acc);
           } else if constexpr (TB) {
             const dbl2* PT = s_pt + ((long)t * nqw + row) * prow;
@@ -1222,7 +1233,7 @@ __global__ __launch_bounds__(256) void k_phitab(PhiTabArgs A) {
   __shared__ double s_etab[kExpTabN];
   for (int i = threadIdx.x; i < kExpTabN; i += 256) s_etab[i] = kExp2Tab[i];
   __syncthreads();
-  const int rw = phitab_row(MODE, A.nphp);
+  const int rw = phitab_row(MODE, A.nphp, A.by != 0);
   const long total = (long)A.npT * A.nc * A.nphp;
   for (long idx = (long)blockIdx.x * 256 + threadIdx.x; idx < total; idx += (long)gridDim.x * 256) {
     const int j = (int)(idx % A.nphp);
@@ -1242,6 +1253,7 @@ __global__ __launch_bounds__(256) void k_phitab(PhiTabArgs A) {
       row[3 * A.nphp + 2 * j] = -fma(R[R_UX], cs.x, R[R_UY] * cs.y);
       row[3 * A.nphp + 2 * j + 1] = fma(R[R_LC], cs.x, R[R_LS] * cs.y);
     }
+    if (A.by) row[(MODE == CE ? 5 : 3) * A.nphp + j] = fma(R[R_SCB], cs.x, R[R_SSB] * cs.y);   // T3 (F_BY)
   }
 }
 
@@ -1299,6 +1311,15 @@ void launch_spectra_kj(dim3 grid, size_t shmem, hipStream_t st, const SpecArgs& 
     }
   }
   if constexpr ((MODE == GRAD || MODE == CE) && (KJ == 24 || KJ == 32)) {
+    if ((flags & F_TS) && (flags & F_TB) && (flags & F_BY)) {
+      switch (flags & 3) {
+        case 0: hipLaunchKernelGGL((k_spectra<MODE, 388, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+        case 1: hipLaunchKernelGGL((k_spectra<MODE, 389, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+        case 2: hipLaunchKernelGGL((k_spectra<MODE, 390, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+        default: hipLaunchKernelGGL((k_spectra<MODE, 391, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+      }
+      return;
+    }
     if ((flags & F_TS) && (flags & F_TB)) {
       switch (flags & 3) {
         case 0: hipLaunchKernelGGL((k_spectra<MODE, 132, KJ>), grid, dim3(kBlock), shmem, st, a); break;
