@@ -25,7 +25,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def short(name):
-    for k in ("k_spectra", "k_reduce", "k_prep", "k_aniso", "k_famod_b", "k_renorm", "k_df_eval"):
+    for k in ("k_spectra", "k_dndx", "k_phitab", "k_reduce", "k_prep", "k_aniso", "k_chain_pass", "k_famod_b", "k_renorm", "k_df_eval"):
         if k in name:
             return name[name.index(k):].split("(")[0]
     return name.split("(")[0][:60]
@@ -91,9 +91,11 @@ def main():
     # the dominant k_spectra kernel (the modified modes also run the short F_FB fallback launch); an F_TS launch
     # over a surface whose tables exceed one chunk runs it several times per pass (engine.hip): per-pass totals =
     # per-launch averages x launches per pass, passes = the reduction launches (one per pass)
-    spec = sorted((k for k in out if k.startswith("k_spectra")), key=lambda k: -out[k].get("avg_ns_pmc_pass", 0.0))
-    passes = sum(out[k].get("launches", 0) for k in out if k.startswith("k_reduce") or k.startswith("k_dndx"))
-    if any(k.startswith("k_dndx") for k in out):
+    # (operation 0: k_dndx, one launch per pass)
+    dom = "k_dndx" if any(k.startswith("k_dndx") for k in out) else "k_spectra"
+    spec = sorted((k for k in out if k.startswith(dom)), key=lambda k: -out[k].get("avg_ns_pmc_pass", 0.0))
+    passes = sum(out[k].get("launches", 0) for k in out if k.startswith("k_reduce"))
+    if dom == "k_dndx":
         passes = sum(out[k].get("launches", 0) for k in out if k.startswith("k_dndx"))
     key = "%s_mode%d" % (config, mode)
     lpp = 1.0
