@@ -1958,7 +1958,8 @@ extern "C" int is3d_calculate_dN_dX(is3d_engine* e, double* dN_taudtaudy, double
     da.npart = nc; da.npT = npT; da.nphi = nphi; da.nk = nk; da.nl = nl; da.nq = nk * nl; da.njb = njb; da.dim = dim;
     const size_t nphp = (size_t)njb * KJ;
     const size_t shmem = sizeof(double) * ((size_t)kTile * NREC + 2 * nphp + 2 * nphp + nphp + 3 * (size_t)kTile * nphp +
-                                           (size_t)kTile * kBlock + (size_t)(nk + 2 * nl) + (size_t)kTile * da.nq * kYRowLY + kExpTabN);
+                                           (size_t)kTile * kBlock + (size_t)(nk + 2 * nl) + (size_t)kTile * da.nq * kYRowLY + kExpTabN +
+                                           (mode == PTM ? (size_t)kTile * kBlock : 0));
     if (shmem > 160 * 1024) return e->fail(IS3D_ERR_ARG, "momentum grid too large for the LDS tile");
     const long nwg = (long)da.nbx * da.nchunk;
     if (nwg > 0x7fffffffL) return e->fail(IS3D_ERR_ARG, "surface too large for one dN/dX launch");

@@ -1095,6 +1095,9 @@ __global__ __launch_bounds__(kBlock, dndx_waves<MODE>()) void k_dndx(DndxArgs A)
   // launch past the LDS of three workgroups per CU (k_dndx 647 -> 784 ms)
   double* s_y = s_grid + A.nk + 2 * A.nl;                 // [kTile][nq][kYRowLY]
   double* s_etab = s_y + (long)kTile * A.nq * kYRowLY;    // [kExpTabN] exp_tab's 2^(j/kExpTabN)
+  // PTM: each lane's renormalisation factor of the tile's cells, loaded once per tile instead of once per pT (the
+  // per-pT loads re-read the [cell][class] array 48 times: 7.3e11 B per config-2 pass)
+  double* s_rn = s_etab + kExpTabN;                        // [kTile][kBlock]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   for (int i = tid; i < kExpTabN; i += kBlock) s_etab[i] = kExp2Tab[i];
@@ -1129,6 +1132,10 @@ __global__ __launch_bounds__(kBlock, dndx_waves<MODE>()) void k_dndx(DndxArgs A)
     for (int i = tid; i < nt * NREC; i += kBlock) s_rec[i] = A.rec[cb * NREC + i];
 #pragma unroll
     for (int t = 0; t < kTile; t++) s_red[t * kBlock + tid] = 0.0;
+    if (MODE == PTM && active) {
+      const int rc = A.rcls[s];
+      for (int t = 0; t < nt; t++) s_rn[t * kBlock + tid] = A.renorm[(cb + t) * A.nrcls + rc];
+    }
     __syncthreads();
     for (int idx = tid; idx < nt * A.nq; idx += kBlock) {
       const int t = idx / A.nq, q = idx % A.nq;
@@ -1168,14 +1175,13 @@ __global__ __launch_bounds__(kBlock, dndx_waves<MODE>()) void k_dndx(DndxArgs A)
       }
       __syncthreads();
       if (!active) continue;
-      const int rc = (MODE == PTM) ? A.rcls[s] : 0;      // the lane's renormalisation class
       for (int t = 0; t < nt; t++) {
         const double* R = s_rec + t * NREC;
         const double kind = R[R_KIND];
         if (kind == 0.0) continue;
         double rn_abs = R[R_RENORM];
         if (MODE == PTM || MODE == PTB) {
-          const double rn = (MODE == PTM) ? A.renorm[(cb + t) * A.nrcls + rc] : R[R_RENORM];
+          const double rn = (MODE == PTM) ? s_rn[t * kBlock + tid] : R[R_RENORM];
           if (!isfinite(rn)) continue;    // cell skipped for this species (SpacetimeDistribution.cpp:972-976)
           rn_abs = fabs(rn);
         }
