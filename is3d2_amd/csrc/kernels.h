@@ -193,6 +193,14 @@ __host__ __device__ constexpr int phitab_row(int mode, int nphp, bool by = false
 #ifndef IS3D_TS_PF
 #define IS3D_TS_PF 1          // F_TS: the table rows of tile i + 2 are touched into L2 (LDS-DMA of one dword per 128 B)
 #endif
+// F_TS: the operands of the next four loaded before this four's arithmetic (bit 1 tail lanes, bit 2 other
+// lanes), per mode: RTA-CE 260.8 -> 250.8 ms (config 2), 2663 -> 2511 ms (config 4); Grad 167.5 -> 168.9 ms (r4d)
+#ifndef IS3D_TS_AHEAD_CE
+#define IS3D_TS_AHEAD_CE 1
+#endif
+#ifndef IS3D_TS_AHEAD_GRAD
+#define IS3D_TS_AHEAD_GRAD 1
+#endif
 #ifndef IS3D_TAIL_PD
 #define IS3D_TAIL_PD 0        // Grad tail lanes: PD table + scalar {pc, ps} instead of {PD, T1}: 2.2% slower (r2d A/B)
 #endif
@@ -433,19 +441,38 @@ __device__ __forceinline__ void sep_phi_loop_ts(const SepLane& L, double mT, dou
   constexpr bool REG = (FLAGS & F_REG) != 0, OUT = (FLAGS & F_OUT) != 0, BY = (FLAGS & F_BY) != 0;
   static_assert(KJ % 4 == 0, "F_TS needs phi blocks of fours");
   constexpr int O3 = (MODE == CE ? 5 : 3) * KJ;        // T3 slot of the row (F_BY)
-#pragma unroll
-  for (int jj = 0; jj < KJ; jj += 4) {
-    dbl2 b[4], pt[4], pe[4];
-    double t3[4];
+  // operands of one four: scalar loads from G and the T1 pairs from LDS (both counted by lgkmcnt, the scalar
+  // ones out of order: a wait for either is a wait for all, so the next four's loads go out before this four's
+  // arithmetic -- AHEAD -- instead of just before their use)
+  struct Four { dbl2 b[4], pt[4], pe[4]; double t3[4]; };
+  auto load = [&](int jj, Four& f) {
     const dbl2 t01 = T1[jj >> 1], t23 = T1[(jj >> 1) + 1];
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-      b[i].x = G[2 * (jj + i)]; b[i].y = G[2 * (jj + i) + 1];
-      pt[i].x = G[2 * KJ + jj + i];
-      if (FL == SEP_CE) { pe[i].x = G[3 * KJ + 2 * (jj + i)]; pe[i].y = G[3 * KJ + 2 * (jj + i) + 1]; }
-      t3[i] = BY ? G[O3 + jj + i] : 0.0;
+      f.b[i].x = G[2 * (jj + i)]; f.b[i].y = G[2 * (jj + i) + 1];
+      f.pt[i].x = G[2 * KJ + jj + i];
+      if (FL == SEP_CE) { f.pe[i].x = G[3 * KJ + 2 * (jj + i)]; f.pe[i].y = G[3 * KJ + 2 * (jj + i) + 1]; }
+      f.t3[i] = BY ? G[O3 + jj + i] : 0.0;
     }
-    pt[0].y = t01.x; pt[1].y = t01.y; pt[2].y = t23.x; pt[3].y = t23.y;
+    f.pt[0].y = t01.x; f.pt[1].y = t01.y; f.pt[2].y = t23.x; f.pt[3].y = t23.y;
+  };
+  constexpr bool AHEAD = (((MODE == GRAD) ? IS3D_TS_AHEAD_GRAD : IS3D_TS_AHEAD_CE) >> (TAIL ? 0 : 1)) & 1;
+  Four fq[2];
+  if (AHEAD) load(0, fq[0]);
+#pragma unroll
+  for (int jj = 0; jj < KJ; jj += 4) {
+    Four& cur = fq[AHEAD ? (jj >> 2) & 1 : 0];
+    if (AHEAD) {
+      // wait for this four's operands (lgkmcnt(0)) before the next four's loads go out, and keep the compiler
+      // from moving them (left alone, it issued the loads of two fours before one wait)
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+      __builtin_amdgcn_sched_barrier(0);
+      if (jj + 4 < KJ) load(jj + 4, fq[((jj >> 2) + 1) & 1]);
+      __builtin_amdgcn_sched_barrier(0);
+    } else {
+      load(jj, cur);
+    }
+    const dbl2* b = cur.b; const dbl2* pt = cur.pt; const dbl2* pe = cur.pe; const double* t3 = cur.t3;
     if (TAIL) {
       sep_quad_tb_tail_t<FL, REG, OUT, true, BY>(L, mT, b, pt, pe, acc + jj, bary, t3);
     } else {
