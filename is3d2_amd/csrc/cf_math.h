@@ -1108,6 +1108,7 @@ struct SepLane {
   double x, Zc, Zs;            // slow path: feq = 1/(exp(x - Zc pc - Zs ps) + sign)
   int skip, fast;
   int tail;                    // Boltzmann tail (sep_setup, allow_tail): a + ssc b' == a at every phi point
+  int near;                    // near the tail (sep_setup, allow_near): ssc b' / a <= e^-kNearX at every phi point
   double escw;                 // 2^-k w_eta (PD-table scale)
 };
 
@@ -1115,6 +1116,10 @@ struct SepLane {
 // 1 - sign f_eq == 1 in FP64 exactly (the sum rounds back to the larger term); a lane whose smallest
 // exponent over phi exceeds it needs no per-point reciprocal at all
 static constexpr double kTailX = 37.5;
+// near-tail bound: for an exponent x >= kNearX, u = sign e^-x <= 1.6e-8, so 1 / (1 + u) = 1 - u to u^2 <= 2.4e-16
+// (the rounding of the reciprocal it replaces: rcp1, ~2e-15); a Grad lane whose smallest exponent exceeds it
+// takes (1 - u) (1 + (1 - u) S) = (1 + S) - u (1 + 2 S) per point, no reciprocal (sep_quad_tb_near_t)
+static constexpr double kNearX = 18.0;
 
 // 1/d for finite normal d: v_rcp_f64 (measured max rel. error 4.5e-8 on gfx950) + one
 // Newton step (~2e-15); IEEE division on the host.  Callers guarantee d is finite.
@@ -1150,7 +1155,8 @@ IS3D_HD bool sep_skips(const double* R, const double* Y, double mT, double pT, d
 }
 
 IS3D_HD void sep_setup(int flavor, const double* R, const double* Y, double mT, double mT2, double m2, double mTb,
-                       double pT, double sign, double baryon, const double* etab, SepLane& L, int allow_tail = 0) {
+                       double pT, double sign, double baryon, const double* etab, SepLane& L, int allow_tail = 0,
+                       int allow_near = 0) {
   L.sign = sign;
   L.x = fma(mT, Y[Y_AT], -baryon * R[R_CHEM]);
   const double zb = pT * R[R_ZB];                 // >= max_j |pT B_j / T|
@@ -1175,6 +1181,15 @@ IS3D_HD void sep_setup(int flavor, const double* R, const double* Y, double mT, 
     L.tail = t;
   }
 #endif
+  // allow_near (with allow_tail; 2 = per wavefront on the device, as the tail vote): near-tail lanes
+  L.near = (allow_near && !L.tail && xs > kNearX) ? 1 : 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (allow_near == 2) {
+    int t = __all(xs > kNearX) && !L.tail;
+    asm volatile("" : "+v"(t));
+    L.near = t;
+  }
+#endif
   const int k = (L.fast && xs > 150.0) ? (int)((xs - 150.0) * 1.4426950408889634) : 0;
   L.a = L.fast ? exp_tab(exp_tab_coef(), etab, xs * kInvLn2xN, k) : 0.0;
   const double esc = ldexp(1.0, -k);
@@ -1183,16 +1198,17 @@ IS3D_HD void sep_setup(int flavor, const double* R, const double* Y, double mT, 
   if (!L.fast) { L.Zc = R[R_UX] * R[R_INVT]; L.Zs = R[R_UY] * R[R_INVT]; } else { L.Zc = L.Zs = 0.0; }
   L.D0 = esc * (mT * Y[Y_D]); L.Dc = esc * Y[Y_WDX]; L.Ds = esc * Y[Y_WDY];
   // fast lanes carry the delta-f coefficients pre-multiplied by a (see sep_fast_tail)
-  const double sa = (L.fast && !L.tail) ? L.a : 1.0;
+  const double sa = (L.fast && !L.tail && !L.near) ? L.a : 1.0;
   L.S0 = sa * fma(mT2, Y[Y_S2], fma(mTb, Y[Y_S1], m2 * R[R_S0M2]));
   L.Sc = sa * fma(mT, Y[Y_SC1], baryon * R[R_SCB]);
   L.Ss = sa * fma(mT, Y[Y_SS1], baryon * R[R_SSB]);
   L.E0 = mT * Y[Y_A]; L.Ec = -R[R_UX]; L.Es = -R[R_UY];
   L.L0 = sa * fma(mT, Y[Y_L1], baryon * R[R_L0B]); L.Lc = sa * R[R_LC]; L.Ls = sa * R[R_LS];
   L.c0 = (flavor == SEP_PTB) ? R[R_DZ] - 3.0 * R[R_DLAM] : 0.0;
-  if (L.tail) {   // f_eq = b' / a: fold 1/a into the p.dsigma coefficients (both carry the same 2^-k)
+  if (L.tail || L.near) {   // f_eq = b' / a: fold 1/a into the p.dsigma coefficients (both carry the same 2^-k)
     const double ra = rcp1(L.a);
     L.D0 *= ra; L.Dc *= ra; L.Ds *= ra; L.escw *= ra;
+    if (L.near) L.ssc *= ra;         // u = ssc b' (sep_quad_tb_near_t)
   }
 }
 
@@ -1563,6 +1579,25 @@ IS3D_HD void sep_quad_tb_tail_t(const SepLane& L, double mT, const dbl2* b, cons
     } else {   // 1 + S0 and 1 + L0 are lane constants (hoisted by the compiler)
       t = needE ? fma(P + L.S0, rE[i], (1.0 + L.L0) + pe[i].y) : P + (1.0 + L.S0);
     }
+    acc[i] = fma(pb, t, acc[i]);
+  }
+}
+
+// sep_quad_tb_t for a near-tail Grad lane without regulate (sep_setup allow_near, L.near = 1: 1/a folded into
+// D0 / escw, delta-f coefficients unscaled, L.ssc = sign 2^-k / a): with u = ssc b' <= e^-kNearX,
+// f_eq = (b'/a) / (1 + u) and 1 - sign f_eq = 1 / (1 + u), so a point is
+//   pb (1 - u) (1 + (1 - u) S) = pb ((1 + S) - u (1 + 2 S))   (to u^2)          8 ops per point instead of ~11
+template <bool OUT, bool SPHI = false, bool BY = false>
+IS3D_HD void sep_quad_tb_near_t(const SepLane& L, double mT, const dbl2* b, const dbl2* pt, double* acc,
+                                double bary = 0.0, const double* t3 = nullptr) {
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    double pb = fma(L.D0, b[i].x, L.escw * pt[i].x);
+    if (OUT) pb = (pb <= 0.0) ? 0.0 : pb;
+    double P = SPHI ? fma_vvs(mT, pt[i].y, b[i].y) : fma(mT, pt[i].y, b[i].y);
+    if (BY) P = fma(bary, t3[i], P);
+    const double S1 = P + (1.0 + L.S0);                    // 1 + S
+    const double t = fma(-(L.ssc * b[i].x), fma(2.0, S1, -1.0), S1);
     acc[i] = fma(pb, t, acc[i]);
   }
 }

@@ -201,6 +201,9 @@ __host__ __device__ constexpr int phitab_row(int mode, int nphp, bool by = false
 #ifndef IS3D_TS_AHEAD_GRAD
 #define IS3D_TS_AHEAD_GRAD 1
 #endif
+#ifndef IS3D_NEAR
+#define IS3D_NEAR 1           // F_TS Grad: near-tail lanes (sep_quad_tb_near_t, kNearX), no reciprocal per point
+#endif
 #ifndef IS3D_TAIL_PD
 #define IS3D_TAIL_PD 0        // Grad tail lanes: PD table + scalar {pc, ps} instead of {PD, T1}: 2.2% slower (r2d A/B)
 #endif
@@ -434,7 +437,7 @@ __device__ __forceinline__ void sep_phi_loop_tb_tail(const SepLane& L, double mT
 // F_TS lanes: the F_TB fours (sep_quad_tb_t / sep_quad_tb_tail_t, the same arithmetic) with {b', Phi}, PD and
 // RTA-CE's {TE, T2} by scalar loads from the cell's k_phitab row G (wave-uniform address: SGPR operands) and T1
 // from the lane's LDS row (16-byte aligned pairs: one ds_read_b128 per two points)
-template <int MODE, int FLAGS, int KJ, bool TAIL>
+template <int MODE, int FLAGS, int KJ, bool TAIL, bool NEAR = false>
 __device__ __forceinline__ void sep_phi_loop_ts(const SepLane& L, double mT, double bary, cs_sptr G, const dbl2* T1,
                                                 double* acc) {
   constexpr int FL = (MODE == GRAD) ? SEP_GRAD : SEP_CE;
@@ -456,7 +459,7 @@ __device__ __forceinline__ void sep_phi_loop_ts(const SepLane& L, double mT, dou
     }
     f.pt[0].y = t01.x; f.pt[1].y = t01.y; f.pt[2].y = t23.x; f.pt[3].y = t23.y;
   };
-  constexpr bool AHEAD = (((MODE == GRAD) ? IS3D_TS_AHEAD_GRAD : IS3D_TS_AHEAD_CE) >> (TAIL ? 0 : 1)) & 1;
+  constexpr bool AHEAD = (((MODE == GRAD) ? IS3D_TS_AHEAD_GRAD : IS3D_TS_AHEAD_CE) >> (TAIL || NEAR ? 0 : 1)) & 1;
   Four fq[2];
   if (AHEAD) load(0, fq[0]);
 #pragma unroll
@@ -473,7 +476,10 @@ __device__ __forceinline__ void sep_phi_loop_ts(const SepLane& L, double mT, dou
       load(jj, cur);
     }
     const dbl2* b = cur.b; const dbl2* pt = cur.pt; const dbl2* pe = cur.pe; const double* t3 = cur.t3;
-    if (TAIL) {
+    if constexpr (NEAR) {
+      static_assert(FL == SEP_GRAD && !REG, "near-tail fours: Grad without regulate");
+      sep_quad_tb_near_t<OUT, true, BY>(L, mT, b, pt, acc + jj, bary, t3);
+    } else if (TAIL) {
       sep_quad_tb_tail_t<FL, REG, OUT, true, BY>(L, mT, b, pt, pe, acc + jj, bary, t3);
     } else {
       double v[4];
@@ -961,8 +967,12 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
         if constexpr (!MODMAIN) {     // Grad / RTA-CE lanes (sep throughout), the F_FB launch's separable lanes
           if ((IS3D_EARLY_SKIP & 1) && sep_skips(R, Y, mT, pT, baryon)) continue;
           SepLane L;
+          // near-tail lanes: F_TS Grad launches without regulate or baryon (IS3D_NEAR: config 2 166.2 -> 162.7 ms;
+          // the F_BY launch, config 3, 176.8 -> 179.5 ms: off there)
+          constexpr bool NEAR = TS && MODE == GRAD && !(FLAGS & (F_REG | F_BY)) && IS3D_NEAR && IS3D_TAIL && IS3D_TAIL_WAVE;
           sep_setup(sep_flavor(MODE), R, Y, mT, mT2, m2, mTb, pT, sign, baryon, s_etab, L,
-                    ((TB && IS3D_TAIL && (MODE == GRAD || IS3D_TAIL_CE || TS)) || PDT) ? (IS3D_TAIL_WAVE ? 2 : 1) : 0);
+                    ((TB && IS3D_TAIL && (MODE == GRAD || IS3D_TAIL_CE || TS)) || PDT) ? (IS3D_TAIL_WAVE ? 2 : 1) : 0,
+                    NEAR ? 2 : 0);
           if (L.skip) continue;
           if constexpr (TS) {
             // this cell's k_phitab row (wave-uniform: ipt, the tile and t are) and the lane's T1 row
@@ -970,6 +980,7 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
             const long go = ((long)ipt * A.phn + (cbx - A.phc0)) * RW + t * RW;
             const dbl2* T1 = (const dbl2*)(s_t1 + ((long)t * nqw + row) * prow2);
             if (IS3D_TAIL && L.tail) sep_phi_loop_ts<MODE, FLAGS, KJ, true>(L, mT, baryon, (cs_sptr)A.phtab + go, T1, acc);
+            else if (NEAR && L.near) sep_phi_loop_ts<MODE, FLAGS, KJ, false, NEAR>(L, mT, baryon, (cs_sptr)A.phtab + go, T1, acc);
             else if (L.fast) sep_phi_loop_ts<MODE, FLAGS, KJ, false>(L, mT, baryon, (cs_sptr)A.phtab + go, T1, acc);
             else sep_phi_loop<MODE, FLAGS, false, KJ>(L, CSl, (const dbl2*)(A.phtab + go), acc);
           } else if constexpr (TB) {

@@ -75,6 +75,9 @@ extern "C" void emu_set_census(long* counts) { g_census = counts; }
 // optional per-lane record (tools/lane_census.py --waves): [pT][cell][species][q] = 1 + (skip 0 / tail 1 / other 2)
 static signed char* g_census_lane = nullptr;
 extern "C" void emu_set_census_lanes(signed char* buf) { g_census_lane = buf; }
+// lanes whose smallest exponent exceeds g_near_x (not tail) are recorded as 4 (tools/lane_census.py --near)
+static double g_near_x = 1e300;
+extern "C" void emu_set_near_x(double x) { g_near_x = x; }
 
 extern "C" int emu_spectra_v(const orc_params* p, const orc_setup* su, const orc_surface* S, int chains, int op,
                              double* out, long* stats, int variant) {
@@ -200,17 +203,23 @@ extern "C" int emu_spectra_v(const orc_params* p, const orc_setup* su, const orc
               // tail lanes: the F_TB fours, or k_spectra's per-lane PD-table fours (Grad / RTA-CE, phi blocks of fours)
               // (operation 0: k_dndx's tail pairs, any phi block)
               const bool pd_tail = tail && !use_tb && mode <= CE && (op == 0 || spectra_kj(nphi) % 4 == 0);
+              // near-tail lanes: the F_TS Grad launch without regulate (sep_quad_tb_near_t)
+              const bool near = use_tb && tail && mode == GRAD && !p->regulate_deltaf;
               sep_setup(sep_flavor(mode), R, Y, mT, mT * mT, m2, mT * baryon, pT, sign, baryon, kExp2Tab, L,
-                        (use_tb || pd_tail) && tail);
+                        (use_tb || pd_tail) && tail, near);
               if (g_census) g_census[i * 3 + (L.skip ? 0 : (L.tail ? 1 : 2))]++;
               if (g_census_lane)
-                g_census_lane[(((size_t)i * n + c) * np + s) * nq + kk * nl + l] = (signed char)(1 + (L.skip ? 0 : (L.tail ? 1 : 2)));
+                g_census_lane[(((size_t)i * n + c) * np + s) * nq + kk * nl + l] =
+                    (signed char)(1 + (L.skip ? 0 : (L.tail ? 1 : (L.near || L.x - pT * R[R_ZB] > g_near_x ? 3 : 2))));
               if (L.skip) continue;
               if (use_tb && L.fast) {   // k_spectra's F_TB fours (normal or Boltzmann-tail lanes)
                 const dbl2* PT = &PTq[(size_t)(kk * nl + l) * nphi];
                 for (int j4 = 0; j4 < nphi; j4 += 4) {
                   const int rg = p->regulate_deltaf, of = p->outflow;
-                  if (L.tail) {
+                  if (L.near) {
+                    if (of) sep_quad_tb_near_t<true>(L, mT, &BP[j4], &PT[j4], &a[j4]);
+                    else sep_quad_tb_near_t<false>(L, mT, &BP[j4], &PT[j4], &a[j4]);
+                  } else if (L.tail) {
 #define EMU_TAIL(FLV, RG, OF) sep_quad_tb_tail_t<FLV, RG, OF>(L, mT, &BP[j4], &PT[j4], &PE[j4], &a[j4])
                     if (mode == GRAD) { if (rg) { if (of) EMU_TAIL(SEP_GRAD, true, true); else EMU_TAIL(SEP_GRAD, true, false); }
                                         else { if (of) EMU_TAIL(SEP_GRAD, false, true); else EMU_TAIL(SEP_GRAD, false, false); } }

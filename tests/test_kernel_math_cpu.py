@@ -4,7 +4,9 @@ libis3d_amd.so on the MI355X."""
 import numpy as np
 import pytest
 
-from helpers import emu_spectra, parity
+import ctypes as C
+
+from helpers import emu_spectra, emulator, parity, rel_quantile
 from is3d2_amd import make_spec, synth
 from oracle import oracle as O
 
@@ -152,6 +154,28 @@ def test_table_and_tail_algebra(dim, mode, reg_out):
         assert rel < 1e-8, (variant, rel)
         assert zr == zg
         assert not np.array_equal(got, base)       # the variant's arithmetic really ran
+
+
+@pytest.mark.parametrize("dim,outflow", [(3, 0), (3, 1), (2, 0)])
+def test_near_tail_lanes(dim, outflow):
+    """Near-tail Grad lanes of the F_TS launch (sep_quad_tb_near_t, smallest exponent in (kNearX, kTailX]:
+    1 / (1 + u) = 1 - u with u <= e^-18, no reciprocal) on the host against the oracle: the lanes occur, the
+    max relative error keeps the 1e-8 bar and the 99th percentile the 1e-11 drift guard of the GPU tier."""
+    s = synth.as_read(synth.surface(8, seed=41, dimension=dim, full3d=(dim == 3)))
+    spec = make_spec(hrg_eos=2, chosen="smash", df_mode=1, dimension=dim, pT="pT24", phi="phi24", outflow=outflow)
+    ref = O.spectra(spec, s, threads=1)
+    # [pT][cell][species][q] lane kinds (1 + skip 0 / tail 1 / other 2 / near 3), sized for any q layout
+    kinds = np.zeros(len(spec["pT"]) * 8 * len(spec["species"]["mass"]) * len(spec["y"]) * len(spec["eta"]), np.int8)
+    emulator().emu_set_census_lanes(kinds.ctypes.data_as(C.c_void_p))
+    try:
+        got, _ = emu_spectra(spec, s, variant=3)
+    finally:
+        emulator().emu_set_census_lanes(None)
+    assert (kinds == 4).sum() > 0.05 * (kinds > 1).sum()      # near-tail lanes really ran
+    rel, zr, zg = parity(got, ref, floor=1e-290)
+    assert rel < 1e-8, rel
+    assert zr == zg
+    assert rel_quantile(got, ref, floor=1e-290) < 1e-11
 
 
 PHI30 = (2 * np.pi * np.arange(30) / 30, np.full(30, 2 * np.pi / 30))
