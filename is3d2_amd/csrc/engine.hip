@@ -36,6 +36,9 @@
 #ifndef IS3D_CHAIN_SLOTS
 #define IS3D_CHAIN_SLOTS 16384   // PTMA chain segments per pass (one wavefront each)
 #endif
+#ifndef IS3D_CHAIN_W
+#define IS3D_CHAIN_W 4        // PTMA chain segments: wavefronts per segment sharing each Newton evaluation's terms
+#endif
 #ifndef IS3D_NEWTON_WAVES
 #define IS3D_NEWTON_WAVES 0   // PTMA Newton kernels (k_aniso, k_chain_pass): waves per SIMD to allocate for (0: compiler)
 #endif
@@ -131,6 +134,41 @@ struct WaveSum {
   }
 };
 
+// sum over the W wavefronts of a workgroup (W x 64 lanes share one cell's Newton terms): each wave's sums, then the
+// W partials from LDS in wave order (every lane gets the same bits), two barriers per red_all call of up to kRedN
+// values
+constexpr int kRedN = 8;
+template <int W>
+struct BlockSum {
+  double* s;   // LDS, kRedN x W doubles
+  __device__ double operator()(double v) const;
+};
+template <int W, class... T>
+__device__ __forceinline__ void red_all(const BlockSum<W>& r, T&... v) {
+  static_assert(sizeof...(T) <= kRedN, "BlockSum: at most kRedN values per call");
+  ((v = WaveSum()(v)), ...);
+  if constexpr (W > 1) {
+    const int wave = threadIdx.x >> 6;
+    int k = 0;
+    if ((threadIdx.x & 63) == 0) ((r.s[(k++) * W + wave] = v), ...);
+    __syncthreads();
+    k = 0;
+    auto sum = [&](int kk) {
+      double a = r.s[kk * W];
+#pragma unroll
+      for (int w = 1; w < W; w++) a += r.s[kk * W + w];
+      return a;
+    };
+    ((v = sum(k++)), ...);
+    __syncthreads();
+  }
+}
+template <int W>
+__device__ double BlockSum<W>::operator()(double v) const {
+  red_all(*this, v);
+  return v;
+}
+
 struct AnisoArgs {
   const double* rec; const double* ain; double* sol;   // rec [n][NREC], ain [9][stride], sol [6][stride]
   long c0, n, chains;   // cells [c0, c0 + n) in `chains` warm-start chains
@@ -214,6 +252,7 @@ __device__ __forceinline__ bool state_eq(const double* a, const double* b) {
 // the stored one and returns true (end state unchanged); otherwise the state after the last cell is in `state`.
 __device__ bool chain_segment_run(const ChainArgs& A, long seg, double* state, bool sync) {
   const int lane = threadIdx.x;
+  __shared__ double s_red[kRedN * IS3D_CHAIN_W];
   const long c = seg / A.nspc, s = seg % A.nspc;
   const long P = min((A.n - c + A.C - 1) / A.C, A.q1);      // positions of chain c in this range's end
   const long p0 = A.q0 + s * A.L, p1 = min(P, p0 + A.L);
@@ -223,12 +262,14 @@ __device__ bool chain_segment_run(const ChainArgs& A, long seg, double* state, b
     double ain[4];
 #pragma unroll
     for (int f = 0; f < 4; f++) ain[f] = A.ain[(long)f * A.n + cell];
-    double out[6];
-    long cnt[3] = {0, 0, 0};
-    aniso_cell(ain, A.h, lane, 64, WaveSum(), A.fp2, state, out, cnt);
+    // the stored state is read before the solve: its barriers keep lane 0's store below from racing a lagging
+    // wavefront's read
     double old[4];
 #pragma unroll
     for (int f = 0; f < 4; f++) old[f] = A.sta[(long)f * A.n + cell];
+    double out[6];
+    long cnt[3] = {0, 0, 0};
+    aniso_cell(ain, A.h, lane, 64 * IS3D_CHAIN_W, BlockSum<IS3D_CHAIN_W>{s_red}, A.fp2, state, out, cnt);
     const bool same = sync && state_eq(state, old);
     if (lane == 0) {
 #pragma unroll
@@ -242,7 +283,9 @@ __device__ bool chain_segment_run(const ChainArgs& A, long seg, double* state, b
   return false;
 }
 
-__global__ __launch_bounds__(64, IS3D_NEWTON_WAVES ? IS3D_NEWTON_WAVES : 1) void k_chain_pass(ChainArgs A, int pass) {
+// one workgroup of IS3D_CHAIN_W wavefronts per segment (the lanes share each Newton evaluation's terms); every
+// branch below is uniform over the workgroup (the reductions hand all lanes the same bits)
+__global__ __launch_bounds__(64 * IS3D_CHAIN_W, IS3D_NEWTON_WAVES ? IS3D_NEWTON_WAVES : 1) void k_chain_pass(ChainArgs A, int pass) {
   const long seg = blockIdx.x, nseg = A.C * A.nspc;
   const long c = seg / A.nspc, s = seg % A.nspc;
   const int lane = threadIdx.x;
@@ -267,12 +310,13 @@ __global__ __launch_bounds__(64, IS3D_NEWTON_WAVES ? IS3D_NEWTON_WAVES : 1) void
       for (int f = 0; f < 4; f++) st0[f] = prev[f * nseg + seg - 1];
     }
     if (state_eq(st0, used)) {                              // same start: the stored run stands
-      if (lane == 0) for (int f = 0; f < 4; f++) cur[f * nseg + seg] = prev[f * nseg + seg];
       done = true;
     } else {
 #pragma unroll
       for (int f = 0; f < 4; f++) state[f] = st0[f];
     }
+    if (IS3D_CHAIN_W > 1) __syncthreads();   // every wavefront has read sstart before lane 0 rewrites it
+    if (done && lane == 0) for (int f = 0; f < 4; f++) cur[f * nseg + seg] = prev[f * nseg + seg];
   }
   if (!done) {
     if (lane == 0) for (int f = 0; f < 4; f++) A.sstart[f * nseg + seg] = state[f];
@@ -302,7 +346,7 @@ __global__ __launch_bounds__(64, IS3D_NEWTON_WAVES ? IS3D_NEWTON_WAVES : 1) void
 // from its predecessor's current end state -- exact by induction.  It walks when this range's last pass changed
 // something or the predecessor shard walked (bin[2] flag); either way it leaves the range's final end states and
 // its walk flag in bout[2] for the next shard.
-__global__ __launch_bounds__(64) void k_chain_finish(ChainArgs A) {
+__global__ __launch_bounds__(64 * IS3D_CHAIN_W) void k_chain_finish(ChainArgs A) {
   const long nseg = A.C * A.nspc, bw = 4 * A.C + 1;
   double* cur = A.send + (long)((A.npass - 1) & 1) * 4 * nseg;
   const double* bfin = A.bin + 2 * bw;
@@ -329,7 +373,9 @@ __global__ __launch_bounds__(64) void k_chain_finish(ChainArgs A) {
     double used[4];
 #pragma unroll
     for (int f = 0; f < 4; f++) used[f] = A.sstart[f * nseg + seg];
-    if (state_eq(carry, used)) {
+    const bool same = state_eq(carry, used);
+    if (IS3D_CHAIN_W > 1) __syncthreads();   // every wavefront has read sstart before lane 0 rewrites it
+    if (same) {
 #pragma unroll
       for (int f = 0; f < 4; f++) carry[f] = cur[f * nseg + seg];
     } else {
@@ -1566,7 +1612,7 @@ static int chain_pass(is3d_engine* e, int pass) {
   LaunchCtx& L = e->lc;
   if (L.empty || !L.chained) return IS3D_OK;
   HIPCHK(e, hipSetDevice(e->device));
-  hipLaunchKernelGGL(k_chain_pass, dim3((unsigned)(L.ca.C * L.ca.nspc)), dim3(64), 0, L.st, L.ca, pass);
+  hipLaunchKernelGGL(k_chain_pass, dim3((unsigned)(L.ca.C * L.ca.nspc)), dim3(64 * IS3D_CHAIN_W), 0, L.st, L.ca, pass);
   HIPCHK(e, hipGetLastError());
   return IS3D_OK;
 }
@@ -1576,7 +1622,7 @@ static int chain_end(is3d_engine* e) {
   if (L.empty || !L.chained) return IS3D_OK;
   HIPCHK(e, hipSetDevice(e->device));
   const long c_lo = L.ca.q0 * L.ca.C, c_hi = std::min(e->ncell, L.ca.q1 * L.ca.C);
-  hipLaunchKernelGGL(k_chain_finish, dim3(1), dim3(64), 0, L.st, L.ca);
+  hipLaunchKernelGGL(k_chain_finish, dim3(1), dim3(64 * IS3D_CHAIN_W), 0, L.st, L.ca);
   hipLaunchKernelGGL(k_chain_count, dim3((unsigned)std::min(1024L, std::max(1L, (c_hi - c_lo + 255) / 256))), dim3(256), 0,
                      L.st, (const double*)e->d_rec, (const int*)L.ca.info, c_lo, c_hi, e->d_cnt);
   HIPCHK(e, hipGetLastError());
