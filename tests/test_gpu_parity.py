@@ -222,3 +222,24 @@ def test_smash_2d_grad_table_phi32(mode):
     ref = O.spectra(spec, s, threads=8)
     got, _ = run_gpu(spec, s)
     assert parity(got, ref)[0] < TOL
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_slow_lanes_scalar_table_launch(mode):
+    """Lanes off the fast path (smallest exponent below -300) in the F_TS / F_BY launches, which integrate them
+    after their tile (k_spectra SLOWD): baryon chemistry mu_B / T = 375 in half the cells, reachable through a
+    delta-f table whose mu_B axis is stretched 100x (same values).  The baryons' exponents there are ~ -350."""
+    s = synth.as_read(synth.surface(48, seed=29, dimension=3, baryon=True, full3d=True))
+    hot = np.arange(48) % 2 == 0
+    s["T"] = np.where(hot, 0.12, s["T"])
+    s["muB"] = np.where(hot, 45.0, s["muB"])
+    spec = make_spec(hrg_eos=2, chosen="smash", df_mode=mode, dimension=3, pT="pT24", phi="phi32", y="y21",
+                     include_baryon=1)
+    T, muB, tab = spec["df"]
+    spec["df"] = (T, np.asarray(muB) * 100.0, tab)
+    ref = O.spectra(spec, s, threads=8)
+    got, _ = run_gpu(spec, s)
+    rel, zr, zg = parity(got, ref)
+    assert rel < TOL, (rel, zr, zg)
+    assert zr == zg
+    assert rel_quantile(got, ref) < P99
