@@ -48,15 +48,18 @@ def wave_census(n=60, pTs=(0, 8, 16, 24, 32, 40, 47)):
     nc = len(rep)
     ntask = nc * nq
     nw = (ntask + 63) // 64
-    tot = {"skip": 0, "tail": 0, "fast": 0, "mixed": 0}
+    tot = {"skip": 0, "tail": 0, "near": 0, "fast": 0, "mixed": 0}
     lanes_in_mixed = 0
     for i in pTs:
         cat = buf[i][:, rep, :]                      # [cell][class][q]
         task = np.transpose(cat, (0, 2, 1)).reshape(n, ntask)   # task = class + nc q
         task = np.concatenate([task, np.zeros((n, nw * 64 - ntask), np.int8)], axis=1).reshape(n, nw, 64)
-        has_t = (task == 2).any(axis=2); has_f = (task == 3).any(axis=2)
-        tot["mixed"] += int((has_t & has_f).sum()); tot["tail"] += int((has_t & ~has_f).sum())
-        tot["fast"] += int((~has_t & has_f).sum()); tot["skip"] += int((~has_t & ~has_f).sum())
+        # lane codes 1 + (skip 0 / tail 1 / other 2 / near-tail 3, cf_emulator.cpp); the device votes per wave:
+        # tail if every live lane is, else near if every live lane is near or tail, else the normal fours
+        has_t = (task == 2).any(axis=2); has_f = (task == 3).any(axis=2); has_n = (task == 4).any(axis=2)
+        tot["mixed"] += int((has_t & has_f).sum()); tot["tail"] += int((has_t & ~has_f & ~has_n).sum())
+        tot["near"] += int((has_n & ~has_f).sum())
+        tot["fast"] += int((~has_t & has_f).sum()); tot["skip"] += int((~has_t & ~has_f & ~has_n).sum())
     allw = sum(tot.values())
     print("waves: " + "  ".join("%s %.3f" % (k, v / allw) for k, v in tot.items()))
 
