@@ -344,7 +344,7 @@ struct DfCoef {
   double c0, c1, c2, c3, c4, shear14, F, G, betabulk, betaV, betapi, lambda, z, dlambda, dz;
 };
 
-enum DfErr : int { DF_OK = 0, DF_SPLINE_RANGE = 1, DF_BAD_MODE = 2, DF_TABLE_RANGE = 3, DF_PTB_BARYON = 4 };
+enum DfErr : int { DF_OK = 0, DF_SPLINE_RANGE = 1, DF_BAD_MODE = 2, DF_TABLE_RANGE = 3, DF_PTB_BARYON = 4, DF_TS_SLOW = 5 };
 
 // gsl_spline_eval for gsl_interp_cspline: range check, binary search, coeff_calc
 IS3D_HD double spline_eval(const double* x, const double* y, const double* c, int n, double xv, int* err) {
@@ -598,6 +598,7 @@ struct PrepConsts {
   int gla_pts;
   const double *gla_r1, *gla_w1, *gla_r2, *gla_w2;
   double two_pi2_hbarC3;
+  double pT_max, b_max;   // momentum grid's largest pT, species' largest |baryon| (sep_slow_cell)
 };
 
 // common fields for every record
@@ -1116,6 +1117,8 @@ struct SepLane {
 // 1 - sign f_eq == 1 in FP64 exactly (the sum rounds back to the larger term); a lane whose smallest
 // exponent over phi exceeds it needs no per-point reciprocal at all
 static constexpr double kTailX = 37.5;
+// fast-path domain of sep_setup: smallest exponent x - zb >= kExpFast (sep_slow_cell bounds it per cell)
+static constexpr double kExpFast = -300.0;
 // near-tail bound: for an exponent x >= kNearX, u = sign e^-x <= 1.6e-8, so 1 / (1 + u) = 1 - u to u^2 <= 2.4e-16
 // (the rounding of the reciprocal it replaces: rcp1, ~2e-15); a Grad lane whose smallest exponent exceeds it
 // takes (1 - u) (1 + (1 - u) S) = (1 + S) - u (1 + 2 S) per point, no reciprocal (sep_quad_tb_near_t)
@@ -1154,6 +1157,18 @@ IS3D_HD bool sep_skips(const double* R, const double* Y, double mT, double pT, d
   return fma(mT, Y[Y_AT], -baryon * R[R_CHEM]) - pT * R[R_ZB] > kExpMax;
 }
 
+// Can a lane of this cell leave sep_setup's fast path (smallest exponent x - zb below -300)?  With
+// A(y - eta) = ch u^tau - sh tau u^eta >= A_min = sqrt(u^tau^2 - (tau u^eta)^2) (its minimum over all rapidities)
+// and zb = pT |u_perp| / T, x - zb = (mT A - pT |u_perp|) / T - b chem >= min(0, pT_max (A_min - |u_perp|)) / T
+// - b_max |chem| (mT >= pT); for a normalised u, A_min = sqrt(1 + u_perp^2) > |u_perp| and the bound is
+// -b_max |chem|: such lanes need |mu_B| / T > ~300.  Conservative (a margin of 10), NaN-safe.
+IS3D_HD bool sep_slow_cell(const double* R, double pT_max, double b_max) {
+  const double a2 = R[R_UT] * R[R_UT] - R[R_TAUUN] * R[R_TAUUN];
+  const double amin = a2 > 0.0 ? sqrt(a2) : 0.0, up = sqrt(R[R_UX] * R[R_UX] + R[R_UY] * R[R_UY]);
+  const double lb = fmin(0.0, pT_max * (amin - up)) * R[R_INVT] - b_max * fabs(R[R_CHEM]);
+  return !(lb > kExpFast + 10.0);
+}
+
 IS3D_HD void sep_setup(int flavor, const double* R, const double* Y, double mT, double mT2, double m2, double mTb,
                        double pT, double sign, double baryon, const double* etab, SepLane& L, int allow_tail = 0,
                        int allow_near = 0) {
@@ -1168,7 +1183,7 @@ IS3D_HD void sep_setup(int flavor, const double* R, const double* Y, double mT, 
   // sep_quad_t) stays finite and normal.  The scale is exact, so
   // a = e^(x - zb) 2^-k is as accurate as e^(x - zb) itself (table exp, ~1 ulp)
   const double xs = L.x - zb;
-  L.fast = (xs >= -300.0) ? 1 : 0;
+  L.fast = (xs >= kExpFast) ? 1 : 0;
   L.tail = (allow_tail && xs > kTailX) ? 1 : 0;
 #if defined(__HIP_DEVICE_COMPILE__)
   // allow_tail == 2: one decision per wavefront (all its live lanes in the tail, or none), so a wavefront

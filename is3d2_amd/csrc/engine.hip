@@ -122,6 +122,10 @@ __global__ __launch_bounds__(256) void k_prep(PrepArgs A) {
   }
   if (err) { atomicMax(A.err, err); R[R_KIND] = 0.0; }
   if (R[R_KIND] != 0.0) sep_cell_consts(MODE, R);
+  // Grad / RTA-CE: cells whose lanes may leave the fast path (|mu_B| / T beyond ~300) counted in cnt[4]: any such
+  // cell sends the launch to the F_TB kernels, the F_TS ones carry no slow loop (launch_end)
+  if (MODE <= CE && A.k.operation == 1 && R[R_KIND] != 0.0 && sep_slow_cell(R, A.k.pT_max, A.k.b_max))
+    atomicAdd(&A.cnt[4], 1ULL);
 #pragma unroll
   for (int f = 0; f < NREC; f++) A.rec[c * NREC + f] = R[f];
 }
@@ -1102,7 +1106,7 @@ struct SpectraPlan {
   size_t shmem;
   size_t shmem_fb;            // modified modes: the F_FB launch (8-cell tiles, per-lane y-term rows, no q tables)
 };
-static SpectraPlan spectra_plan(const is3d_engine* e) {
+static SpectraPlan spectra_plan(const is3d_engine* e, bool allow_ts = true) {
   SpectraPlan P{};
   P.npw = 1;
   const int mode = e->p.df_mode, dim = e->p.dimension;
@@ -1122,14 +1126,14 @@ static SpectraPlan spectra_plan(const is3d_engine* e) {
     // workgroup
     // with include_baryon only as F_TS + F_BY (one phi block of 24 or 32 points: the baryon part of the linear
     // coefficients comes from the table as T3)
-    const bool ts_shape = IS3D_TS && IS3D_TS_BY && P.njb == 1 && (KJ == 24 || KJ == 32);
+    const bool ts_shape = IS3D_TS && IS3D_TS_BY && allow_ts && P.njb == 1 && (KJ == 24 || KJ == 32);
     P.tb = (IS3D_GRAD_TB && (mode == GRAD || (mode == CE && IS3D_CE_TB)) && (!e->p.include_baryon || ts_shape) &&
             KJ % 4 == 0 && P.nqmax <= kTbQ) ? F_TB : 0;
   };
   int kTile = (mode >= PTM) ? IS3D_KTILE_MOD : is3d::kern::kTile;   // spectra_tile<MODE, FLAGS>()
   // k_spectra's LDS layout (kernels.h): record tiles x kRecBufs, per-tile tables x kTabBufs
   // F_TS (kernels.h TS): an F_TB launch with one phi block of 24 or 32 points
-  auto ts_ok = [&]() { return IS3D_TS && P.tb && P.njb == 1 && (P.KJ == 24 || P.KJ == 32); };
+  auto ts_ok = [&]() { return IS3D_TS && allow_ts && P.tb && P.njb == 1 && (P.KJ == 24 || P.KJ == 32); };
   auto lds_bytes = [&](int qrows) {     // qrows = 0: F_LY layout (one y-term row per lane)
     const size_t nphp = (size_t)P.njb * P.KJ, tile = (size_t)kTile;
     if (ts_ok()) {
@@ -1512,6 +1516,9 @@ static PrepConsts make_consts(const is3d_engine* e) {
     k.gla_w1 = w + 1 * e->gla_pts; k.gla_w2 = w + 2 * e->gla_pts;
   }
   k.two_pi2_hbarC3 = 2.0 * std::pow(M_PI, 2) * std::pow(kHbarC, 3);
+  k.pT_max = 0.0; k.b_max = 0.0;
+  for (double v : e->pT) k.pT_max = std::max(k.pT_max, std::fabs(v));
+  for (double v : e->baryon) k.b_max = std::max(k.b_max, std::fabs(v));
   return k;
 }
 
@@ -1670,7 +1677,16 @@ static int launch_end(is3d_engine* e) {
   // the integral and the reduction see the window only: records from wlo on, nw cells
   const double* rec_w = e->d_rec + wlo * (long)NREC;
   // --- main integral
-  const SpectraPlan P = spectra_plan(e);
+  // Grad / RTA-CE: a surface with cells whose lanes may leave the fast path (k_prep's cnt[4]; none in any
+  // tabulated delta-f range) takes the F_TB kernels, which carry the slow loop; the F_TS kernels do not
+  bool allow_ts = true;
+  if (mode <= CE) {
+    unsigned long long nslow = 0;
+    HIPCHK(e, hipMemcpyAsync(&nslow, e->d_cnt + 4, sizeof(nslow), hipMemcpyDeviceToHost, st));
+    HIPCHK(e, hipStreamSynchronize(st));
+    allow_ts = nslow == 0;
+  }
+  const SpectraPlan P = spectra_plan(e, allow_ts);
   const int KJ = P.KJ, njb = P.njb;
   if (!spectra_kj_supported(KJ)) return e->fail(IS3D_ERR_ARG, "internal: no k_spectra instantiation for this phi block");
   if (P.shmem > 160 * 1024) return e->fail(IS3D_ERR_ARG, "momentum grid too large for the LDS tile (phi table)");
@@ -1718,6 +1734,7 @@ static int launch_end(is3d_engine* e) {
     HIPCHK(e, hipGetLastError());
   }
   SpecArgs sa{};
+  sa.err = e->d_err;
   sa.rec = rec_w; sa.n = nw; sa.renorm = e->d_renorm; sa.rcls = e->d_crcls; sa.nrcls = e->nrcls; sa.slab = e->d_slab; sa.outsize = outsize;
   sa.smass = e->d_cmass; sa.ssign = e->d_csign; sa.sbaryon = e->d_cbaryon; sa.sorig = e->d_sorig;
   sa.csg = e->d_csg;
@@ -1904,6 +1921,7 @@ extern "C" int is3d_finish(is3d_engine* e) {
     case DF_SPLINE_RANGE: return e->fail(IS3D_ERR_DF_RANGE, "gsl: interp.c: interpolation error (df coefficient spline evaluated outside its table)");
     case DF_TABLE_RANGE: return e->fail(IS3D_ERR_DF_RANGE, "Error: (T,muB) outside df coefficient table. Exiting...");
     case DF_PTB_BARYON: return e->fail(IS3D_ERR_UNSUPPORTED, "Bilinear interpolation error: Jonah df doesn't work for nonzero muB. Exiting..");
+    case DF_TS_SLOW: return e->fail(IS3D_ERR_DEVICE, "internal: a scalar-table (F_TS) lane left the fast path (sep_slow_cell bound)");
     default: return e->fail(IS3D_ERR_ARG, "Error: choose df_mode = (1,2,3,4,5)");
   }
 }

@@ -77,6 +77,7 @@ constexpr int kYRowLY = Y_MU2 | 1;
 // ------------------------------------------------------------------------------------------
 struct SpecArgs {
   const double* rec; long n;
+  int* err;                   // DF_TS_SLOW: a F_TS lane off the fast path (engine.hip routes such surfaces to F_TB)
   const double* renorm;       // PTM: [c][renorm class]
   const int* rcls; int nrcls; // renorm class of each sorted species (engine.hip), number of classes
   double* slab; long outsize;
@@ -200,6 +201,9 @@ __host__ __device__ constexpr int phitab_row(int mode, int nphp, bool by = false
 #endif
 #ifndef IS3D_TS_AHEAD_GRAD
 #define IS3D_TS_AHEAD_GRAD 1
+#endif
+#ifndef IS3D_TS_SLOW
+#define IS3D_TS_SLOW 0        // F_TS kernels with the slow-path loop (0: such surfaces take F_TB, sep_slow_cell)
 #endif
 #ifndef IS3D_NEAR
 #define IS3D_NEAR 1           // F_TS Grad: near-tail lanes (sep_quad_tb_near_t, kNearX), no reciprocal per point
@@ -982,7 +986,10 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
             if (IS3D_TAIL && L.tail) sep_phi_loop_ts<MODE, FLAGS, KJ, true>(L, mT, baryon, (cs_sptr)A.phtab + go, T1, acc);
             else if (NEAR && L.near) sep_phi_loop_ts<MODE, FLAGS, KJ, false, NEAR>(L, mT, baryon, (cs_sptr)A.phtab + go, T1, acc);
             else if (L.fast) sep_phi_loop_ts<MODE, FLAGS, KJ, false>(L, mT, baryon, (cs_sptr)A.phtab + go, T1, acc);
-            else sep_phi_loop<MODE, FLAGS, false, KJ>(L, CSl, (const dbl2*)(A.phtab + go), acc);
+            // lanes off the fast path never reach F_TS (sep_slow_cell, engine.hip launch_end): their loop, inlined
+            // here, was the kernels' register peak (IS3D_TS_SLOW = 1 keeps it)
+            else if constexpr (IS3D_TS_SLOW) sep_phi_loop<MODE, FLAGS, false, KJ>(L, CSl, (const dbl2*)(A.phtab + go), acc);
+            else atomicMax(A.err, (int)DF_TS_SLOW);
           } else if constexpr (TB) {
             const dbl2* PT = s_pt + ((long)t * nqw + row) * prow;
             if (IS3D_TAIL && L.tail) {
