@@ -50,8 +50,8 @@ def log(*a):
 
 def make_surface(cfg, rank, world, dim, baryon, whole=False):
     """This rank's cells: weak scaling -- its own surface (seed 7 + rank); strong scaling -- its cost-balanced
-    contiguous range of the one surface (dist.shard_bounds), or the whole surface and the range (whole=True,
-    PTMA warm-start chains: every rank walks the chain, integrates its range)."""
+    contiguous range of the one surface (dist.shard_bounds), or the whole surface (whole=True, PTMA warm-start
+    chains: every rank then solves and integrates its own chain positions, dist.chain_bounds)."""
     from is3d2_amd import dist as D, synth
     if cfg["scaling"] == "strong":
         s = synth.as_read(synth.surface(cfg["cells"], seed=7, dimension=dim, baryon=baryon, full3d=(dim == 3)))
@@ -224,8 +224,17 @@ def run_workload(args, cfg_name, mode, steps, warmup, rank, world, local_rank, d
         flags.pop("include_baryon", None); flags.pop("include_baryondiff_deltaf", None)
     spec = make_spec(hrg_eos=cfg["hrg"], chosen=cfg["chosen"], pT=cfg["pT"], phi=cfg["phi"], y="y21", eta="eta24",
                      dimension=cfg["dim"], df_mode=mode, gla_points=cfg.get("gla", 32), **flags)
-    chained = mode == 5 and spec["params"]["famod_chains"] > 0 and world > 1
+    # one surface split over the ranks (strong scaling) with PTMA warm-start chains: a recurrence over the whole surface
+    chained = mode == 5 and spec["params"]["famod_chains"] > 0 and world > 1 and cfg["scaling"] == "strong"
     surf, window = make_surface(cfg, rank, world, cfg["dim"], bool(flags.get("include_baryon", 0)), whole=chained)
+    qrange = None
+    if chained:
+        # PTMA warm-start chains split over the ranks (dist.launch_chained): every rank holds the whole surface and
+        # solves its own chain positions, the boundary states passed rank to rank after every pass
+        C = spec["params"]["famod_chains"]
+        qrange = D.chain_bounds(surf, rank, world, C)
+        n_all = len(surf["tau"])
+        window = (min(n_all, qrange[0] * C), min(n_all, qrange[1] * C))
     n_local = len(surf["tau"]) if window is None else window[1] - window[0]
     reduce = D.torch_all_reduce(dist, dev) if world > 1 else (lambda a: a)
     mine = surf if window is None else {k: v[window[0]:window[1]] for k, v in surf.items()}
@@ -233,7 +242,9 @@ def run_workload(args, cfg_name, mode, steps, warmup, rank, world, local_rank, d
 
     eng = build_engine(spec, surf, T_avg=T_avg, device=local_rank, species_classes=classes)
     n_integrated = eng.species_integrated()
-    if window is not None:
+    if qrange is not None:
+        eng.set_chain_range(*qrange)
+    elif window is not None:
         eng.set_cell_window(*window)
     outsize = eng.output_size()
     out = torch.zeros(outsize, dtype=torch.float64, device=dev)
@@ -255,7 +266,10 @@ def run_workload(args, cfg_name, mode, steps, warmup, rank, world, local_rank, d
                 binned = torch.from_numpy(np.concatenate([t.ravel(), r.ravel(), ph.ravel()])).to(dev)
                 dist.all_reduce(binned)
             return eng.stats()
-        eng.launch(out.data_ptr(), stream)
+        if qrange is not None:
+            D.launch_chained(eng, out.data_ptr(), stream, rank, world, dist, device=dev)
+        else:
+            eng.launch(out.data_ptr(), stream)
         if world > 1:
             dist.all_reduce(out)
         eng.finish()
@@ -297,7 +311,9 @@ def run_workload(args, cfg_name, mode, steps, warmup, rank, world, local_rank, d
         "cells_per_gpu": n_local, "species": nsp, "grid": [npT, nphi, ny, neta], "df_mode": mode,
         "species_integrated": n_integrated,
         "famod_chains": spec["params"]["famod_chains"] if mode == 5 else None,
-        "parallelism": "dp%d (cell shards + RCCL all-reduce of spectra)" % world if world > 1 else "1 GPU",
+        "parallelism": ("dp%d (cell shards + RCCL all-reduce of spectra%s)"
+                        % (world, "; PTMA chain positions split, boundary states sent rank to rank per pass" if chained else "")
+                        if world > 1 else "1 GPU"),
     }
     return dict(value=total_units / elapsed, elapsed=elapsed, steps=steps, warmup=warmup, cfg=cfg, config=config,
                 roofline=roofline, spec=spec, surf=surf, units_per_cell=units_per_cell, n_local=n_local)

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define IS3D_ABI_VERSION 4
+#define IS3D_ABI_VERSION 5
 
 enum {
   IS3D_OK = 0,
@@ -126,6 +126,15 @@ void is3d_destroy(is3d_engine *e);
 const char *is3d_last_error(const is3d_engine *e);
 
 int is3d_set_params(is3d_engine *e, const is3d_params *p);
+/* Engine tuning knobs (no reference counterpart; a device-list engine forwards them to every shard).
+ *   "phitab_one_bytes"    F_TS scalar tables (Grad / RTA-CE, one phi block) of the whole window up to this size are
+ *                         written and integrated in one chunk (default 8 GiB)
+ *   "phitab_chunk_bytes"  larger ones in chunks of whole cell splits of about this size, alternating over two streams
+ *                         (default 2 GiB; BASELINE config 4 runs 29 chunks)
+ * A negative value restores the default.  is3d_get_tuning also reads "phitab_chunks": the F_TS chunks of the last
+ * launch (0: not an F_TS launch); -1 = unknown key. */
+int is3d_set_tuning(is3d_engine *e, const char *key, long value);
+long is3d_get_tuning(const is3d_engine *e, const char *key);
 int is3d_set_species(is3d_engine *e, int n, const double *mass, const double *sign,
                      const double *degeneracy, const double *baryon);
 /* Integrand classes (no reference counterpart: an engine option, default on).  The momentum integrals see a
@@ -171,6 +180,36 @@ int is3d_set_cell_window(is3d_engine *e, long lo, long hi);
  * tools/fb_cost_probe.py); every other cell 1 (PTMA's breakdowns are only known after its Newton solves).
  * Runs the record prepass on the engine's GPU (synchronous); cost holds n_cells doubles. */
 int is3d_cell_costs(is3d_engine *e, double *cost);
+
+/* PTMA warm-start chains split over processes (one process per GPU; SURVEY.md 8(e) "partition by chain and keep
+ * chain order").  The reference warm-starts each Newton solve from the previous successful cell of its OpenMP thread
+ * (MomentumSpectra.cpp:1132-1135, 1308-1364): chain c = cells c, c + C, c + 2C, ... with C = famod_chains.  Every
+ * process holds the whole surface; is3d_set_chain_range(e, q0, q1) makes this engine solve chain positions
+ * [q0, q1) of every chain and integrate cells [q0 C, min(n, q1 C)) (q0 = q1 = -1: off; setting a surface or a cell
+ * window clears it).  The staged launch then lets the caller move the boundary states between processes:
+ *   is3d_launch_begin                        prepass of the range (on `stream`)
+ *   for pass j < is3d_chain_passes(e):
+ *     [q0 > 0, j > 0]  is3d_chain_boundary_put(e, (j - 1) & 1, buf)   the predecessor's pass j - 1 end states
+ *     is3d_chain_pass(e, j)
+ *     [successor]      is3d_chain_boundary_get(e, j & 1, buf)         this range's pass j end states, to send
+ *   [q0 > 0]  is3d_chain_boundary_put(e, 2, buf)   the predecessor's final states (after its is3d_chain_end)
+ *   is3d_chain_end(e)
+ *   [successor]  is3d_chain_boundary_get(e, 2, buf)
+ *   is3d_launch_end(e)   ...   is3d_finish(e)
+ * Buffers hold is3d_chain_boundary_size(e) doubles, in device memory (or host memory: the copies are asynchronous
+ * on the launch stream, so the caller synchronises it before reading a host buffer it got).
+ * At the fixed point each range's solutions are the one-chain solutions bit for bit (engine.hip k_chain_pass), so
+ * the per-process Newton iteration counts (is3d_get_stats) add up to the serial chain's.  is3d_launch refuses an
+ * engine with a chain range. */
+int is3d_set_chain_range(is3d_engine *e, long q0, long q1);
+int is3d_launch_begin(is3d_engine *e, double *dev_out, void *stream);
+int is3d_chain_passes(const is3d_engine *e);
+int is3d_chain_pass(is3d_engine *e, int pass);
+int is3d_chain_end(is3d_engine *e);
+int is3d_launch_end(is3d_engine *e);
+long is3d_chain_boundary_size(const is3d_engine *e);
+int is3d_chain_boundary_get(is3d_engine *e, int slot, double *dev_buf);
+int is3d_chain_boundary_put(is3d_engine *e, int slot, const double *dev_buf);
 
 /* Full call: kernels + device->host copy of dN/(pT dpT dphi dy) into dN_out. */
 int is3d_calculate_spectra(is3d_engine *e, double *dN_out);

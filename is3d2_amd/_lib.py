@@ -15,12 +15,14 @@ SURFACE_FIELDS = ["tau", "x", "y", "eta", "dat", "dax", "day", "dan", "ux", "uy"
 IS3D_OK, IS3D_ERR_ARG, IS3D_ERR_STATE, IS3D_ERR_DEVICE, IS3D_ERR_DF_RANGE, IS3D_ERR_UNSUPPORTED = range(6)
 
 # every symbol include/is3d_amd.h declares
-EXPORTS = ["is3d_abi_version", "is3d_build_id", "is3d_create", "is3d_create_devices", "is3d_destroy", "is3d_last_error", "is3d_set_params",
+EXPORTS = ["is3d_abi_version", "is3d_build_id", "is3d_create", "is3d_create_devices", "is3d_destroy", "is3d_last_error", "is3d_set_params", "is3d_set_tuning", "is3d_get_tuning",
            "is3d_set_species", "is3d_set_species_classes", "is3d_species_integrated", "is3d_set_pdg", "is3d_set_momentum_grid", "is3d_set_gauss_laguerre",
            "is3d_set_df_tables", "is3d_set_surface", "is3d_set_surface_device", "is3d_set_cell_window", "is3d_cell_costs", "is3d_calculate_spectra",
            "is3d_launch", "is3d_finish", "is3d_get_stats", "is3d_output_size", "is3d_evaluate_df_coefficients",
            "is3d_surface_averages", "is3d_get_jonah_table", "is3d_set_momentum_weights", "is3d_set_spacetime_bins",
-           "is3d_calculate_dN_dX", "is3d_get_cell_yields", "is3d_total_yield"]
+           "is3d_calculate_dN_dX", "is3d_get_cell_yields", "is3d_total_yield", "is3d_set_chain_range",
+           "is3d_launch_begin", "is3d_chain_passes", "is3d_chain_pass", "is3d_chain_end", "is3d_launch_end",
+           "is3d_chain_boundary_size", "is3d_chain_boundary_get", "is3d_chain_boundary_put"]
 
 
 class Params(C.Structure):
@@ -69,6 +71,9 @@ def load():
     lib.is3d_last_error.restype = C.c_char_p
     lib.is3d_last_error.argtypes = [C.c_void_p]
     lib.is3d_set_params.argtypes = [C.c_void_p, P(Params)]
+    lib.is3d_set_tuning.argtypes = [C.c_void_p, C.c_char_p, C.c_long]
+    lib.is3d_get_tuning.restype = C.c_long
+    lib.is3d_get_tuning.argtypes = [C.c_void_p, C.c_char_p]
     lib.is3d_set_species.argtypes = [C.c_void_p, C.c_int, pd, pd, pd, pd]
     lib.is3d_set_species_classes.argtypes = [C.c_void_p, C.c_int]
     lib.is3d_species_integrated.argtypes = [C.c_void_p]
@@ -94,6 +99,16 @@ def load():
     lib.is3d_calculate_dN_dX.argtypes = [C.c_void_p, pd, pd, pd]
     lib.is3d_get_cell_yields.argtypes = [C.c_void_p, pd]
     lib.is3d_total_yield.argtypes = [C.c_void_p, pd, d, pd, pd]
+    lib.is3d_set_chain_range.argtypes = [C.c_void_p, C.c_long, C.c_long]
+    lib.is3d_launch_begin.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.is3d_chain_passes.argtypes = [C.c_void_p]
+    lib.is3d_chain_pass.argtypes = [C.c_void_p, C.c_int]
+    lib.is3d_chain_end.argtypes = [C.c_void_p]
+    lib.is3d_launch_end.argtypes = [C.c_void_p]
+    lib.is3d_chain_boundary_size.restype = C.c_long
+    lib.is3d_chain_boundary_size.argtypes = [C.c_void_p]
+    lib.is3d_chain_boundary_get.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
+    lib.is3d_chain_boundary_put.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
     _lib = lib
     return lib
 

@@ -337,12 +337,23 @@ __global__ __launch_bounds__(64 * IS3D_CHAIN_W, IS3D_NEWTON_WAVES ? IS3D_NEWTON_
         if (moved && pass > 0) atomicOr(&A.changed[pass], 1);
       }
     }
-    if (pass == 0 && lane == 0 && A.nspc > 1) atomicOr(&A.changed[0], 1);
+    // pass 0 ran cold starts: exact only for the first segment of a range without a predecessor, so it flags a
+    // change whenever some segment may be wrong (a finisher after a single pass must then walk)
+    if (pass == 0 && lane == 0 && (A.nspc > 1 || A.has_pred)) atomicOr(&A.changed[0], 1);
+  }
+  // pass 0 fills both parity slots: a range without a predecessor and with one segment per chain is exact after
+  // pass 0 and flags nothing, so passes 1.. return early above and never write slot 1 -- which the finisher's
+  // no-walk copy and the successor shard's odd-pass boundary read
+  if (pass == 0 && lane == 0) {
+    double* other = A.send + 4 * nseg;
+    for (int f = 0; f < 4; f++) other[f * nseg + seg] = cur[f * nseg + seg];
   }
   // the range's last segment of chain c: its end state is the next shard's boundary in
   if (s == A.nspc - 1 && lane == 0) {
-    double* b = A.bout + (long)(pass & 1) * bw;
-    for (int f = 0; f < 4; f++) b[f * A.C + c] = cur[f * nseg + seg];
+    for (int slot = pass & 1; slot <= (pass == 0 ? 1 : (pass & 1)); slot++) {
+      double* b = A.bout + (long)slot * bw;
+      for (int f = 0; f < 4; f++) b[f * A.C + c] = cur[f * nseg + seg];
+    }
   }
 }
 
@@ -505,6 +516,7 @@ struct ReduceArgs {
   const int* sorig; const double* degen_orig; double prefactor;
   const int *cmem_off, *cmem;   // member sorted species of each class
   double* out;
+  const unsigned long long* gate; int gate_want;   // launch_end's device-side plan choice (kernels.h SpecArgs)
 };
 
 // every member species of class c gets (2 pi hbarc)^-3 g_s x the class's sum
@@ -519,6 +531,7 @@ __device__ __forceinline__ void write_members(const ReduceArgs& A, int c, long o
 // One thread per slab entry of an l = 0 lane; the lanes of the other eta nodes of the same (class, y,
 // phi block) are task + l * npart.
 __global__ __launch_bounds__(256) void k_reduce(ReduceArgs A) {
+  if (gate_closed(A.gate, A.gate_want)) return;
   const long e = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= A.sstride) return;
   const int KJ = A.kj;
@@ -549,6 +562,7 @@ __global__ __launch_bounds__(256) void k_reduce(ReduceArgs A) {
 // output and took 2.4 ms for pikp 1e5 cells): lane i adds terms i, i + 64, ... of the (l, split) list,
 // then a fixed xor-shuffle tree combines the lanes, so the order stays fixed (bit-reproducible).
 __global__ __launch_bounds__(256) void k_reduce_wave(ReduceArgs A) {
+  if (gate_closed(A.gate, A.gate_want)) return;
   const long o = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   const long nout = (long)A.npart * A.npT * A.nphi * A.ny_out;
@@ -778,6 +792,9 @@ struct is3d_engine {
   // cell window [win_lo, win_hi) of the held surface that k_spectra integrates (-1: every cell); set by a
   // group whose shards hold the whole surface for the PTMA warm-start chains
   long win_lo = -1, win_hi = -1;
+  // is3d_set_chain_range: PTMA warm-start chain positions [chain_q0, chain_q1) this engine solves (-1: all), for the
+  // staged launch of one process per GPU
+  long chain_q0 = -1, chain_q1 = -1;
   bool have_params = false, have_species = false, have_pdg = false, have_grid = false, have_gla = false, have_df = false;
   is3d_params p{};
   // species (original order) and mass-sorted permutation
@@ -840,6 +857,10 @@ struct is3d_engine {
   long phtab2_cap = 0;
   hipStream_t side = nullptr; // F_TS chunks alternate between the launch stream and this one
   hipEvent_t fork = nullptr, join = nullptr;
+  // is3d_set_tuning: F_TS table chunking (defaults IS3D_PHITAB_ONE / IS3D_PHITAB_BYTES): tables of the whole window
+  // up to phitab_one bytes are one chunk, larger ones chunks of whole cell splits of about phitab_chunk bytes
+  long phitab_one = IS3D_PHITAB_ONE, phitab_chunk = IS3D_PHITAB_BYTES;
+  long last_nchunk = 0;       // F_TS chunks of the last launch (0: not an F_TS launch)
   // operation 0
   double *d_ycell = nullptr, *d_part = nullptr; long ycell_cap = 0, part_cap = 0;
   int *d_keys = nullptr, *d_perm = nullptr; long keys_cap = 0, perm_cap = 0;
@@ -928,10 +949,29 @@ extern "C" is3d_engine* is3d_create_devices(int n, const int* devices) {
 extern "C" int is3d_set_cell_window(is3d_engine* e, long lo, long hi) {
   if (!e) return IS3D_ERR_ARG;
   if (e->grp) return is3d::group_fail(e->grp, IS3D_ERR_UNSUPPORTED, "a device-list engine places its own windows");
+  e->chain_q0 = e->chain_q1 = -1;
   if (lo < 0 || hi < 0) { e->win_lo = e->win_hi = -1; return IS3D_OK; }
   if (lo > hi || hi > e->ncell) return e->fail(IS3D_ERR_ARG, "cell window outside the surface");
   e->win_lo = lo; e->win_hi = hi;
   return IS3D_OK;
+}
+
+extern "C" int is3d_set_tuning(is3d_engine* e, const char* key, long value) {
+  if (e && e->grp) return key ? is3d::group_set_tuning(e->grp, key, value) : IS3D_ERR_ARG;
+  if (!e || !key) return IS3D_ERR_ARG;
+  if (!std::strcmp(key, "phitab_one_bytes")) e->phitab_one = value < 0 ? (long)IS3D_PHITAB_ONE : value;
+  else if (!std::strcmp(key, "phitab_chunk_bytes")) e->phitab_chunk = value <= 0 ? (long)IS3D_PHITAB_BYTES : value;
+  else return e->fail(IS3D_ERR_ARG, std::string("is3d_set_tuning: unknown key ") + key);
+  return IS3D_OK;
+}
+
+extern "C" long is3d_get_tuning(const is3d_engine* e, const char* key) {
+  if (!e || !key) return -1;
+  if (e->grp) return is3d::group_get_tuning(e->grp, key);
+  if (!std::strcmp(key, "phitab_one_bytes")) return e->phitab_one;
+  if (!std::strcmp(key, "phitab_chunk_bytes")) return e->phitab_chunk;
+  if (!std::strcmp(key, "phitab_chunks")) return e->last_nchunk;
+  return -1;
 }
 
 extern "C" int is3d_set_params(is3d_engine* e, const is3d_params* p) {
@@ -1448,6 +1488,7 @@ extern "C" int is3d_set_surface(is3d_engine* e, long n, const is3d_surface* s) {
   }
   e->ncell = n;
   e->win_lo = e->win_hi = -1;
+  e->chain_q0 = e->chain_q1 = -1;
   if (n == 0) return IS3D_OK;
   for (int f = 0; f < NSURF; f++) {
     double* dst = e->d_surf + (size_t)f * n;
@@ -1466,6 +1507,7 @@ extern "C" int is3d_set_surface_device(is3d_engine* e, long n, const double* dev
   e->d_surf = const_cast<double*>(dev_fields);
   e->ncell = n;
   e->win_lo = e->win_hi = -1;
+  e->chain_q0 = e->chain_q1 = -1;
   return IS3D_OK;
 }
 
@@ -1481,6 +1523,7 @@ extern "C" int is3d_internal_copy_surface(is3d_engine* e, long n, const double* 
   }
   e->ncell = n;
   e->win_lo = e->win_hi = -1;
+  e->chain_q0 = e->chain_q1 = -1;
   for (int f = 0; f < NSURF && n > 0; f++)
     HIPCHK(e, hipMemcpyPeer(e->d_surf + (size_t)f * n, e->device, src + (size_t)f * src_n + lo, src_device, n * sizeof(double)));
   return IS3D_OK;
@@ -1636,57 +1679,16 @@ static int chain_end(is3d_engine* e) {
   return IS3D_OK;
 }
 
-static int launch_end(is3d_engine* e) {
-  LaunchCtx& L = e->lc;
-  hipStream_t st = L.st;
-  double* dev_out = L.dev_out;
-  HIPCHK(e, hipSetDevice(e->device));
-  if (L.empty) {
-    HIPCHK(e, hipEventRecord(e->ev[1], st));
-    HIPCHK(e, hipEventRecord(e->ev[2], st));
-    HIPCHK(e, hipEventRecord(e->ev[3], st));
-    e->launched = true;
-    return IS3D_OK;
-  }
-  const long n = e->ncell;
-  const int mode = e->p.df_mode, dim = e->p.dimension;
-  const long outsize = is3d_output_size(e);
-  const int np = (int)e->mass.size(), npT = (int)e->pT.size(), nphi = (int)e->phi.size();
-  const int ny_out = (dim == 3) ? (int)e->y.size() : 1;
-  const int nk = ny_out, nl = (dim == 3) ? 1 : (int)e->eta.size();
-  const long wlo = L.wlo, nw = L.nw;
-  const PrepArgs& pa = L.pa;
-  const dim3 g1((unsigned)std::max(1L, (L.p1 - L.p0 + 255) / 256)), b1(256);
-  (void)np;
-  if (mode == PTMA) {
-    hipLaunchKernelGGL(k_famod_b, g1, b1, 0, st, pa, (const double*)e->d_sol);
-    HIPCHK(e, hipGetLastError());
-  }
-  if (mode == PTM) {
-    if (!ensure(e->d_renorm, e->renorm_cap, nw * (long)e->nrcls)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(renorm) failed");
-    RenormArgs ra{};
-    ra.k = pa.k; ra.rec = e->d_rec; ra.aux = e->d_aux; ra.renorm = e->d_renorm;
-    ra.mass = e->d_smass; ra.sign = e->d_ssign; ra.degen = e->d_sdegen; ra.baryon = e->d_sbaryon;
-    ra.c0 = wlo; ra.n = nw; ra.stride = n;
-    ra.npart = e->nrcls; ra.rrep = e->d_rrep;
-    const long tot = nw * (long)e->nrcls;
-    hipLaunchKernelGGL(k_renorm, dim3((unsigned)std::max(1L, (tot + 255) / 256)), dim3(256), 0, st, ra);
-    HIPCHK(e, hipGetLastError());
-  }
-  HIPCHK(e, hipEventRecord(e->ev[1], st));
-  // the integral and the reduction see the window only: records from wlo on, nw cells
-  const double* rec_w = e->d_rec + wlo * (long)NREC;
-  // --- main integral
-  // Grad / RTA-CE: a surface with cells whose lanes may leave the fast path (k_prep's cnt[4]; none in any
-  // tabulated delta-f range) takes the F_TB kernels, which carry the slow loop; the F_TS kernels do not
-  bool allow_ts = true;
-  if (mode <= CE) {
-    unsigned long long nslow = 0;
-    HIPCHK(e, hipMemcpyAsync(&nslow, e->d_cnt + 4, sizeof(nslow), hipMemcpyDeviceToHost, st));
-    HIPCHK(e, hipStreamSynchronize(st));
-    allow_ts = nslow == 0;
-  }
-  const SpectraPlan P = spectra_plan(e, allow_ts);
+// Cell splits and slab geometry of one k_spectra plan over a launch window of nw cells.
+struct IntegralPlan {
+  SpectraPlan P;
+  long ntask = 0, bx = 0, wgs = 0, nsplit = 0, cps = 0, sstride = 0, nsplit_fb = 0;
+};
+
+static int integral_plan(is3d_engine* e, const SpectraPlan& P, long nw, IntegralPlan& I) {
+  const int dim = e->p.dimension, mode = e->p.df_mode;
+  const int npT = (int)e->pT.size();
+  const int nk = (dim == 3) ? (int)e->y.size() : 1, nl = (dim == 3) ? 1 : (int)e->eta.size();
   const int KJ = P.KJ, njb = P.njb;
   if (!spectra_kj_supported(KJ)) return e->fail(IS3D_ERR_ARG, "internal: no k_spectra instantiation for this phi block");
   if (P.shmem > 160 * 1024) return e->fail(IS3D_ERR_ARG, "momentum grid too large for the LDS tile (phi table)");
@@ -1715,19 +1717,32 @@ static int launch_end(is3d_engine* e) {
   // while the F_LY launch of the modified modes lost 14% with it: profiles/round3_r3p_ab_fill.log)
   const long by_fill = ((P.mp ? IS3D_FILL_WGS_MP : IS3D_FILL_WGS) + wgs - 1) / wgs;
   const long by_l2 = ((long)NREC * 8 * nw + IS3D_SPLIT_BYTES - 1) / IS3D_SPLIT_BYTES;
-  const long sstride0 = (long)npT * bx * KJ * kBlock;
-  const long max_slabs = std::max(8L, std::min((long)IS3D_MAX_SPLITS, (long)(IS3D_SLAB_BYTES / 8) / std::max(1L, sstride0)));
+  const long sstride = (long)npT * bx * KJ * kBlock;
+  const long max_slabs = std::max(8L, std::min((long)IS3D_MAX_SPLITS, (long)(IS3D_SLAB_BYTES / 8) / std::max(1L, sstride)));
   long nsplit = std::max(by_fill, std::min(by_l2, max_slabs));
   if (nsplit >= 8) nsplit = (nsplit + 7) / 8 * 8;
   nsplit = std::max(1L, std::min(nsplit, max_split));
   long cps = std::max(1L, (nw + nsplit - 1) / nsplit);
   cps = ((cps + kTile - 1) / kTile) * kTile;
   nsplit = std::max(1L, (nw + cps - 1) / cps);
-  const long sstride = (long)npT * bx * KJ * kBlock;
+  I.P = P; I.ntask = ntask; I.bx = bx; I.wgs = wgs; I.nsplit = nsplit; I.cps = cps; I.sstride = sstride;
   // modified modes: the F_FB launch (separable-fallback lanes, cells listed by k_fbscan) writes its own
   // nsplit_fb slabs after the main ones; k_reduce sums both
-  const long nsplit_fb = (mode >= PTM) ? std::max(1L, std::min(nsplit, 8L)) : 0;
-  if (!ensure(e->d_slab, e->slab_cap, (nsplit + nsplit_fb) * sstride)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(slabs) failed");
+  I.nsplit_fb = (mode >= PTM) ? std::max(1L, std::min(nsplit, 8L)) : 0;
+  return IS3D_OK;
+}
+
+// the integral of one plan over the launch window (records rec_w, nw cells) into the slabs; gate: launch_end's
+// device-side choice between two plans (kernels.h gate_closed), nullptr = unconditional
+static int enqueue_spectra(is3d_engine* e, const IntegralPlan& I, const double* rec_w, long nw, hipStream_t st,
+                           const unsigned long long* gate, int want) {
+  const SpectraPlan& P = I.P;
+  const int mode = e->p.df_mode, dim = e->p.dimension;
+  const int npT = (int)e->pT.size(), nphi = (int)e->phi.size();
+  const int ny_out = (dim == 3) ? (int)e->y.size() : 1;
+  const int nk = ny_out, nl = (dim == 3) ? 1 : (int)e->eta.size();
+  const int KJ = P.KJ, njb = P.njb, nc = e->ncls;
+  const long nsplit = I.nsplit, cps = I.cps, wgs = I.wgs;
   if (mode >= PTM) {
     if (!ensure(e->d_fb, e->fb_cap, nw + 1)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(fallback list) failed");
     hipLaunchKernelGGL(k_fbscan, dim3(1), dim3(1024), 0, st, rec_w, nw, e->d_fb + 1, e->d_fb);
@@ -1735,30 +1750,34 @@ static int launch_end(is3d_engine* e) {
   }
   SpecArgs sa{};
   sa.err = e->d_err;
-  sa.rec = rec_w; sa.n = nw; sa.renorm = e->d_renorm; sa.rcls = e->d_crcls; sa.nrcls = e->nrcls; sa.slab = e->d_slab; sa.outsize = outsize;
+  sa.rec = rec_w; sa.n = nw; sa.renorm = e->d_renorm; sa.rcls = e->d_crcls; sa.nrcls = e->nrcls; sa.slab = e->d_slab;
+  sa.outsize = is3d_output_size(e);
   sa.smass = e->d_cmass; sa.ssign = e->d_csign; sa.sbaryon = e->d_cbaryon; sa.sorig = e->d_sorig;
   sa.csg = e->d_csg;
   sa.pT = e->d_pT; sa.cphi = e->d_cphi; sa.sphi = e->d_sphi; sa.yv = e->d_y; sa.etav = e->d_eta; sa.etaw = e->d_etaw;
   sa.npart = nc; sa.npT = npT; sa.nphi = nphi; sa.ny_out = ny_out; sa.nk = nk; sa.nl = nl; sa.nq = nk * nl; sa.njb = njb;
   sa.nqmax = P.nqmax;
-  sa.ntask = ntask; sa.cells_per_split = cps; sa.nbx = (int)bx; sa.nsplit = (int)nsplit; sa.sstride = sstride;
+  sa.ntask = I.ntask; sa.cells_per_split = cps; sa.nbx = (int)I.bx; sa.nsplit = (int)nsplit; sa.sstride = I.sstride;
   sa.npw = P.npw;
   sa.regulate = e->p.regulate_deltaf; sa.outflow = e->p.outflow; sa.dim = dim; sa.op = 1;
+  sa.gate = gate; sa.gate_want = want;
   const size_t shmem = P.shmem;
   const int tb = P.tb | P.ly | P.t8 | P.mp | P.ts | P.by;
   const int kflags = (e->p.regulate_deltaf ? F_REG : 0) | (e->p.outflow ? F_OUT : 0) | tb;
   if (P.ts) {
     // F_TS: k_phitab writes the per-(cell, pT, phi) rows of a chunk of whole cell splits (at most
-    // IS3D_PHITAB_BYTES), then k_spectra integrates that chunk's splits; one chunk at config 2 (3.7 GB).  Several
-    // chunks (config 4: 61 GB of rows) alternate between the launch stream and a side stream with a table buffer
-    // each, so the next chunk's k_phitab and the first workgroups of its k_spectra fill the CUs the previous
-    // launch's last workgroups leave idle (config 4: 11 chunks ran 2811 ms back to back, one 61 GB chunk 2739 ms)
+    // phitab_chunk bytes, is3d_set_tuning), then k_spectra integrates that chunk's splits; one chunk at config 2
+    // (3.7 GB).  Several chunks (config 4: 61 GB of rows) alternate between the launch stream and a side stream
+    // with a table buffer each, so the next chunk's k_phitab and the first workgroups of its k_spectra fill the
+    // CUs the previous launch's last workgroups leave idle (config 4: 11 chunks ran 2811 ms back to back, one
+    // 61 GB chunk 2739 ms)
     const long rw = phitab_row(mode, KJ, P.by != 0);
     const long per_split = cps * (long)npT * rw;
     const long whole = per_split * nsplit * 8;          // bytes of the whole surface's rows
-    const long budget = whole <= IS3D_PHITAB_ONE ? whole : (long)IS3D_PHITAB_BYTES;
+    const long budget = whole <= e->phitab_one ? whole : e->phitab_chunk;
     const long spc = std::max(1L, std::min(nsplit, budget / 8 / per_split));
     const long phn = spc * cps, nchunk = (nsplit + spc - 1) / spc;
+    e->last_nchunk = nchunk;
     if (!ensure(e->d_phtab, e->phtab_cap, phn * npT * rw)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(phi tables) failed");
     if (nchunk > 1) {
       if (!ensure(e->d_phtab2, e->phtab2_cap, phn * npT * rw)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(phi tables) failed");
@@ -1776,6 +1795,7 @@ static int launch_end(is3d_engine* e) {
       PhiTabArgs ta{};
       ta.rec = rec_w; ta.c0 = c0; ta.nc = ncc; ta.pT = e->d_pT; ta.cphi = e->d_cphi; ta.sphi = e->d_sphi;
       ta.npT = npT; ta.nphi = nphi; ta.nphp = KJ; ta.tab = tab; ta.phn = phn; ta.by = P.by != 0;
+      ta.gate = gate; ta.gate_want = want;
       SpecArgs sc = sa;
       sc.split0 = (int)s0; sc.nsplit = (int)ns; sc.phtab = tab; sc.phn = phn; sc.phc0 = c0; sc.phrow = (int)rw;
       const dim3 grid((unsigned)(wgs * ns));
@@ -1805,10 +1825,10 @@ static int launch_end(is3d_engine* e) {
   HIPCHK(e, hipGetLastError());
   if (mode >= PTM) {
     SpecArgs fa = sa;
-    fa.slab = e->d_slab + nsplit * sstride; fa.nsplit = (int)nsplit_fb; fa.cells_per_split = 0;
+    fa.slab = e->d_slab + nsplit * I.sstride; fa.nsplit = (int)I.nsplit_fb; fa.cells_per_split = 0;
     fa.fbcells = e->d_fb + 1; fa.fbcount = e->d_fb;
     const int fflags = (e->p.regulate_deltaf ? F_REG : 0) | (e->p.outflow ? F_OUT : 0) | F_FB;
-    const dim3 gfb((unsigned)(bx * npT * nsplit_fb));
+    const dim3 gfb((unsigned)(I.bx * npT * I.nsplit_fb));
     switch (mode) {
       case PTM: launch_spectra<PTM>(gfb, P.shmem_fb, st, fa, fflags, KJ); break;
       case PTB: launch_spectra<PTB>(gfb, P.shmem_fb, st, fa, fflags, KJ); break;
@@ -1816,22 +1836,96 @@ static int launch_end(is3d_engine* e) {
     }
     HIPCHK(e, hipGetLastError());
   }
-  HIPCHK(e, hipEventRecord(e->ev[2], st));
+  return IS3D_OK;
+}
+
+// sum of one plan's slabs into the reference-layout output (k_reduce / k_reduce_wave), gated as enqueue_spectra
+static int enqueue_reduce(is3d_engine* e, const IntegralPlan& I, double* dev_out, hipStream_t st,
+                          const unsigned long long* gate, int want) {
+  const int dim = e->p.dimension;
+  const int npT = (int)e->pT.size(), nphi = (int)e->phi.size();
+  const int ny_out = (dim == 3) ? (int)e->y.size() : 1;
+  const int nk = ny_out, nl = (dim == 3) ? 1 : (int)e->eta.size();
+  const int nc = e->ncls;
   ReduceArgs ra{};
-  ra.slab = e->d_slab; ra.sstride = sstride; ra.nsplit = (int)(nsplit + nsplit_fb);
-  ra.nbx = (int)bx; ra.npart = nc; ra.npT = npT; ra.nphi = nphi; ra.nk = nk; ra.nl = nl; ra.ny_out = ny_out; ra.kj = KJ;
-  ra.ntask = ntask;
+  ra.slab = e->d_slab; ra.sstride = I.sstride; ra.nsplit = (int)(I.nsplit + I.nsplit_fb);
+  ra.nbx = (int)I.bx; ra.npart = nc; ra.npT = npT; ra.nphi = nphi; ra.nk = nk; ra.nl = nl; ra.ny_out = ny_out; ra.kj = I.P.KJ;
+  ra.ntask = I.ntask;
   ra.sorig = e->d_sorig; ra.degen_orig = e->d_degen_orig; ra.prefactor = std::pow(2.0 * M_PI * kHbarC, -3);
   ra.cmem_off = e->d_cmem_off; ra.cmem = e->d_cmem;
   ra.out = dev_out;
+  ra.gate = gate; ra.gate_want = want;
   // one wavefront per output when each output sums many (eta node, split) terms and there are few outputs
-  if ((long)nl * ra.nsplit >= 128 && sstride / nl < (1L << 20)) {
+  if ((long)nl * ra.nsplit >= 128 && I.sstride / nl < (1L << 20)) {
     const long nout = (long)nc * npT * nphi * ny_out;
     hipLaunchKernelGGL(k_reduce_wave, dim3((unsigned)((nout + 3) / 4)), dim3(256), 0, st, ra);
   } else {
-    hipLaunchKernelGGL(k_reduce, dim3((unsigned)((sstride + 255) / 256)), dim3(256), 0, st, ra);
+    hipLaunchKernelGGL(k_reduce, dim3((unsigned)((I.sstride + 255) / 256)), dim3(256), 0, st, ra);
   }
   HIPCHK(e, hipGetLastError());
+  return IS3D_OK;
+}
+
+static int launch_end(is3d_engine* e) {
+  LaunchCtx& L = e->lc;
+  hipStream_t st = L.st;
+  double* dev_out = L.dev_out;
+  HIPCHK(e, hipSetDevice(e->device));
+  if (L.empty) {
+    HIPCHK(e, hipEventRecord(e->ev[1], st));
+    HIPCHK(e, hipEventRecord(e->ev[2], st));
+    HIPCHK(e, hipEventRecord(e->ev[3], st));
+    e->launched = true;
+    return IS3D_OK;
+  }
+  const long n = e->ncell;
+  const int mode = e->p.df_mode;
+  const long wlo = L.wlo, nw = L.nw;
+  const PrepArgs& pa = L.pa;
+  const dim3 g1((unsigned)std::max(1L, (L.p1 - L.p0 + 255) / 256)), b1(256);
+  if (mode == PTMA) {
+    hipLaunchKernelGGL(k_famod_b, g1, b1, 0, st, pa, (const double*)e->d_sol);
+    HIPCHK(e, hipGetLastError());
+  }
+  if (mode == PTM) {
+    if (!ensure(e->d_renorm, e->renorm_cap, nw * (long)e->nrcls)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(renorm) failed");
+    RenormArgs ra{};
+    ra.k = pa.k; ra.rec = e->d_rec; ra.aux = e->d_aux; ra.renorm = e->d_renorm;
+    ra.mass = e->d_smass; ra.sign = e->d_ssign; ra.degen = e->d_sdegen; ra.baryon = e->d_sbaryon;
+    ra.c0 = wlo; ra.n = nw; ra.stride = n;
+    ra.npart = e->nrcls; ra.rrep = e->d_rrep;
+    const long tot = nw * (long)e->nrcls;
+    hipLaunchKernelGGL(k_renorm, dim3((unsigned)std::max(1L, (tot + 255) / 256)), dim3(256), 0, st, ra);
+    HIPCHK(e, hipGetLastError());
+  }
+  HIPCHK(e, hipEventRecord(e->ev[1], st));
+  // the integral and the reduction see the window only: records from wlo on, nw cells
+  const double* rec_w = e->d_rec + wlo * (long)NREC;
+  // --- main integral
+  // Grad / RTA-CE F_TS: a surface with cells whose lanes may leave the fast path (k_prep counts them in cnt[4]; none
+  // in any tabulated delta-f range) needs the kernels that carry the slow loop, which the F_TS ones do not.  The
+  // choice is made on the device: both plans are enqueued, each gated on cnt[4] (gate_closed: the other plan's
+  // workgroups return at once, ~10 us), so is3d_launch never waits for the prepass (no host round trip)
+  const SpectraPlan P = spectra_plan(e, true);
+  e->last_nchunk = 0;
+  IntegralPlan I{}, J{};
+  int rc = integral_plan(e, P, nw, I);
+  if (rc) return rc;
+  const bool gated = mode <= CE && P.ts;
+  if (gated) {
+    rc = integral_plan(e, spectra_plan(e, false), nw, J);
+    if (rc) return rc;
+  }
+  const long slab_need = std::max((I.nsplit + I.nsplit_fb) * I.sstride, gated ? (J.nsplit + J.nsplit_fb) * J.sstride : 0L);
+  if (!ensure(e->d_slab, e->slab_cap, slab_need)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(slabs) failed");
+  const unsigned long long* gate = gated ? e->d_cnt + 4 : nullptr;
+  rc = enqueue_spectra(e, I, rec_w, nw, st, gate, 0);
+  if (!rc && gated) rc = enqueue_spectra(e, J, rec_w, nw, st, gate, 1);
+  if (rc) return rc;
+  HIPCHK(e, hipEventRecord(e->ev[2], st));
+  rc = enqueue_reduce(e, I, dev_out, st, gate, 0);
+  if (!rc && gated) rc = enqueue_reduce(e, J, dev_out, st, gate, 1);
+  if (rc) return rc;
   HIPCHK(e, hipEventRecord(e->ev[3], st));
   e->launched = true;
   return IS3D_OK;
@@ -1840,6 +1934,9 @@ static int launch_end(is3d_engine* e) {
 extern "C" int is3d_launch(is3d_engine* e, double* dev_out, void* stream) {
   if (e && e->grp) return is3d::group_launch(e->grp, dev_out, stream);
   if (!e) return IS3D_ERR_ARG;
+  if (e->chain_q1 >= 0)
+    return e->fail(IS3D_ERR_STATE, "a chain range (is3d_set_chain_range) runs through the staged launch: its first "
+                                   "positions need the previous range's boundary states");
   int rc = launch_begin(e, dev_out, stream, 0, -1, 0);
   for (int pass = 0; !rc && e->lc.chained && pass < e->lc.ca.npass; pass++) rc = chain_pass(e, pass);
   if (!rc) rc = chain_end(e);
@@ -1862,6 +1959,59 @@ double* is3d_internal_chain_bnd(is3d_engine* e, int out, int slot) {
 }
 long is3d_internal_chain_bnd_bytes(const is3d_engine* e) { return (4 * e->lc.ca.C + 1) * (long)sizeof(double); }
 
+// ---- staged launch for PTMA warm-start chains split over processes (include/is3d_amd.h) ----------------------------
+extern "C" int is3d_set_chain_range(is3d_engine* e, long q0, long q1) {
+  if (!e) return IS3D_ERR_ARG;
+  if (e->grp) return is3d::group_fail(e->grp, IS3D_ERR_UNSUPPORTED, "a device-list engine splits its chains itself");
+  if (q0 < 0 || q1 < 0) { e->chain_q0 = e->chain_q1 = -1; e->win_lo = e->win_hi = -1; return IS3D_OK; }
+  if (!e->have_params || e->p.df_mode != PTMA || e->p.famod_chains <= 0)
+    return e->fail(IS3D_ERR_STATE, "a chain range needs PTMA (df_mode 5) with famod_chains > 0 set first");
+  const long n = e->ncell, C = std::max(1L, std::min<long>(e->p.famod_chains, std::max(n, 1L))), P = (n + C - 1) / C;
+  if (q0 > q1 || q1 > P) return e->fail(IS3D_ERR_ARG, "chain range outside the surface's chain positions");
+  e->win_lo = std::min(n, q0 * C);
+  e->win_hi = std::min(n, q1 * C);
+  e->chain_q0 = q0; e->chain_q1 = q1;
+  return IS3D_OK;
+}
+
+extern "C" int is3d_launch_begin(is3d_engine* e, double* dev_out, void* stream) {
+  if (!e) return IS3D_ERR_ARG;
+  if (e->grp) return is3d::group_fail(e->grp, IS3D_ERR_UNSUPPORTED, "the staged launch runs on one-device engines");
+  if (e->chain_q1 >= 0 && (e->p.df_mode != PTMA || e->p.famod_chains <= 0))
+    return e->fail(IS3D_ERR_STATE, "a chain range needs PTMA with famod_chains > 0 (params changed since)");
+  const bool range = e->chain_q1 >= 0;
+  return launch_begin(e, dev_out, stream, range ? e->chain_q0 : 0, range ? e->chain_q1 : -1, range && e->chain_q0 > 0);
+}
+extern "C" int is3d_chain_passes(const is3d_engine* e) { return e && !e->grp ? is3d_internal_chain_npass(e) : 0; }
+extern "C" int is3d_chain_pass(is3d_engine* e, int pass) {
+  if (!e || e->grp) return IS3D_ERR_ARG;
+  if (pass < 0 || pass >= is3d_internal_chain_npass(e)) return e->fail(IS3D_ERR_ARG, "chain pass out of range");
+  return chain_pass(e, pass);
+}
+extern "C" int is3d_chain_end(is3d_engine* e) { return (!e || e->grp) ? IS3D_ERR_ARG : chain_end(e); }
+extern "C" int is3d_launch_end(is3d_engine* e) { return (!e || e->grp) ? IS3D_ERR_ARG : launch_end(e); }
+extern "C" long is3d_chain_boundary_size(const is3d_engine* e) {
+  return (e && !e->grp && e->lc.chained && !e->lc.empty) ? 4 * e->lc.ca.C + 1 : 0;
+}
+// boundary slot `slot` (0, 1: pass parity, 2: the finisher's) out of this range into dev_buf / from dev_buf into this
+// range's incoming slot, on the launch stream (hipMemcpyDefault: a host buffer works too, read after a stream sync)
+extern "C" int is3d_chain_boundary_get(is3d_engine* e, int slot, double* dev_buf) {
+  if (!e || e->grp || !dev_buf || slot < 0 || slot >= kBndSlots) return e ? e->fail(IS3D_ERR_ARG, "bad chain boundary slot") : IS3D_ERR_ARG;
+  const long nb = is3d_chain_boundary_size(e);
+  if (nb == 0) return e->fail(IS3D_ERR_STATE, "no chains in the launch in flight");
+  HIPCHK(e, hipSetDevice(e->device));
+  HIPCHK(e, hipMemcpyAsync(dev_buf, is3d_internal_chain_bnd(e, 1, slot), nb * sizeof(double), hipMemcpyDefault, e->lc.st));
+  return IS3D_OK;
+}
+extern "C" int is3d_chain_boundary_put(is3d_engine* e, int slot, const double* dev_buf) {
+  if (!e || e->grp || !dev_buf || slot < 0 || slot >= kBndSlots) return e ? e->fail(IS3D_ERR_ARG, "bad chain boundary slot") : IS3D_ERR_ARG;
+  const long nb = is3d_chain_boundary_size(e);
+  if (nb == 0) return e->fail(IS3D_ERR_STATE, "no chains in the launch in flight");
+  HIPCHK(e, hipSetDevice(e->device));
+  HIPCHK(e, hipMemcpyAsync(is3d_internal_chain_bnd(e, 0, slot), dev_buf, nb * sizeof(double), hipMemcpyDefault, e->lc.st));
+  return IS3D_OK;
+}
+
 extern "C" int is3d_cell_costs(is3d_engine* e, double* cost) {
   if (e && e->grp) return is3d::group_fail(e->grp, IS3D_ERR_UNSUPPORTED, "is3d_cell_costs: call it on a one-device engine");
   if (!e || !cost) return IS3D_ERR_ARG;
@@ -1871,17 +2021,23 @@ extern "C" int is3d_cell_costs(is3d_engine* e, double* cost) {
   if (n <= 0) return IS3D_OK;
   HIPCHK(e, hipSetDevice(e->device));
   const int mode = e->p.df_mode;
-  if (!ensure(e->d_rec, e->rec_cap, (long)NREC * n)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(records) failed");
-  if (!ensure(e->d_aux, e->aux_cap, 9L * n)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(aux) failed");
-  double* d_cost = nullptr;
-  HIPCHK(e, hipMalloc(&d_cost, n * sizeof(double)));
+  // private scratch (records, aux, cost, error word, counters), freed on return: a launch in flight keeps its
+  // buffers and the error word is3d_finish reports, and a device group's cost prepass over the whole surface
+  // (group_set_surface on shard 0) leaves no full-surface-sized buffers behind on that shard
+  double* scratch = nullptr;
+  const size_t nd = (size_t)(NREC + 9 + 1) * n + 9;
+  HIPCHK(e, hipMalloc(&scratch, nd * sizeof(double)));
+  double* d_rec = scratch;
+  double* d_aux = d_rec + (size_t)NREC * n;
+  double* d_cost = d_aux + 9 * (size_t)n;
+  int* d_err = (int*)(d_cost + n);
+  unsigned long long* d_cnt = (unsigned long long*)(d_cost + n + 1);
   PrepArgs pa{};
-  pa.k = make_consts(e); pa.tb = e->dtb; pa.surf = e->d_surf; pa.rec = e->d_rec; pa.aux = e->d_aux; pa.n = n;
+  pa.k = make_consts(e); pa.tb = e->dtb; pa.surf = e->d_surf; pa.rec = d_rec; pa.aux = d_aux; pa.n = n;
   pa.c0 = 0; pa.c1 = n;
-  pa.err = e->d_err; pa.cnt = e->d_cnt;
+  pa.err = d_err; pa.cnt = d_cnt;
   const dim3 g1((unsigned)((n + 255) / 256)), b1(256);
-  hipError_t er = hipMemsetAsync(e->d_err, 0, sizeof(int), nullptr);
-  if (er == hipSuccess) er = hipMemsetAsync(e->d_cnt, 0, 8 * sizeof(unsigned long long), nullptr);
+  hipError_t er = hipMemsetAsync(d_err, 0, 9 * sizeof(double), nullptr);
   switch (mode) {
     case GRAD: hipLaunchKernelGGL(k_prep<GRAD>, g1, b1, 0, nullptr, pa); break;
     case CE: hipLaunchKernelGGL(k_prep<CE>, g1, b1, 0, nullptr, pa); break;
@@ -1892,10 +2048,10 @@ extern "C" int is3d_cell_costs(is3d_engine* e, double* cost) {
   // separable-fallback cells of PTM / PTB relative to a modified cell (config-2 shape, MI355X,
   // tools/fb_cost_probe.py: PTM 1.37-1.43, PTB 1.58-1.80)
   const double fb_cost = mode == PTM ? 1.4 : mode == PTB ? 1.8 : 0.0;
-  hipLaunchKernelGGL(k_cell_cost, g1, b1, 0, nullptr, (const double*)e->d_rec, n, fb_cost, d_cost);
+  hipLaunchKernelGGL(k_cell_cost, g1, b1, 0, nullptr, (const double*)d_rec, n, fb_cost, d_cost);
   if (er == hipSuccess) er = hipGetLastError();
   if (er == hipSuccess) er = hipMemcpy(cost, d_cost, n * sizeof(double), hipMemcpyDeviceToHost);
-  (void)hipFree(d_cost);
+  (void)hipFree(scratch);
   if (er != hipSuccess) return e->fail(IS3D_ERR_DEVICE, std::string("is3d_cell_costs: ") + hipGetErrorString(er));
   return IS3D_OK;
 }

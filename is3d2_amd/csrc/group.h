@@ -22,6 +22,8 @@ void group_destroy(Group* g);
 const char* group_error(const Group* g);
 
 int group_set_params(Group* g, const is3d_params* p);
+int group_set_tuning(Group* g, const char* key, long value);
+long group_get_tuning(const Group* g, const char* key);   // shard 0's value; "phitab_chunks": the max over shards
 int group_set_species(Group* g, int n, const double* mass, const double* sign, const double* degen, const double* baryon);
 int group_set_species_classes(Group* g, int on);
 int group_species_integrated(Group* g);

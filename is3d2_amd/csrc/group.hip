@@ -180,6 +180,15 @@ int group_set_params(Group* g, const is3d_params* p) {
   if (!rc) { g->p = *p; g->have_params = true; }
   return rc;
 }
+int group_set_tuning(Group* g, const char* key, long value) {
+  return each(g, [&](is3d_engine* e) { return is3d_set_tuning(e, key, value); });
+}
+long group_get_tuning(const Group* g, const char* key) {
+  if (std::strcmp(key, "phitab_chunks")) return is3d_get_tuning(g->sh[0], key);
+  long m = 0;
+  for (auto* e : g->sh) m = std::max(m, is3d_get_tuning(e, key));
+  return m;
+}
 int group_set_species(Group* g, int n, const double* m, const double* s, const double* d, const double* b) {
   const int rc = each(g, [&](is3d_engine* e) { return is3d_set_species(e, n, m, s, d, b); });
   if (!rc) g->np = n;

@@ -98,7 +98,14 @@ struct SpecArgs {
   int split0;                 // first cell split of this launch (F_TS launches cover the splits chunk by chunk)
   // F_TS: the per-(cell, pT, phi) tables k_phitab wrote for this chunk of cells, rows [pT][cell - phc0][phrow]
   const double* phtab; long phn, phc0; int phrow;
+  // device-side choice between two enqueued plans (engine.hip launch_end): the workgroups return at once unless
+  // (*gate != 0) == gate_want; gate = nullptr: always run
+  const unsigned long long* gate; int gate_want;
 };
+
+__device__ __forceinline__ bool gate_closed(const unsigned long long* gate, int want) {
+  return gate && ((*gate != 0ULL) != (want != 0));
+}
 
 // flag bits of the spectra kernel instantiation
 // F_TB (Grad / RTA-CE, include_baryon = 0, one phi block, KJ % 4 == 0): linear delta-f part from the
@@ -250,6 +257,7 @@ struct PhiTabArgs {
   int npT, nphi, nphp;
   double* tab; long phn;                    // rows per pT plane (>= nc)
   int by;                                   // F_BY: rows carry T3
+  const unsigned long long* gate; int gate_want;   // as SpecArgs
 };
 
 template <int MODE>
@@ -648,6 +656,7 @@ __device__ __forceinline__ void wait_fetch() { asm volatile("s_waitcnt vmcnt(0)"
 // summed by k_reduce, so a few species still fill the wavefronts
 template <int MODE, int FLAGS, int KJ>
 __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void k_spectra(SpecArgs A) {
+  if (gate_closed(A.gate, A.gate_want)) return;
   constexpr int kTile = spectra_tile<MODE, FLAGS>();      // cells per LDS tile for this mode / launch
   extern __shared__ double smem[];
   const int nphp = A.njb * KJ;                            // phi rows padded to KJ multiples
@@ -1281,6 +1290,7 @@ __global__ __launch_bounds__(kBlock, dndx_waves<MODE>()) void k_dndx(DndxArgs A)
 // padding slots and cells with u.dsigma <= 0 get zeros, as in the LDS tables.
 template <int MODE>
 __global__ __launch_bounds__(256) void k_phitab(PhiTabArgs A) {
+  if (gate_closed(A.gate, A.gate_want)) return;
   __shared__ double s_etab[kExpTabN];
   for (int i = threadIdx.x; i < kExpTabN; i += 256) s_etab[i] = kExp2Tab[i];
   __syncthreads();

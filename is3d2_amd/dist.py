@@ -9,8 +9,10 @@ ds_max-weighted Plasma average (5 sums) the PTB table needs (readindata.cpp:316-
 Shards are contiguous cell ranges balanced by estimated cost: a cell with
 u.dsigma <= 0 is skipped by every kernel (MomentumSpectra.cpp:132) and costs only its record prep.
 PTMA with the reference's warm-start chains (famod_chains > 0) is a serial recurrence over the whole
-surface: every rank then holds the whole surface, walks the chains itself and integrates its range
-only (Engine.set_cell_window), so each rank sees the serial chain's solutions.
+surface (MomentumSpectra.cpp:1132-1135, 1308-1364): every rank then holds the whole surface and solves only its
+range of chain positions (Engine.set_chain_range), starting each chain from the end state the previous rank
+sends after every pass of the segmented solve (launch_chained: point-to-point send / recv of 4 C + 1 doubles per
+pass, RCCL on the GPU), so each rank's solutions are the serial chain's and its prepass shrinks with the rank count.
 """
 import numpy as np
 
@@ -91,3 +93,64 @@ def torch_all_reduce(dist, device=None):
         dist.all_reduce(t)
         return t.cpu().numpy()
     return f
+
+
+def chain_bounds(surf, rank, world, chains, costs=None):
+    """Chain positions [q0, q1) of `rank` when the PTMA warm-start chains (C = chains) are split over the ranks: the
+    cost-balanced cell boundaries rounded to whole positions (C cells each), as group.hip chain_windows does."""
+    n = len(surf["tau"])
+    C = max(1, min(int(chains), n))
+    P = (n + C - 1) // C
+    r = balanced_ranges(cell_costs(surf) if costs is None else np.asarray(costs), world)
+    q = [0]
+    for k in range(world - 1):
+        q.append(max(q[-1], min(P, (r[k][1] + C // 2) // C)))
+    q.append(P)
+    return q[rank], q[rank + 1]
+
+
+def launch_chained(eng, out_ptr, stream_ptr, rank, world, dist, device=None, sync=None):
+    """One pass of the PTMA hot path with the warm-start chains split over the ranks (include/is3d_amd.h staged
+    launch): rank k solves its chain positions; after every chain pass j but the last it sends its range's end states
+    (slot j & 1) to rank k + 1, which puts them into its incoming slot before its pass j + 1; then the finishers run in
+    rank order, each handing its final states (slot 2) on.  With the 'nccl' backend every copy, send and receive
+    is ordered on the GPU streams (torch's current stream = the launch stream) and the host never waits; with
+    'gloo' the boundary buffers live on the host (device=None) and sync() -- e.g. the launch stream's synchronize --
+    runs after each copy out of the engine, before the send reads the buffer.  Every rank's range must hold at
+    least one position.  The caller then all-reduces the spectra and calls eng.finish()."""
+    import torch
+    eng.launch_begin(out_ptr, stream_ptr)
+    npass, nb = eng.chain_passes(), eng.chain_boundary_size()
+    if npass <= 0 or nb <= 0:
+        raise RuntimeError("launch_chained: rank %d has no PTMA chain positions (empty chain range)" % rank)
+    pred = rank - 1 if rank > 0 else None
+    succ = rank + 1 if rank + 1 < world else None
+    rbuf = [torch.zeros(nb, dtype=torch.float64, device=device) for _ in range(3)]
+    sbuf = [torch.zeros(nb, dtype=torch.float64, device=device) for _ in range(3)]
+    sends = [None, None, None]
+
+    def send(slot):
+        if sends[slot] is not None:
+            sends[slot].wait()          # the buffer's previous send (two passes back) is out before it is rewritten
+        eng.chain_boundary_get(slot, sbuf[slot])
+        if sync is not None:
+            sync()
+        sends[slot] = dist.isend(sbuf[slot], dst=succ)
+
+    for j in range(npass):
+        if pred is not None and j > 0:
+            dist.recv(rbuf[(j - 1) & 1], src=pred)
+            eng.chain_boundary_put((j - 1) & 1, rbuf[(j - 1) & 1])
+        eng.chain_pass(j)
+        if succ is not None and j + 1 < npass:      # the successor reads pass j's states in its pass j + 1
+            send(j & 1)
+    if pred is not None:
+        dist.recv(rbuf[2], src=pred)
+        eng.chain_boundary_put(2, rbuf[2])
+    eng.chain_end()
+    if succ is not None:
+        send(2)
+    eng.launch_end()
+    for w in sends:
+        if w is not None:
+            w.wait()

@@ -83,6 +83,15 @@ class Engine:
         self.params = p
         self._chk(self.lib.is3d_set_params(self._e, C.byref(_lib.Params(**p))))
 
+    def set_tuning(self, key, value):
+        """Engine knob (is3d_set_tuning): "phitab_one_bytes" / "phitab_chunk_bytes" (F_TS table chunking); a
+        negative value restores the default."""
+        self._chk(self.lib.is3d_set_tuning(self._e, key.encode(), int(value)))
+
+    def get_tuning(self, key):
+        """is3d_get_tuning: the knobs above, or "phitab_chunks" (F_TS chunks of the last launch); -1 = unknown."""
+        return self.lib.is3d_get_tuning(self._e, key.encode())
+
     def set_species(self, mass, sign, degen, baryon):
         a = [_arr(x) for x in (mass, sign, degen, baryon)]
         self._chk(self.lib.is3d_set_species(self._e, len(a[0]), *[_dp(x) for x in a]))
@@ -178,6 +187,38 @@ class Engine:
 
     def finish(self):
         self._chk(self.lib.is3d_finish(self._e))
+
+    # --- staged launch: PTMA warm-start chains split over processes (include/is3d_amd.h, dist.launch_chained) ---
+    def set_chain_range(self, q0, q1):
+        """Solve chain positions [q0, q1) of every PTMA warm-start chain and integrate cells [q0 C, q1 C)
+        (-1, -1: off).  Needs the staged launch (dist.launch_chained)."""
+        self._chk(self.lib.is3d_set_chain_range(self._e, int(q0), int(q1)))
+
+    def launch_begin(self, dev_out_ptr, stream_ptr=None):
+        self._chk(self.lib.is3d_launch_begin(self._e, C.c_void_p(dev_out_ptr), C.c_void_p(stream_ptr or 0)))
+
+    def chain_passes(self):
+        return self.lib.is3d_chain_passes(self._e)
+
+    def chain_pass(self, j):
+        self._chk(self.lib.is3d_chain_pass(self._e, int(j)))
+
+    def chain_end(self):
+        self._chk(self.lib.is3d_chain_end(self._e))
+
+    def launch_end(self):
+        self._chk(self.lib.is3d_launch_end(self._e))
+
+    def chain_boundary_size(self):
+        return self.lib.is3d_chain_boundary_size(self._e)
+
+    def chain_boundary_get(self, slot, buf):
+        """Copy this range's boundary slot (0, 1: pass parity, 2: final) into the device tensor buf (launch stream)."""
+        self._chk(self.lib.is3d_chain_boundary_get(self._e, int(slot), C.c_void_p(buf.data_ptr())))
+
+    def chain_boundary_put(self, slot, buf):
+        """Copy the device tensor buf (the previous range's end states) into this range's incoming slot."""
+        self._chk(self.lib.is3d_chain_boundary_put(self._e, int(slot), C.c_void_p(buf.data_ptr())))
 
     def stats(self):
         s = _lib.Stats()

@@ -976,6 +976,83 @@ int orc_aniso_solve(const orc_setup *s, double E, double pl, double pt, double l
   return 0;
 }
 
+/* PTMA warm-start chain state of one OpenMP thread (MomentumSpectra.cpp:1132-1135): the previous successful
+ * cell's (lambda, aT, aL) */
+typedef struct { double lambda_prev, aT_prev, aL_prev; int prev_ok; } chain_state;
+
+/* one cell's warm-started Newton solve and the chain update (MomentumSpectra.cpp:1288-1368): p_L or p_T < 0 passes
+ * the state through (breakdown), a failed warm start retries from (T, 1, 1), a failed retry resets the chain.
+ * Returns 1 when the cell breaks down; lambda / aT / aL hold the cell's solution (or its (T, 1, 1) fallback). */
+static int famod_chain_step(chain_state *cs, double T, double E, double pl, double pt, const hadrons *h,
+                            double *lambda, double *aT, double *aL, tstats *st) {
+  int broken = 0;
+  *lambda = T; *aT = 1; *aL = 1;
+  if (pl < 0 || pt < 0) { st->pl_negative++; broken = 1; }
+  else {
+    if (cs->prev_ok) { *lambda = cs->lambda_prev; *aT = cs->aT_prev; *aL = cs->aL_prev; }
+    aniso X = find_aniso(E, pl, pt, *lambda, *aT, *aL, h);
+    if (X.fail && cs->prev_ok) {
+      *lambda = T; *aT = 1; *aL = 1;
+      X = find_aniso(E, pl, pt, *lambda, *aT, *aL, h);
+      if (X.fail) { broken = 1; st->recon_fail++; cs->prev_ok = 0; }
+      else {
+        *lambda = X.lambda; *aT = X.aT; *aL = X.aL;
+        cs->lambda_prev = *lambda; cs->aT_prev = *aT; cs->aL_prev = *aL; cs->prev_ok = 1;
+      }
+    } else {
+      *lambda = X.lambda; *aT = X.aT; *aL = X.aL;
+      cs->lambda_prev = *lambda; cs->aT_prev = *aT; cs->aL_prev = *aL; cs->prev_ok = 1;
+    }
+    st->iterations += X.iters;
+  }
+  return broken;
+}
+
+/* PTMA warm-start chain over an explicit cell list (test hook for the distributed chain hand-off): the cells are
+ * solved in list order from state[4] = (prev_ok, lambda_prev, aT_prev, aL_prev), with the prologue of
+ * spectra_famod below (MomentumSpectra.cpp:1155-1268) and its chain step; cells with u.dsigma <= 0 are not in the
+ * chain (:1146).  states[4 i + f] = the chain state after cell i, iters[i] = its Newton iterations (-1: skipped);
+ * state returns the state after the last cell.  Returns the sum of iters over the solved cells. */
+long orc_famod_chain(const orc_params *p, const orc_setup *s, const orc_surface *S, const long *cells, long ncells,
+                     double *state, double *states, int *iters) {
+  hadrons h = {s->npdg < 320 ? s->npdg : 320, s->pdg_mass, s->pdg_sign, s->pdg_degen};
+  chain_state cs = {state[1], state[2], state[3], state[0] != 0.0};
+  long total = 0;
+  for (long i = 0; i < ncells; i++) {
+    const long ic = cells[i];
+    double tau = S->tau[ic], tau2 = tau * tau;
+    double dat = S->dat[ic], dax = S->dax[ic], day = S->day[ic], dan = S->dan[ic];
+    double ux = S->ux[ic], uy = S->uy[ic], un = S->un[ic];
+    double ut = sqrt(1. + ux * ux + uy * uy + tau2 * un * un);
+    iters[i] = -1;
+    if (ut * dat + ux * dax + uy * day + un * dan > 0) {
+      double ut2 = ut * ut, ux2 = ux * ux, uy2 = uy * uy;
+      double uperp = sqrt(ux * ux + uy * uy), utperp = sqrt(1. + ux * ux + uy * uy);
+      double T = S->T[ic], P = S->P[ic], E = S->E[ic];
+      double pixx = S->pixx[ic], pixy = S->pixy[ic], pixn = S->pixn[ic], piyy = S->piyy[ic], piyn = S->piyn[ic];
+      double pinn = (pixx * (ux2 - ut2) + piyy * (uy2 - ut2) + 2. * (pixy * ux * uy + tau2 * un * (pixn * ux + piyn * uy))) / (tau2 * utperp * utperp);
+      double pitn = (pixn * ux + piyn * uy + tau2 * pinn * un) / ut;
+      double pity = (pixy * ux + piyy * uy + tau2 * piyn * un) / ut;
+      double pitx = (pixx * ux + pixy * uy + tau2 * pixn * un) / ut;
+      double pitt = (pitx * ux + pity * uy + tau2 * pitn * un) / ut;
+      double bulkPi = S->bulkPi[ic];
+      milne b = milne_basis(ut, ux, uy, un, uperp, utperp, tau);
+      pilrf pl_ = boost_pimunu(b, tau2, pitt, pitx, pity, pitn, pixx, pixy, pixn, piyy, piyn, pinn);
+      double pl = P + bulkPi + pl_.zz, pt = P + bulkPi - pl_.zz / 2.;
+      tstats st = {0, 0, 0, 0, 0, 0};
+      double lambda, aT, aL;
+      famod_chain_step(&cs, T, E, pl, pt, &h, &lambda, &aT, &aL, &st);
+      iters[i] = (int)st.iterations;
+      total += st.iterations;
+    }
+    states[4 * i] = cs.prev_ok; states[4 * i + 1] = cs.lambda_prev; states[4 * i + 2] = cs.aT_prev; states[4 * i + 3] = cs.aL_prev;
+  }
+  (void)p;
+  state[0] = cs.prev_ok; state[1] = cs.lambda_prev; state[2] = cs.aT_prev; state[3] = cs.aL_prev;
+  return total;
+}
+
+
 /* ------------------------------------------------------------------------- */
 /* calculate_dN_pTdpTdphidy_famod  (MomentumSpectra.cpp:1049-1682)            */
 /* ------------------------------------------------------------------------- */
@@ -986,8 +1063,7 @@ static void spectra_famod(const orc_params *p, const orc_setup *s, const orc_sur
   const int DIMENSION = p->dimension;
   const double detB_min = p->deta_min;
   hadrons h = {s->npdg < 320 ? s->npdg : 320, s->pdg_mass, s->pdg_sign, s->pdg_degen};  /* :1295 */
-  double lambda_prev = 0, aT_prev = 0, aL_prev = 0;
-  int prev_ok = 0;
+  chain_state cs = {0, 0, 0, 0};
   double B_copy[3][3], B_inv[3][3];
   CELL_LOOP_BEGIN(n, C, S->n, ic)
     double tau = S->tau[ic], tau2 = tau * tau;
@@ -1018,22 +1094,7 @@ static void spectra_famod(const orc_params *p, const orc_setup *s, const orc_sur
       WTzx = pl_.xz; WTzy = pl_.yz;
     }
     double lambda = T, aT = 1, aL = 1, upsilonB = alphaB;
-    int broken = 0;
-    if (pl < 0 || pt < 0) { st->pl_negative++; broken = 1; }
-    else {
-      if (prev_ok) { lambda = lambda_prev; aT = aT_prev; aL = aL_prev; }
-      aniso X = find_aniso(E, pl, pt, lambda, aT, aL, &h);
-      if (X.fail && prev_ok) {
-        lambda = T; aT = 1; aL = 1;
-        X = find_aniso(E, pl, pt, lambda, aT, aL, &h);
-        if (X.fail) { broken = 1; st->recon_fail++; prev_ok = 0; }
-        else { lambda = X.lambda; aT = X.aT; aL = X.aL; lambda_prev = lambda; aT_prev = aT; aL_prev = aL; prev_ok = 1; }
-      } else {
-        lambda = X.lambda; aT = X.aT; aL = X.aL;
-        lambda_prev = lambda; aT_prev = aT; aL_prev = aL; prev_ok = 1;
-      }
-      st->iterations += X.iters;
-    }
+    int broken = famod_chain_step(&cs, T, E, pl, pt, &h, &lambda, &aT, &aL, st);
     double bpi, bW;
     famod_coefficient(lambda, aT, aL, &h, &bpi, &bW);
     double shear_coeff = 0.5 / bpi, diff_coeff = 1. / bW;

@@ -136,6 +136,11 @@ int orc_jonah_table(const orc_setup *s, double *lambda2, double *z, double *bulk
 void orc_surface_averages(const orc_surface *surf, double *out5);
 int orc_aniso_solve(const orc_setup *s, double E, double pl, double pt, double l0,
                     double aT0, double aL0, double *out6);
+/* PTMA warm-start chain over an explicit cell list from state[4] = (prev_ok, lambda, aT, aL) (MomentumSpectra.cpp:
+ * 1288-1368): states[4 i ..] = chain state after cell i, iters[i] = Newton iterations (-1: u.dsigma <= 0, not in the
+ * chain); state is updated to the last cell's; returns the total iterations. */
+long orc_famod_chain(const orc_params *p, const orc_setup *s, const orc_surface *surf, const long *cells,
+                     long ncells, double *state, double *states, int *iters);
 
 #ifdef __cplusplus
 }

@@ -77,6 +77,9 @@ def load():
                                         C.c_double, PD, PD, C.c_char_p, C.c_int]
         lib.orc_aniso_solve.argtypes = [C.POINTER(OrcSetup), C.c_double, C.c_double, C.c_double, C.c_double,
                                         C.c_double, C.c_double, PD]
+        lib.orc_famod_chain.restype = C.c_long
+        lib.orc_famod_chain.argtypes = [C.POINTER(OrcParams), C.POINTER(OrcSetup), C.POINTER(OrcSurface),
+                                        C.POINTER(C.c_long), C.c_long, PD, PD, C.POINTER(C.c_int)]
         _lib = lib
     return _lib
 
@@ -148,6 +151,26 @@ def spectra(spec, surf, T_avg=None, threads=1, omp_threads=0, return_stats=False
     if return_stats:
         return out, list(stats)
     return out
+
+
+class FamodChain:
+    """The PTMA warm-start chain step of the oracle (orc_famod_chain, MomentumSpectra.cpp:1288-1368) over explicit
+    cell lists of one surface: walk(cells, state) solves the cells in order from state = (prev_ok, lambda, aT, aL)
+    and returns (states after each cell [n][4], Newton iterations per cell (-1: not in the chain), end state)."""
+
+    def __init__(self, spec, surf, T_avg=None):
+        self.lib = load()
+        self.inp = _Inputs(spec, surf, T_avg, 1)
+
+    def walk(self, cells, state):
+        cells = np.ascontiguousarray(cells, dtype=np.int64)
+        st = np.array(state, dtype=np.float64)
+        states = np.zeros((len(cells), 4))
+        iters = np.zeros(len(cells), dtype=np.int32)
+        self.lib.orc_famod_chain(C.byref(self.inp.params), C.byref(self.inp.setup), C.byref(self.inp.surf),
+                                 cells.ctypes.data_as(C.POINTER(C.c_long)), len(cells), _p(st), _p(states),
+                                 iters.ctypes.data_as(C.POINTER(C.c_int)))
+        return states, iters, st
 
 
 def df_coefficients(spec, T, muB, E, P, bulkPi, T_avg=0.0):

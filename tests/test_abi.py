@@ -24,7 +24,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version():
     lib = _lib.load()
-    assert lib.is3d_abi_version() == 4
+    assert lib.is3d_abi_version() == 5
 
 
 def test_build_id_names_the_sources():

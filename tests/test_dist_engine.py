@@ -88,3 +88,81 @@ def test_facade_multi_device_path_on_one_gpu(tmp_path, mode):
     three = host.run_particlization_devices(d, n_out, [0, 0, 0])
     assert parity(two, one)[0] < 1e-12
     assert parity(three, one)[0] < 1e-12
+
+
+def _chain_surface():
+    from is3d2_amd import synth
+    s = synth.as_read(synth.surface(1200, seed=109, dimension=3, full3d=True))
+    s["bulkPi"] = s["bulkPi"].copy()
+    s["bulkPi"][::2] *= 10.0
+    s["dat"] = s["dat"].copy()
+    s["dat"][300:380] *= -20.0
+    return s
+
+
+def _chain_spec(chains):
+    from is3d2_amd import make_spec
+    return make_spec(hrg_eos=2, chosen="pikp", df_mode=5, dimension=3, famod_chains=chains)
+
+
+def _chain_worker(rank, world, port, chains, npass, q):
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    if npass:
+        os.environ["IS3D_CHAIN_PASSES"] = str(npass)
+    import torch
+    import torch.distributed as dist
+    from is3d2_amd import build_engine, dist as D
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        s = _chain_surface()
+        q0, q1 = D.chain_bounds(s, rank, world, chains)
+        e = build_engine(_chain_spec(chains), s, device=0)
+        e.set_chain_range(q0, q1)
+        out = torch.zeros(e.output_size(), dtype=torch.float64, device="cuda:0")
+        stream = torch.cuda.current_stream(0)
+        for _ in range(2):        # a second pass: the engine's chain buffers are reused
+            D.launch_chained(e, out.data_ptr(), stream.cuda_stream, rank, world, dist, sync=stream.synchronize)
+            e.finish()
+        st = e.stats()
+        e.close()
+        part = out.cpu()
+        dist.all_reduce(part)
+        q.put((rank, st["iterations"], st["cells"], part.numpy() if rank == 0 else None))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,chains,npass", [(2, 1, 0), (3, 3, 0), (2, 16, 1), (4, 1, 2)])
+def test_ptma_chains_split_over_processes(world, chains, npass):
+    """PTMA warm-start chains split over processes: every rank holds the whole surface, solves
+    its chain positions (Engine.set_chain_range) through the staged launch and hands its boundary states to the
+    next rank after every pass (dist.launch_chained, here over gloo with host staging; bench.py runs it over RCCL).
+    The per-rank Newton iteration counts add up to the oracle's serial-chain count, every cell is integrated once,
+    and the all-reduced spectra equal one engine's (summation order only)."""
+    import torch.multiprocessing as mp
+    from helpers import parity
+    from is3d2_amd import build_engine
+    from oracle import oracle as O
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29700 + (os.getpid() + 13 * world + chains + 7 * npass) % 1000
+    procs = [ctx.Process(target=_chain_worker, args=(r, world, port, chains, npass, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=240) for _ in range(world)], key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    s = _chain_surface()
+    spec = _chain_spec(chains)
+    _, rst = O.spectra(spec, s, threads=chains, return_stats=True)
+    assert sum(r[1] for r in res) == rst[3]
+    assert sum(r[2] for r in res) == len(s["tau"])
+    e = build_engine(spec, s, device=0)
+    one = e.calculate_spectra()
+    e.close()
+    got = res[0][3]
+    assert np.array_equal(np.isnan(got), np.isnan(one))
+    assert parity(np.nan_to_num(got), np.nan_to_num(one))[0] < 1e-12

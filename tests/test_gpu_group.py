@@ -67,12 +67,14 @@ def test_group_ptma_chain_walks_whole_surface(monkeypatch, dist):
 
 
 @pytest.mark.parametrize("chains,ndev,passes", [(1, 3, None), (3, 2, None), (1, 5, None), (16, 3, None),
-                                                 (1, 4, "1"), (3, 3, "2")])
+                                                 (1, 4, "1"), (3, 3, "2"), (32, 3, None), (48, 2, None)])
 def test_group_ptma_distributed_chains(monkeypatch, chains, ndev, passes):
     """Chains split over the shards on a breakdown-heavy surface (failed solves reset the state, p_L < 0 cells pass
     it through) with u.dsigma <= 0 runs: the iteration / failure counts equal one device's, which equal the
     oracle's serial chains.  IS3D_CHAIN_PASSES = 1 or 2 leaves most of the ripple to the finishers, which hand the
-    final boundary states from shard to shard."""
+    final boundary states from shard to shard.  (32, 3) and (48, 2) give every shard 25 positions per chain, one
+    segment each: the first shard is exact after pass 0 and its later passes return at once (both
+    parity slots of its boundary must still hold its end states)."""
     if passes:
         monkeypatch.setenv("IS3D_CHAIN_PASSES", passes)
     s = synth.as_read(synth.surface(2400, seed=109, dimension=3, full3d=True))

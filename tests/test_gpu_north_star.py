@@ -1,0 +1,170 @@
+"""GPU tier: the code path the north_star number is timed on (BASELINE config 4: 10^6 3+1D cells, SMASH 444 species,
+48 pT x 32 phi x 21 y, RTA-CE).  Its F_TS scalar tables (61 GB of rows at that size) are written and integrated
+chunk by chunk, the chunks alternating between the launch stream and a side stream with a table buffer each
+(engine.hip enqueue_spectra; reference loop MomentumSpectra.cpp:250-365).  is3d_set_tuning makes the chunk size a
+run-time knob, so a ~200-cell surface on the same grid runs the same multi-chunk schedule (>= 3 chunks: both table
+buffers are reused and the side stream forks and joins) against the oracle and against the one-chunk launch; a
+10^6-cell test checks the default schedule at full size through size-independent properties.
+
+Also here: the launch is asynchronous (no host round trip inside is3d_launch: the F_TS / F_TB choice for surfaces
+with lanes off the fast path is made on the device), for one engine and for a device group."""
+import time
+
+import numpy as np
+import pytest
+
+from helpers import parity, rel_quantile
+from is3d2_amd import build_engine, make_spec, synth
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-8
+P99 = 1e-11
+
+
+def config4_spec(mode):
+    return make_spec(hrg_eos=2, chosen="smash", df_mode=mode, dimension=3, pT="pT48", phi="phi32", y="y21")
+
+
+def run(spec, s, tuning=None, T_avg=None):
+    e = build_engine(spec, s, T_avg=T_avg)
+    for k, v in (tuning or {}).items():
+        e.set_tuning(k, v)
+    out = e.calculate_spectra()
+    chunks = e.get_tuning("phitab_chunks")
+    e.close()
+    return out, chunks
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("chunk_bytes", [1, 3 << 20])
+def test_chunked_scalar_tables_match_oracle_and_one_chunk(mode, chunk_bytes):
+    """The config-4 shape on 200 cells with the F_TS tables forced into chunks of one cell split (chunk_bytes = 1)
+    or of a few splits: >= 3 chunks, results bit-identical to the one-chunk launch (every chunk writes its own
+    splits' slabs; the chunking changes no summation order) and within the parity bars of the oracle."""
+    s = synth.as_read(synth.surface(200, seed=41, dimension=3, full3d=True))
+    spec = config4_spec(mode)
+    one, n1 = run(spec, s)
+    many, nk = run(spec, s, {"phitab_one_bytes": 0, "phitab_chunk_bytes": chunk_bytes})
+    assert n1 == 1, n1
+    assert nk >= 3, nk
+    assert np.array_equal(many, one)
+    ref = O.spectra(spec, s, threads=8)
+    rel, zr, zg = parity(many, ref)
+    assert rel < TOL, (rel, zr, zg)
+    assert rel_quantile(many, ref) < P99
+    assert zr == zg
+
+
+def test_chunked_scalar_tables_with_baryon_rows():
+    """F_BY rows (include_baryon: the T3 operand) through the chunked schedule: same as one chunk, oracle parity."""
+    s = synth.as_read(synth.surface(120, seed=43, dimension=3, baryon=True, full3d=True))
+    spec = make_spec(hrg_eos=2, chosen="smash", df_mode=2, dimension=3, pT="pT48", phi="phi32", y="y21",
+                     include_baryon=1, include_baryondiff_deltaf=1)
+    one, n1 = run(spec, s)
+    many, nk = run(spec, s, {"phitab_one_bytes": 0, "phitab_chunk_bytes": 1})
+    assert n1 == 1 and nk >= 3, (n1, nk)
+    assert np.array_equal(many, one)
+    ref = O.spectra(spec, s, threads=8)
+    assert parity(many, ref)[0] < TOL
+    assert rel_quantile(many, ref) < P99
+
+
+def test_tuning_keys():
+    s = synth.as_read(synth.surface(16, seed=1, dimension=3))
+    e = build_engine(config4_spec(2), s)
+    assert e.get_tuning("phitab_one_bytes") == 8 << 30
+    assert e.get_tuning("phitab_chunk_bytes") == 2 << 30
+    e.set_tuning("phitab_chunk_bytes", 12345)
+    assert e.get_tuning("phitab_chunk_bytes") == 12345
+    e.set_tuning("phitab_chunk_bytes", -1)
+    assert e.get_tuning("phitab_chunk_bytes") == 2 << 30
+    assert e.get_tuning("no_such_key") == -1
+    with pytest.raises(Exception, match="unknown key"):
+        e.set_tuning("no_such_key", 1)
+    e.close()
+
+
+def test_north_star_full_size_chunked_properties():
+    """BASELINE config 4 at full size (10^6 cells, RTA-CE) on the default schedule -- the F_TS tables of the whole
+    surface exceed 8 GiB, so they run in 2 GiB chunks over two streams (the timed path of the north_star number),
+    where the oracle would take a day: the spectrum is additive over a cell split (to summation-order rounding)
+    and p.dsigma enters linearly, so doubling dsigma_mu doubles every normal-range entry bit for bit."""
+    s = synth.as_read(synth.surface(1000000, seed=7, dimension=3, full3d=True))
+    spec = config4_spec(2)
+    e = build_engine(spec, s)
+    full = e.calculate_spectra()
+    nchunk = e.get_tuning("phitab_chunks")
+    n = len(s["tau"])
+    h = n // 2 + 4321
+    e.set_surface({k: np.ascontiguousarray(v[:h]) for k, v in s.items()})
+    a = e.calculate_spectra()
+    e.set_surface({k: np.ascontiguousarray(v[h:]) for k, v in s.items()})
+    b = e.calculate_spectra()
+    s2 = dict(s)
+    for k in ("dat", "dax", "day", "dan"):
+        s2[k] = 2.0 * s[k]
+    e.set_surface(s2)
+    d = e.calculate_spectra()
+    e.close()
+    assert nchunk >= 3, nchunk
+    assert np.isfinite(full).all() and (full != 0).sum() > 0.5 * full.size
+    m = np.abs(full) > 1e-290
+    assert float((np.abs((a + b)[m] - full[m]) / np.abs(full[m])).max()) < TOL
+    assert np.array_equal(d[m], 2.0 * full[m])
+    assert np.abs(d[~m] - 2.0 * full[~m]).max(initial=0.0) <= 1e-300
+
+
+def _busy_stream(torch, seconds=1.0):
+    """Queue a spin kernel of ~seconds on torch's current stream (torch.cuda._sleep counts GPU clock cycles)."""
+    torch.cuda._sleep(int(seconds * 2.0e9))
+
+
+@pytest.mark.parametrize("mode", [1, 2, 5])
+def test_launch_is_asynchronous(mode):
+    """is3d_launch enqueues the whole pass and returns while a long kernel queued ahead of it on the same stream is
+    still running: no host synchronisation inside the launch (round 4 read k_prep's slow-cell count back to the
+    host in every Grad / RTA-CE pass).  Then the result equals a plain calculate_spectra."""
+    torch = pytest.importorskip("torch")
+    s = synth.as_read(synth.surface(400, seed=47, dimension=3, full3d=True))
+    spec = make_spec(hrg_eos=2, chosen="smash", df_mode=mode, dimension=3, pT="pT24", phi="phi32", y="y21",
+                     famod_chains=1)
+    e = build_engine(spec, s)
+    ref = e.calculate_spectra()
+    out = torch.zeros(e.output_size(), dtype=torch.float64, device="cuda:0")
+    stream = torch.cuda.current_stream(0)
+    torch.cuda.synchronize()
+    _busy_stream(torch)
+    t0 = time.perf_counter()
+    e.launch(out.data_ptr(), stream.cuda_stream)
+    dt = time.perf_counter() - t0
+    still_busy = not stream.query()
+    e.finish()
+    got = out.cpu().numpy()
+    e.close()
+    assert still_busy, "the stream drained before is3d_launch returned (host sync inside the launch?)"
+    assert dt < 0.5, dt
+    assert np.array_equal(got, ref)
+
+
+def test_group_launch_is_asynchronous():
+    """A device group enqueues every shard without waiting for any of them (two shards on GPU 0 here)."""
+    torch = pytest.importorskip("torch")
+    s = synth.as_read(synth.surface(400, seed=53, dimension=3, full3d=True))
+    spec = make_spec(hrg_eos=2, chosen="smash", df_mode=2, dimension=3, pT="pT24", phi="phi32", y="y21")
+    e1 = build_engine(spec, s)
+    ref = e1.calculate_spectra()
+    e1.close()
+    e = build_engine(spec, s, devices=[0, 0])
+    out = torch.zeros(e.output_size(), dtype=torch.float64, device="cuda:0")
+    stream = torch.cuda.current_stream(0)
+    torch.cuda.synchronize()
+    _busy_stream(torch)
+    e.launch(out.data_ptr(), stream.cuda_stream)
+    still_busy = not stream.query()
+    e.finish()
+    got = out.cpu().numpy()
+    e.close()
+    assert still_busy
+    # two shard sums + their sum: near-cancelling SMASH entries move by rounding (test_gpu_group.py: 6.5e-12)
+    assert parity(got, ref)[0] < 1e-10
