@@ -8,13 +8,17 @@
 #   pmcK  : scalar-cache requests / misses (the F_TS launches read their per-(cell, phi) operands by scalar loads)
 # Every pass is its own process under its own time limit; the script stops at the first failure.
 # usage: tools/profile_modes.sh <tag> <config> "<modes>" [bench args...]
+# output: gpurun_out/prof_<tag>_<config>[_op0]_m<mode>/ (operation 0 runs get their own directory: the same tag and
+# mode for both operations used to overwrite operation 1's raw CSVs)
 set -e
 TAG=$1; CFG=$2; MODES=$3; shift 3
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd /tmp && export TMPDIR=/tmp
 PY=$(command -v python3)
+OPN=""
+case " $* " in *" --operation 0 "*) OPN="_op0" ;; esac
 for M in $MODES; do
-  OUT=$R/gpurun_out/prof_${TAG}_${CFG}_m$M
+  OUT=$R/gpurun_out/prof_${TAG}_${CFG}${OPN}_m$M
   mkdir -p "$OUT"
   B="$R/bench.py --no-cpu-baseline --no-per-species --north-star-steps 0 --config $CFG --df-mode $M --steps 2 --warmup 1 $*"
   timeout -s KILL 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- "$PY" $B > "$OUT/trace.log" 2>&1

@@ -87,7 +87,11 @@ def main():
             cyc = e["GRBM_GUI_ACTIVE"] / 8.0
             e["clock_ghz"] = cyc / e["avg_ns_pmc_pass"]
             e["valu_issue_frac"] = 4.0 * e["SQ_ACTIVE_INST_VALU"] / (1024.0 * cyc)
+    # the raw per-kernel summary names the library it was taken on, so bench.py's roofline can be recomputed from it
+    out["_meta"] = {"build_id": bid, "tag": tag, "config": config, "df_mode": mode,
+                    "note": "per-kernel averages over the launches of each rocprofv3 --pmc pass (one process per pass)"}
     json.dump(out, open(os.path.join(prof, "%s_pmc.json" % tag), "w"), indent=1, sort_keys=True)
+    meta = out.pop("_meta")
     # the dominant k_spectra kernel (the modified modes also run the short F_FB fallback launch); an F_TS launch
     # over a surface whose tables exceed one chunk runs it several times per pass (engine.hip): per-pass totals =
     # per-launch averages x launches per pass, passes = the reduction launches (one per pass)
@@ -133,6 +137,7 @@ def main():
         json.dump(v, open(vp, "w"), indent=1, sort_keys=True)
     for k, e in sorted(out.items()):
         print(k, {c: round(v, 3) for c, v in e.items()})
+    print("_meta", meta)
 
 
 if __name__ == "__main__":
