@@ -2191,6 +2191,20 @@ extern "C" int is3d_calculate_dN_dX(is3d_engine* e, double* dN_taudtaudy, double
       default: launch_dndx<PTB>(dim3((unsigned)nwg), shmem, st, da, kflags, KJ); break;
     }
     HIPCHK(e, hipGetLastError());
+    if (mode >= PTM) {
+      // the separable-fallback lanes of the cells k_fbscan lists (breakdown, narrow rapidity windows) in their own
+      // launch (kernels.h k_dndx F_FB), added to ycell; the list's length stays on the device, so the grid is sized
+      // for the whole surface and the workgroups split whatever the list holds
+      if (!ensure(e->d_fb, e->fb_cap, n + 1)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(fallback list) failed");
+      hipLaunchKernelGGL(k_fbscan, dim3(1), dim3(1024), 0, st, (const double*)e->d_rec, n, e->d_fb + 1, e->d_fb);
+      DndxArgs fa = da;
+      fa.fbcells = e->d_fb + 1; fa.fbcount = e->d_fb;
+      fa.nchunk = std::max(1L, std::min(da.nchunk, (4096L + da.nbx - 1) / da.nbx));
+      const long nfw = (long)da.nbx * fa.nchunk;
+      if (mode == PTM) launch_dndx<PTM>(dim3((unsigned)nfw), shmem, st, fa, kflags | F_FB, KJ);
+      else launch_dndx<PTB>(dim3((unsigned)nfw), shmem, st, fa, kflags | F_FB, KJ);
+      HIPCHK(e, hipGetLastError());
+    }
     e->ycell_n = n;
   } else {
     e->ycell_n = 0;

@@ -63,6 +63,15 @@ constexpr int spectra_waves_f() {
 // the separable fallback inline)
 template <int MODE>
 constexpr int dndx_waves() { return (MODE == CE || MODE >= PTM) ? 2 : spectra_waves<MODE>(); }
+#ifndef IS3D_DNDX_WAVES_MOD
+#define IS3D_DNDX_WAVES_MOD 2      // k_dndx's modified-lane launch (the separable fallback in its own F_FB launch)
+#endif
+#ifndef IS3D_DNDX_MOD_UNROLL
+#define IS3D_DNDX_MOD_UNROLL 2     // k_dndx modified lanes: phi pairs per loop trip (fully unrolled, 16 at 32 points, the
+                                   // PTM / PTB launch held 256 VGPRs + 95 spilled; two: 129 VGPRs, 3 waves per SIMD)
+#endif
+template <int MODE, int FLAGS>
+constexpr int dndx_waves_f() { return (MODE >= PTM && !(FLAGS & 32)) ? IS3D_DNDX_WAVES_MOD : dndx_waves<MODE>(); }
 
 // LDS row stride of the y-terms (doubles): NYT | 1 is odd, so the 8-byte stores of one y-term field
 // by consecutive lanes (rows 152 B apart) spread over the 64 banks instead of hitting two of them
@@ -248,6 +257,8 @@ struct DndxArgs {
                               // (y x phi block x eta node), species groups
   long cells_per_wg, nchunk;
   int dim;
+  const int* fbcells;         // F_FB launch (modified modes): ascending indices of the cells with separable-fallback
+  const int* fbcount;         //   lanes (k_fbscan) and their number; the launch adds those lanes' sums to ycell
 };
 
 // k_phitab: the F_TS tables of one chunk of cells (every pT), rows [pT][cell - c0][phitab_row]
@@ -1112,7 +1123,7 @@ __device__ __forceinline__ double mod_phi_wsum(const ModLane& M, const dbl2* CS,
   constexpr bool OUT = (FLAGS & F_OUT) != 0;
   double a0 = 0.0, a1 = 0.0;
   dbl2 c0 = CS[0], c1 = CS[1], q = QV[0];
-#pragma unroll
+#pragma unroll IS3D_DNDX_MOD_UNROLL
   for (int jj = 0; jj < KJ; jj += 2) {
     dbl2 n0 = c0, n1 = c1, nq = q;
     if (jj + 2 < KJ) { n0 = CS[jj + 2]; n1 = CS[jj + 3]; nq = QV[(jj >> 1) + 1]; }
@@ -1133,8 +1144,14 @@ __device__ __forceinline__ double mod_phi_wsum(const ModLane& M, const dbl2* CS,
 // k_spectra.  The momentum loop (pT) is inside: per (cell tile, pT) the {b', Phi} phi-terms are rebuilt
 // in LDS and every lane adds w_pT x sum_phi w_phi (point) into its column of s_red; after the pT loop a
 // species' slot columns are summed in slot order.  No atomics: bit-reproducible.
+// Modified modes (PTM / PTB) run two launches, as k_spectra does: the main one integrates the modified lanes only
+// and writes ycell, the F_FB one integrates the separable-fallback lanes (breakdown cells, narrow rapidity windows:
+// MomentumSpectra.cpp:863-929) of the cells k_fbscan lists and adds them to ycell.  With both in one kernel the
+// PTM / PTB instances spilled 147 VGPRs at 2 waves per SIMD (5.6e11 B of scratch traffic per config-2 pass).
 template <int MODE, int FLAGS, int KJ>
-__global__ __launch_bounds__(kBlock, dndx_waves<MODE>()) void k_dndx(DndxArgs A) {
+__global__ __launch_bounds__(kBlock, (dndx_waves_f<MODE, FLAGS>())) void k_dndx(DndxArgs A) {
+  constexpr bool FB = MODE >= PTM && (FLAGS & F_FB) != 0;   // separable-fallback launch of a modified mode
+  constexpr bool MODMAIN = MODE >= PTM && !FB;              // modified launch: separable lanes left to F_FB
   extern __shared__ double smem[];
   const int nphp = A.njb * KJ;
   double* s_rec = smem;                                   // [kTile][NREC]
@@ -1178,17 +1195,26 @@ __global__ __launch_bounds__(kBlock, dndx_waves<MODE>()) void k_dndx(DndxArgs A)
     s_grid[A.nk + A.nl + i] = (A.dim == 3) ? 1.0 : A.etaw[i];
   }
 
-  const long c_begin = ch * A.cells_per_wg;
-  const long c_end = min(A.n, c_begin + A.cells_per_wg);
+  // F_FB: positions in the fallback cell list (its length is known on the device only), split evenly
+  long c_begin, c_end;
+  if constexpr (FB) {
+    const long nfb = *A.fbcount, cpw = ((nfb + A.nchunk - 1) / A.nchunk + kTile - 1) / kTile * kTile;
+    c_begin = ch * cpw;
+    c_end = min(nfb, c_begin + cpw);
+  } else {
+    c_begin = ch * A.cells_per_wg;
+    c_end = min(A.n, c_begin + A.cells_per_wg);
+  }
+  auto cell_of = [&](long pos) -> long { return FB ? (long)A.fbcells[pos] : pos; };
   for (long cb = c_begin; cb < c_end; cb += kTile) {
     const int nt = (int)min((long)kTile, c_end - cb);
     __syncthreads();                                       // previous tile fully consumed
-    for (int i = tid; i < nt * NREC; i += kBlock) s_rec[i] = A.rec[cb * NREC + i];
+    for (int i = tid; i < nt * NREC; i += kBlock) s_rec[i] = A.rec[cell_of(cb + i / NREC) * NREC + i % NREC];
 #pragma unroll
     for (int t = 0; t < kTile; t++) s_red[t * kBlock + tid] = 0.0;
     if (MODE == PTM && active) {
       const int rc = A.rcls[s];
-      for (int t = 0; t < nt; t++) s_rn[t * kBlock + tid] = A.renorm[(cb + t) * A.nrcls + rc];
+      for (int t = 0; t < nt; t++) s_rn[t * kBlock + tid] = A.renorm[cell_of(cb + t) * A.nrcls + rc];
     }
     __syncthreads();
     for (int idx = tid; idx < nt * A.nq; idx += kBlock) {
@@ -1247,7 +1273,9 @@ __global__ __launch_bounds__(kBlock, dndx_waves<MODE>()) void k_dndx(DndxArgs A)
           const dbl2* BP = s_bp + t * nphp + j0;
           const dbl2* W = (const dbl2*)(s_w + j0);
           const bool sep = (MODE <= CE) || kind == 1.0 || Y[Y_NARROW] != 0.0;
-          if (sep) {
+          if (MODMAIN && sep) continue;
+          if (FB && !sep) continue;
+          if constexpr (!MODMAIN) {
             SepLane L;
             // Boltzmann-tail lanes of Grad / RTA-CE (decided per wavefront, as in k_spectra)
             // (Grad only: RTA-CE's tail pairs, one 1/E per pair, were slower -- 508 -> 560 ms at config 2 against
@@ -1258,7 +1286,8 @@ __global__ __launch_bounds__(kBlock, dndx_waves<MODE>()) void k_dndx(DndxArgs A)
             if (TL && L.tail) cell += sep_phi_wsum_tail<MODE, FLAGS, KJ>(L, s_cs + j0, BP, W);
             else cell += L.fast ? sep_phi_wsum<MODE, FLAGS, true, KJ>(L, s_cs + j0, BP, W)
                                 : sep_phi_wsum<MODE, FLAGS, false, KJ>(L, s_cs + j0, BP, W);
-          } else if (MODE >= PTM) {
+          }
+          if constexpr (MODMAIN) {
             ModLane M;
             mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, s_etab, M, false);
             if (M.skip) continue;
@@ -1279,7 +1308,8 @@ __global__ __launch_bounds__(kBlock, dndx_waves<MODE>()) void k_dndx(DndxArgs A)
       double acc = 0.0;
       for (int w = 0; w < 4; w++)
         for (int yl = 0; yl < A.Yl; yl++) acc += s_red[t * kBlock + w * 64 + yl * A.Sl + sl];
-      A.ycell[(long)s2 * A.n + cb + t] = acc;
+      double* y = A.ycell + (long)s2 * A.n + cell_of(cb + t);
+      *y = FB ? *y + acc : acc;          // F_FB runs after the main launch on the same stream
     }
   }
 }
@@ -1427,7 +1457,18 @@ void launch_spectra(dim3 grid, size_t shmem, hipStream_t st, const SpecArgs& a, 
 
 template <int MODE, int KJ>
 void launch_dndx_kj(dim3 grid, size_t shmem, hipStream_t st, const DndxArgs& a, int flags) {
-  switch (flags) {
+  if constexpr (MODE >= PTM) {
+    if (flags & F_FB) {
+      switch (flags & 3) {
+        case 0: hipLaunchKernelGGL((k_dndx<MODE, 32, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+        case 1: hipLaunchKernelGGL((k_dndx<MODE, 33, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+        case 2: hipLaunchKernelGGL((k_dndx<MODE, 34, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+        default: hipLaunchKernelGGL((k_dndx<MODE, 35, KJ>), grid, dim3(kBlock), shmem, st, a); break;
+      }
+      return;
+    }
+  }
+  switch (flags & 3) {
     case 0: hipLaunchKernelGGL((k_dndx<MODE, 0, KJ>), grid, dim3(kBlock), shmem, st, a); break;
     case 1: hipLaunchKernelGGL((k_dndx<MODE, 1, KJ>), grid, dim3(kBlock), shmem, st, a); break;
     case 2: hipLaunchKernelGGL((k_dndx<MODE, 2, KJ>), grid, dim3(kBlock), shmem, st, a); break;
