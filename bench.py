@@ -241,6 +241,9 @@ def run_workload(args, cfg_name, mode, steps, warmup, rank, world, local_rank, d
     T_avg = D.global_averages(D.average_sums(mine, flags.get("include_baryon", 0)), reduce)[0]
 
     eng = build_engine(spec, surf, T_avg=T_avg, device=local_rank, species_classes=classes)
+    for kv in args.tune or []:      # is3d_set_tuning knobs (A/B experiments; the driver's runs use the defaults)
+        k, v = kv.split("=", 1)
+        eng.set_tuning(k, int(float(v)))
     n_integrated = eng.species_integrated()
     if qrange is not None:
         eng.set_chain_range(*qrange)
@@ -277,6 +280,7 @@ def run_workload(args, cfg_name, mode, steps, warmup, rank, world, local_rank, d
 
     for _ in range(warmup):
         step()
+    nsplit = eng.get_tuning("splits")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -311,6 +315,7 @@ def run_workload(args, cfg_name, mode, steps, warmup, rank, world, local_rank, d
         "cells_per_gpu": n_local, "species": nsp, "grid": [npT, nphi, ny, neta], "df_mode": mode,
         "species_integrated": n_integrated,
         "famod_chains": spec["params"]["famod_chains"] if mode == 5 else None,
+        "cell_splits": nsplit if operation == 1 else None,
         "parallelism": ("dp%d (cell shards + RCCL all-reduce of spectra%s)"
                         % (world, "; PTMA chain positions split, boundary states sent rank to rank per pass" if chained else "")
                         if world > 1 else "1 GPU"),
@@ -334,6 +339,8 @@ def main():
     ap.add_argument("--no-per-species", action="store_true",
                     help="skip the second timing of the main workload with one integral per species (classes off)")
     ap.add_argument("--cpu-seconds", type=float, default=25.0)
+    ap.add_argument("--tune", action="append", metavar="KEY=VALUE",
+                    help="engine tuning knob (is3d_set_tuning), e.g. max_splits=128; repeatable")
     ap.add_argument("--north-star-steps", type=int, default=3,
                     help="timed passes of the north_star workload (config4: 10^6 3+1D cells, SMASH, RTA-CE, "
                          "sharded over the ranks) reported beside the main line; 0 skips it")

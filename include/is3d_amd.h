@@ -131,8 +131,13 @@ int is3d_set_params(is3d_engine *e, const is3d_params *p);
  *                         written and integrated in one chunk (default 8 GiB)
  *   "phitab_chunk_bytes"  larger ones in chunks of whole cell splits of about this size, alternating over two streams
  *                         (default 2 GiB; BASELINE config 4 runs 29 chunks)
+ *   "max_splits"          cap on k_spectra's cell splits, one output-sized partial slab each (default 1024)
+ *   "slab_bytes"          cap on those slabs' memory (default 48 GiB; also at most half the device's free memory)
+ *   "split_bytes"         record bytes per cell split the plan aims for (default 512 KiB: a split stays in an XCD's L2)
  * A negative value restores the default.  is3d_get_tuning also reads "phitab_chunks": the F_TS chunks of the last
- * launch (0: not an F_TS launch); -1 = unknown key. */
+ * launch (0: not an F_TS launch), "splits": the cell splits of the last launch, and "slabs": the output-sized partial
+ * slabs it held (several 3+1D F_TS chunks fold theirs into one accumulator as they finish: 1 + 2 x splits per chunk);
+ * -1 = unknown key. */
 int is3d_set_tuning(is3d_engine *e, const char *key, long value);
 long is3d_get_tuning(const is3d_engine *e, const char *key);
 int is3d_set_species(is3d_engine *e, int n, const double *mass, const double *sign,

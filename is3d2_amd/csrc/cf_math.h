@@ -1761,6 +1761,12 @@ IS3D_HD double sqrt_nr(double v) {
 #ifndef IS3D_MOD_TAIL
 #define IS3D_MOD_TAIL 1
 #endif
+#ifndef IS3D_MOD_WIDE_TAIL
+#define IS3D_MOD_WIDE_TAIL 1
+#endif
+#ifndef IS3D_MOD_EXACT
+#define IS3D_MOD_EXACT 1
+#endif
 #ifndef IS3D_MOD_EXP_DEG
 #define IS3D_MOD_EXP_DEG 3
 #endif
@@ -1818,8 +1824,14 @@ IS3D_HD bool mod_skips(const double* R, const double* Y, double mT, double m2, d
   return thr < 0.0 || (lo > 0.0 && (m2s + lo * lo) * (1.0 - 2e-12) > thr * thr);
 }
 
+// KJX > 0 (k_spectra's table lanes; -1: nx points, the host emulator): MW / MT are the lane's {PDm, Qv} and T2 rows of KJX points.  A lane whose bounds
+// span more than 250 binades (wide) takes its exact smallest / largest X over those points instead (IS3D_MOD_EXACT): the
+// bounds |mT U| -+ pT |V|max are loose where pT |V| is large, and a lane found wide by them went to the clamped en form
+// (1.6x the normal fours' instructions) although its points spanned a median 134 binades (config 2 PTM, host census)
+template <int KJX = 0>
 IS3D_HD void mod_setup(const double* R, const double* Y, double mT, double m2, double pT, double sign, double baryon,
-                       double renorm_abs, const double* etab, ModLane& L, bool ymu = true, bool allow_tail = false) {
+                       double renorm_abs, const double* etab, ModLane& L, bool ymu = true, bool allow_tail = false,
+                       const dbl2* MW = nullptr, const double* MT = nullptr, int nx = KJX) {
   const double ux = Y[Y_MUX], uy = Y[Y_MUY], uz = Y[Y_MUZ];   // sig U
   const double u2 = ymu ? Y[Y_MU2] : fma(ux, ux, fma(uy, uy, uz * uz));
   const double sig = R[R_INVTM] * kInvLn2xN, m2s = m2 * (sig * sig);
@@ -1848,28 +1860,54 @@ IS3D_HD void mod_setup(const double* R, const double* Y, double mT, double m2, d
   const double emax = sqrt(m2s + hi * hi) * kLn2overN;
   L.clamp = (emax < kModTabX && fabs(L.chemm) < kModTabChem) ? 0 : 1;
 #endif
-  int k = 0;
+  int k = 0, wide = 0;
 #if IS3D_MOD_PLUS
   if (!L.clamp) {
     // k = floor(x_min / ln2) from the lane's smallest sig E_mod (a lower bound of it: rounding down only
-    // raises E by a factor < 2); the largest point must stay within 250 binades of 2^k
-    const double e2 = m2s + (lo > 0.0 ? lo * lo : 0.0);
+    // raises E by a factor < 2); the normal fours need the largest point within 250 binades of 2^k (wide: not)
+    double e2 = m2s + (lo > 0.0 ? lo * lo : 0.0), e2h = m2s + hi * hi;
+    auto scale = [&]() {
 #if defined(__HIP_DEVICE_COMPILE__)
-    const double emin = e2 * __builtin_amdgcn_rsq(e2);
+      const double emin = e2 * __builtin_amdgcn_rsq(e2);
 #else
-    const double emin = sqrt(e2);
+      const double emin = sqrt(e2);
 #endif
-    k = (int)(emin * ((1.0 - 1e-6) / kExpTabN));
-    const double xk = (k + 250.0) * kExpTabN;
-    if (!(m2s + hi * hi < xk * xk)) L.clamp = 1;
+      k = (int)(emin * ((1.0 - 1e-6) / kExpTabN));
+      const double xk = (k + 250.0) * kExpTabN;
+      wide = (e2h < xk * xk) ? 0 : 1;
+    };
+    scale();
+    if constexpr (KJX != 0) {   // KJX = -1: nx points (the host emulator)
+      if (IS3D_MOD_EXACT && MW) {
+        // the exact range of the lane's points (the loops' own X expression); a wave-uniform branch on the device
+#if defined(__HIP_DEVICE_COMPILE__)
+        int aw = __any(wide);
+        asm volatile("" : "+v"(aw));
+        if (aw) {
+#else
+        {
+#endif
+          if (wide) {
+            double mn = 1.0e300, mx = 0.0;
+#pragma unroll 8
+            for (int j = 0; j < (KJX > 0 ? KJX : nx); j++) {
+              const double X = fma(mT, MT[j], L.E0 + MW[j].y);
+              mn = fmin(mn, X); mx = fmax(mx, X);
+            }
+            e2 = mn; e2h = mx;
+            scale();
+          }
+        }
+      }
+    }
   }
 #endif
-  // e^chem of the table lanes (1 for mesons and without baryon chemistry: a wave-uniform skip there)
-  double ec = 1.0;
-  if (!L.clamp && L.chemm != 0.0) ec = exp_tab(exp_tab_coef(), etab, L.chemm * kInvLn2xN);
-  if (L.clamp) k = 0;
-  // only callers that evaluate tail lanes with mod_quad_tab_tail_t pass allow_tail
-  L.tail = (IS3D_MOD_PLUS && IS3D_MOD_TAIL && allow_tail && !L.clamp && L.chemm * 1.4426950408889634 < k - 55) ? 1 : 0;
+  // only callers that evaluate tail lanes with mod_quad_tab_tail_t pass allow_tail.  The tail form has no
+  // denominators (no product of four), so a wide lane is a tail lane too when its sign term is negligible
+  // (IS3D_MOD_WIDE_TAIL; before, every wide lane took the clamped en form: 5% of config 2's PTM wavefronts, at 1.6x the
+  // normal fours' instructions)
+  L.tail = (IS3D_MOD_PLUS && IS3D_MOD_TAIL && allow_tail && !L.clamp && (IS3D_MOD_WIDE_TAIL || !wide) &&
+            L.chemm * 1.4426950408889634 < k - 55) ? 1 : 0;
 #if defined(__HIP_DEVICE_COMPILE__)
   if (IS3D_MOD_TAIL && allow_tail) {   // one decision per wavefront, passed through a VGPR (see sep_setup)
     int t = __all(L.tail);
@@ -1877,6 +1915,11 @@ IS3D_HD void mod_setup(const double* R, const double* Y, double mT, double m2, d
     L.tail = t;
   }
 #endif
+  if (wide && !L.tail) L.clamp = 1;
+  // e^chem of the table lanes (1 for mesons and without baryon chemistry: a wave-uniform skip there)
+  double ec = 1.0;
+  if (!L.clamp && L.chemm != 0.0) ec = exp_tab(exp_tab_coef(), etab, L.chemm * kInvLn2xN);
+  if (L.clamp) k = 0;
   L.shiftk = 6755399441055744.0 + (L.tail ? 1.0 : -1.0) * ((double)k * kExpTabN);
   const double d = ldexp(renorm_abs * ec, -k);
   L.sign = ldexp(sign * ec, -k);
@@ -1889,6 +1932,16 @@ IS3D_HD void mod_setup(const double* R, const double* Y, double mT, double m2, d
 // num = en = e^(-E_mod/T_mod), q = 1 + s en.  X = (sig E_mod)^2: one Newton step of the v_rsq_f64 estimate y
 // folded into the exp argument, sig E_mod = g v with g = X y, v = 1.5 - 0.5 g y, and the range reduction folded
 // into the product (t = fma(g, v, shift) rounds g v to the integer K exactly, rs = fma(g, v, shift - t))
+// rsq estimate of the table lanes' X = (sig E_mod)^2 (v_rsq_f64, 16 cycles per wave on MI355X, tools/microbench.hip; v_rsq_f32
+// with the two conversions costs the same 16.5 and measured no faster, profiles/round5_r5a_ab_mod.log)
+IS3D_HD double mod_rsq(double X) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_rsq(X);
+#else
+  return 1.0 / sqrt(X);
+#endif
+}
+
 template <bool CLAMP>
 IS3D_HD void mod_nq_x(const ModLane& L, double X, double& num, double& q) {
   if (CLAMP) {
@@ -1896,11 +1949,7 @@ IS3D_HD void mod_nq_x(const ModLane& L, double X, double& num, double& q) {
     q = fma(L.sign, num, 1.0);
     return;
   }
-#if defined(__HIP_DEVICE_COMPILE__)
-  const double y = __builtin_amdgcn_rsq(X);
-#else
-  const double y = 1.0 / sqrt(X);
-#endif
+  const double y = mod_rsq(X);
   const double g = IS3D_MOD_PLUS ? X * y : -(X * y);
   const double v = fma(-0.5, X * y * y, 1.5);
   const double sh = IS3D_MOD_PLUS ? L.shiftk : kconst(6755399441055744.0);
@@ -2004,11 +2053,7 @@ IS3D_HD void mod_nq4(const ModLane& L, const double* X, double* num, double* q) 
   const double sh = IS3D_MOD_PLUS ? L.shiftk : kconst(6755399441055744.0);
 #pragma unroll
   for (int i = 0; i < 4; i++) {
-#if defined(__HIP_DEVICE_COMPILE__)
-    const double y = __builtin_amdgcn_rsq(X[i]);
-#else
-    const double y = 1.0 / sqrt(X[i]);
-#endif
+    const double y = mod_rsq(X[i]);
     const double g = (IS3D_MOD_PLUS && !TAIL) ? X[i] * y : -(X[i] * y);
     const double v = fma(-0.5, X[i] * y * y, 1.5);
     t[i] = fma(g, v, sh);

@@ -588,6 +588,17 @@ __global__ __launch_bounds__(256) void k_reduce_wave(ReduceArgs A) {
   write_members(A, s, ((long)ipt * A.nphi + j) * A.ny_out + k, acc, lane, 64);
 }
 
+// Chunk-wise slab fold (folded F_TS launches, enqueue_spectra): acc[i] = (init ? 0 : acc[i]) + src[0][i] + ... +
+// src[ns - 1][i], added in split order, so the folded accumulator equals k_reduce's sequential sum over all splits
+// bit for bit (3+1D: one term per split and output).  Memory-bound: ns + 2 doubles per entry.
+__global__ __launch_bounds__(256) void k_fold(double* acc, const double* src, long sstride, int ns, int init) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < sstride; i += (long)gridDim.x * blockDim.x) {
+    double a = init ? 0.0 : acc[i];
+    for (int z = 0; z < ns; z++) a += src[(long)z * sstride + i];
+    acc[i] = a;
+  }
+}
+
 // per-cell spacetime bin indices (SpacetimeDistribution.cpp:380-392): keys[0..2][c] = itau, ir, iphi (-1 outside)
 struct KeyArgs {
   const double *tau, *x, *y; long n;
@@ -857,10 +868,18 @@ struct is3d_engine {
   long phtab2_cap = 0;
   hipStream_t side = nullptr; // F_TS chunks alternate between the launch stream and this one
   hipEvent_t fork = nullptr, join = nullptr;
+  // folded F_TS chunks (IS3D_SLAB_FOLD): k_fold runs on its own stream, in chunk order, after each chunk's k_spectra
+  // (ev_spec); a chunk reusing a slab buffer waits for the fold that emptied it (ev_fold)
+  hipStream_t fold_st = nullptr;
+  hipEvent_t ev_spec[2] = {nullptr, nullptr}, ev_fold[2] = {nullptr, nullptr}, fold_join = nullptr;
   // is3d_set_tuning: F_TS table chunking (defaults IS3D_PHITAB_ONE / IS3D_PHITAB_BYTES): tables of the whole window
   // up to phitab_one bytes are one chunk, larger ones chunks of whole cell splits of about phitab_chunk bytes
   long phitab_one = IS3D_PHITAB_ONE, phitab_chunk = IS3D_PHITAB_BYTES;
   long last_nchunk = 0;       // F_TS chunks of the last launch (0: not an F_TS launch)
+  // is3d_set_tuning: k_spectra's cell splits (defaults IS3D_MAX_SPLITS / IS3D_SLAB_BYTES / IS3D_SPLIT_BYTES)
+  long max_splits = IS3D_MAX_SPLITS, slab_bytes = IS3D_SLAB_BYTES, split_bytes = IS3D_SPLIT_BYTES;
+  long last_nsplit = 0;       // cell splits of the last launch's main plan
+  long last_nslab = 0;        // ... and the output-sized partial slabs it held (folded F_TS chunks: 1 + 2 spc)
   // operation 0
   double *d_ycell = nullptr, *d_part = nullptr; long ycell_cap = 0, part_cap = 0;
   int *d_keys = nullptr, *d_perm = nullptr; long keys_cap = 0, perm_cap = 0;
@@ -923,6 +942,9 @@ extern "C" void is3d_destroy(is3d_engine* e) {
   dfree(e->d_rec); dfree(e->d_aux); dfree(e->d_sol); dfree(e->d_renorm); dfree(e->d_slab); dfree(e->d_out);
   dfree(e->d_fb); dfree(e->d_phtab); dfree(e->d_phtab2);
   if (e->side) (void)hipStreamDestroy(e->side);
+  if (e->fold_st) (void)hipStreamDestroy(e->fold_st);
+  for (auto v : {e->ev_spec[0], e->ev_spec[1], e->ev_fold[0], e->ev_fold[1], e->fold_join})
+    if (v) (void)hipEventDestroy(v);
   if (e->fork) (void)hipEventDestroy(e->fork);
   if (e->join) (void)hipEventDestroy(e->join);
   dfree(e->d_ycell); dfree(e->d_part); dfree(e->d_keys); dfree(e->d_perm); dfree(e->d_offs);
@@ -961,6 +983,9 @@ extern "C" int is3d_set_tuning(is3d_engine* e, const char* key, long value) {
   if (!e || !key) return IS3D_ERR_ARG;
   if (!std::strcmp(key, "phitab_one_bytes")) e->phitab_one = value < 0 ? (long)IS3D_PHITAB_ONE : value;
   else if (!std::strcmp(key, "phitab_chunk_bytes")) e->phitab_chunk = value <= 0 ? (long)IS3D_PHITAB_BYTES : value;
+  else if (!std::strcmp(key, "max_splits")) e->max_splits = value <= 0 ? (long)IS3D_MAX_SPLITS : value;
+  else if (!std::strcmp(key, "slab_bytes")) e->slab_bytes = value <= 0 ? (long)IS3D_SLAB_BYTES : value;
+  else if (!std::strcmp(key, "split_bytes")) e->split_bytes = value <= 0 ? (long)IS3D_SPLIT_BYTES : value;
   else return e->fail(IS3D_ERR_ARG, std::string("is3d_set_tuning: unknown key ") + key);
   return IS3D_OK;
 }
@@ -971,6 +996,11 @@ extern "C" long is3d_get_tuning(const is3d_engine* e, const char* key) {
   if (!std::strcmp(key, "phitab_one_bytes")) return e->phitab_one;
   if (!std::strcmp(key, "phitab_chunk_bytes")) return e->phitab_chunk;
   if (!std::strcmp(key, "phitab_chunks")) return e->last_nchunk;
+  if (!std::strcmp(key, "max_splits")) return e->max_splits;
+  if (!std::strcmp(key, "slab_bytes")) return e->slab_bytes;
+  if (!std::strcmp(key, "split_bytes")) return e->split_bytes;
+  if (!std::strcmp(key, "splits")) return e->last_nsplit;
+  if (!std::strcmp(key, "slabs")) return e->last_nslab;
   return -1;
 }
 
@@ -1479,7 +1509,9 @@ extern "C" int is3d_set_surface(is3d_engine* e, long n, const is3d_surface* s) {
                                  s->muB, s->nB, s->Vx, s->Vy, s->Vn};
   for (int f = 0; f < S_MUB; f++)
     if (!fields[f] && n > 0) return e->fail(IS3D_ERR_ARG, "surface field missing");
-  if (!e->surf_owned || e->surf_cap < n) {
+  // (reallocated when too small, or more than twice the size: a device group's cost prepass uploads the whole
+  // surface to shard 0 before its own window)
+  if (!e->surf_owned || e->surf_cap < n || e->surf_cap > 2 * n + 4096) {
     if (e->surf_owned) dfree(e->d_surf);
     e->d_surf = dalloc<double>((size_t)NSURF * std::max(n, 1L));
     if (!e->d_surf) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(surface) failed");
@@ -1514,7 +1546,9 @@ extern "C" int is3d_set_surface_device(is3d_engine* e, long n, const double* dev
 extern "C" int is3d_internal_copy_surface(is3d_engine* e, long n, const double* src, long src_n, int src_device, long lo) {
   if (!e || e->grp || n < 0 || lo < 0 || lo + n > src_n || (!src && n > 0)) return e ? e->fail(IS3D_ERR_ARG, "bad surface copy") : IS3D_ERR_ARG;
   HIPCHK(e, hipSetDevice(e->device));
-  if (!e->surf_owned || e->surf_cap < n) {
+  // (reallocated when too small, or more than twice the size: a device group's cost prepass uploads the whole
+  // surface to shard 0 before its own window)
+  if (!e->surf_owned || e->surf_cap < n || e->surf_cap > 2 * n + 4096) {
     if (e->surf_owned) dfree(e->d_surf);
     e->d_surf = dalloc<double>((size_t)NSURF * std::max(n, 1L));
     if (!e->d_surf) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(surface) failed");
@@ -1683,9 +1717,42 @@ static int chain_end(is3d_engine* e) {
 struct IntegralPlan {
   SpectraPlan P;
   long ntask = 0, bx = 0, wgs = 0, nsplit = 0, cps = 0, sstride = 0, nsplit_fb = 0;
+  // F_TS table chunks: spc splits per chunk, nchunk chunks; fold: each chunk's slabs are folded into one accumulator
+  // slab as soon as the chunk is integrated (3+1D, several chunks), so the slabs take 1 + 2 spc output sizes of HBM
+  // instead of nsplit (config 4: 947 -> 67 slabs, 47 -> 3.4 GB)
+  long spc = 0, nchunk = 0, rw = 0;
+  bool fold = false;
+  long slabs() const { return fold ? 1 + 2 * spc : nsplit + nsplit_fb; }
 };
 
-static int integral_plan(is3d_engine* e, const SpectraPlan& P, long nw, IntegralPlan& I) {
+#ifndef IS3D_SLAB_FOLD
+#define IS3D_SLAB_FOLD 1
+#endif
+
+// F_TS chunking of plan I over nw cells: tables of the whole window up to phitab_one bytes in one chunk, larger ones in
+// chunks of whole cell splits of about phitab_chunk bytes; both within half the device's free memory (plus the table
+// buffers this engine already holds)
+static void ts_chunking(is3d_engine* e, IntegralPlan& I) {
+  const int npT = (int)e->pT.size();
+  I.rw = phitab_row(e->p.df_mode, I.P.KJ, I.P.by != 0);
+  const long per_split = I.cps * (long)npT * I.rw;
+  const long whole = per_split * I.nsplit * 8;          // bytes of the whole surface's rows
+  long one = e->phitab_one, chunk = e->phitab_chunk;
+  {
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess && tot > 0) {
+      const long avail = (long)(fr / 2) + (e->phtab_cap + e->phtab2_cap) * (long)sizeof(double);
+      one = std::min(one, avail);
+      chunk = std::max(8L * per_split, std::min(chunk, avail / 2));
+    }
+  }
+  const long budget = whole <= one ? whole : chunk;
+  I.spc = std::max(1L, std::min(I.nsplit, budget / 8 / per_split));
+  I.nchunk = (I.nsplit + I.spc - 1) / I.spc;
+  I.fold = IS3D_SLAB_FOLD && I.nchunk > 1 && e->p.dimension == 3 && I.nsplit_fb == 0;
+}
+
+static int integral_plan(is3d_engine* e, const SpectraPlan& P, long nw, IntegralPlan& I, long cap_slabs = 0) {
   const int dim = e->p.dimension, mode = e->p.df_mode;
   const int npT = (int)e->pT.size();
   const int nk = (dim == 3) ? (int)e->y.size() : 1, nl = (dim == 3) ? 1 : (int)e->eta.size();
@@ -1716,9 +1783,18 @@ static int integral_plan(is3d_engine* e, const SpectraPlan& P, long nw, Integral
   // splits cost config 1's shape 0.5 ms of a 4.7 ms pass -- Grad 4.7 -> 4.2 ms, RTA-CE 5.4 -> 5.0 ms with 2k,
   // while the F_LY launch of the modified modes lost 14% with it: profiles/round3_r3p_ab_fill.log)
   const long by_fill = ((P.mp ? IS3D_FILL_WGS_MP : IS3D_FILL_WGS) + wgs - 1) / wgs;
-  const long by_l2 = ((long)NREC * 8 * nw + IS3D_SPLIT_BYTES - 1) / IS3D_SPLIT_BYTES;
+  const long by_l2 = ((long)NREC * 8 * nw + e->split_bytes - 1) / e->split_bytes;
   const long sstride = (long)npT * bx * KJ * kBlock;
-  const long max_slabs = std::max(8L, std::min((long)IS3D_MAX_SPLITS, (long)(IS3D_SLAB_BYTES / 8) / std::max(1L, sstride)));
+  // slab memory: the tuning cap, and at most half of what the device has free (plus the slabs this engine already
+  // holds) -- a smaller GPU, or several engines on one device, get fewer splits instead of a failed allocation
+  long slab_budget = e->slab_bytes;
+  {
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess && tot > 0)
+      slab_budget = std::min(slab_budget, (long)(fr / 2) + e->slab_cap * (long)sizeof(double));
+  }
+  long max_slabs = std::max(8L, std::min(e->max_splits, (slab_budget / 8) / std::max(1L, sstride)));
+  if (cap_slabs > 0) max_slabs = std::min(max_slabs, cap_slabs);
   long nsplit = std::max(by_fill, std::min(by_l2, max_slabs));
   if (nsplit >= 8) nsplit = (nsplit + 7) / 8 * 8;
   nsplit = std::max(1L, std::min(nsplit, max_split));
@@ -1729,6 +1805,7 @@ static int integral_plan(is3d_engine* e, const SpectraPlan& P, long nw, Integral
   // modified modes: the F_FB launch (separable-fallback lanes, cells listed by k_fbscan) writes its own
   // nsplit_fb slabs after the main ones; k_reduce sums both
   I.nsplit_fb = (mode >= PTM) ? std::max(1L, std::min(nsplit, 8L)) : 0;
+  if (P.ts) ts_chunking(e, I);
   return IS3D_OK;
 }
 
@@ -1771,12 +1848,8 @@ static int enqueue_spectra(is3d_engine* e, const IntegralPlan& I, const double* 
     // with a table buffer each, so the next chunk's k_phitab and the first workgroups of its k_spectra fill the
     // CUs the previous launch's last workgroups leave idle (config 4: 11 chunks ran 2811 ms back to back, one
     // 61 GB chunk 2739 ms)
-    const long rw = phitab_row(mode, KJ, P.by != 0);
-    const long per_split = cps * (long)npT * rw;
-    const long whole = per_split * nsplit * 8;          // bytes of the whole surface's rows
-    const long budget = whole <= e->phitab_one ? whole : e->phitab_chunk;
-    const long spc = std::max(1L, std::min(nsplit, budget / 8 / per_split));
-    const long phn = spc * cps, nchunk = (nsplit + spc - 1) / spc;
+    const long rw = I.rw, spc = I.spc, nchunk = I.nchunk;
+    const long phn = spc * cps;
     e->last_nchunk = nchunk;
     if (!ensure(e->d_phtab, e->phtab_cap, phn * npT * rw)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(phi tables) failed");
     if (nchunk > 1) {
@@ -1787,6 +1860,14 @@ static int enqueue_spectra(is3d_engine* e, const IntegralPlan& I, const double* 
       HIPCHK(e, hipEventRecord(e->fork, st));
       HIPCHK(e, hipStreamWaitEvent(e->side, e->fork, 0));
     }
+    if (I.fold) {
+      if (!e->fold_st) HIPCHK(e, hipStreamCreateWithFlags(&e->fold_st, hipStreamNonBlocking));
+      for (auto* v : {&e->ev_spec[0], &e->ev_spec[1], &e->ev_fold[0], &e->ev_fold[1], &e->fold_join})
+        if (!*v) HIPCHK(e, hipEventCreateWithFlags(v, hipEventDisableTiming));
+      HIPCHK(e, hipStreamWaitEvent(e->fold_st, e->fork, 0));
+    }
+    // folded: slab 0 is the accumulator, chunk ic's splits go to buffer ic & 1 (slabs 1 + (ic & 1) spc ...)
+    const int fgrid = (int)std::min(4096L, std::max(1L, (I.sstride + 255) / 256));
     for (long ic = 0; ic < nchunk; ic++) {
       const long s0 = ic * spc, ns = std::min(spc, nsplit - s0);
       const long c0 = s0 * cps, ncc = std::min(nw, (s0 + ns) * cps) - c0;
@@ -1798,19 +1879,32 @@ static int enqueue_spectra(is3d_engine* e, const IntegralPlan& I, const double* 
       ta.gate = gate; ta.gate_want = want;
       SpecArgs sc = sa;
       sc.split0 = (int)s0; sc.nsplit = (int)ns; sc.phtab = tab; sc.phn = phn; sc.phc0 = c0; sc.phrow = (int)rw;
+      double* buf = e->d_slab + (1 + (ic & 1) * spc) * I.sstride;
+      if (I.fold) { sc.slab = buf; sc.slab0 = (int)s0; }
       const dim3 grid((unsigned)(wgs * ns));
-      if (mode == GRAD) {
-        launch_phitab<GRAD>(cs, ta);
-        launch_spectra<GRAD>(grid, shmem, cs, sc, kflags, KJ);
-      } else {
-        launch_phitab<CE>(cs, ta);
-        launch_spectra<CE>(grid, shmem, cs, sc, kflags, KJ);
-      }
+      if (mode == GRAD) launch_phitab<GRAD>(cs, ta);
+      else launch_phitab<CE>(cs, ta);
+      // a folded chunk reusing slab buffer ic & 1 waits for the fold of chunk ic - 2, which emptied it
+      if (I.fold && ic >= 2) HIPCHK(e, hipStreamWaitEvent(cs, e->ev_fold[ic & 1], 0));
+      if (mode == GRAD) launch_spectra<GRAD>(grid, shmem, cs, sc, kflags, KJ);
+      else launch_spectra<CE>(grid, shmem, cs, sc, kflags, KJ);
       HIPCHK(e, hipGetLastError());
+      if (I.fold) {
+        HIPCHK(e, hipEventRecord(e->ev_spec[ic & 1], cs));
+        HIPCHK(e, hipStreamWaitEvent(e->fold_st, e->ev_spec[ic & 1], 0));
+        hipLaunchKernelGGL(k_fold, dim3((unsigned)fgrid), dim3(256), 0, e->fold_st, e->d_slab, (const double*)buf,
+                           I.sstride, (int)ns, ic == 0 ? 1 : 0);
+        HIPCHK(e, hipGetLastError());
+        HIPCHK(e, hipEventRecord(e->ev_fold[ic & 1], e->fold_st));
+      }
     }
     if (nchunk > 1) {
       HIPCHK(e, hipEventRecord(e->join, e->side));
       HIPCHK(e, hipStreamWaitEvent(st, e->join, 0));
+    }
+    if (I.fold) {
+      HIPCHK(e, hipEventRecord(e->fold_join, e->fold_st));
+      HIPCHK(e, hipStreamWaitEvent(st, e->fold_join, 0));
     }
   } else {
     const dim3 grid((unsigned)(wgs * nsplit));
@@ -1848,7 +1942,7 @@ static int enqueue_reduce(is3d_engine* e, const IntegralPlan& I, double* dev_out
   const int nk = ny_out, nl = (dim == 3) ? 1 : (int)e->eta.size();
   const int nc = e->ncls;
   ReduceArgs ra{};
-  ra.slab = e->d_slab; ra.sstride = I.sstride; ra.nsplit = (int)(I.nsplit + I.nsplit_fb);
+  ra.slab = e->d_slab; ra.sstride = I.sstride; ra.nsplit = I.fold ? 1 : (int)(I.nsplit + I.nsplit_fb);
   ra.nbx = (int)I.bx; ra.npart = nc; ra.npT = npT; ra.nphi = nphi; ra.nk = nk; ra.nl = nl; ra.ny_out = ny_out; ra.kj = I.P.KJ;
   ra.ntask = I.ntask;
   ra.sorig = e->d_sorig; ra.degen_orig = e->d_degen_orig; ra.prefactor = std::pow(2.0 * M_PI * kHbarC, -3);
@@ -1911,12 +2005,15 @@ static int launch_end(is3d_engine* e) {
   IntegralPlan I{}, J{};
   int rc = integral_plan(e, P, nw, I);
   if (rc) return rc;
+  e->last_nsplit = I.nsplit;
+  e->last_nslab = I.slabs();
   const bool gated = mode <= CE && P.ts;
   if (gated) {
-    rc = integral_plan(e, spectra_plan(e, false), nw, J);
+    // the fallback plan shares the slab memory: a folded main plan caps its splits at the same footprint
+    rc = integral_plan(e, spectra_plan(e, false), nw, J, I.fold ? I.slabs() : 0);
     if (rc) return rc;
   }
-  const long slab_need = std::max((I.nsplit + I.nsplit_fb) * I.sstride, gated ? (J.nsplit + J.nsplit_fb) * J.sstride : 0L);
+  const long slab_need = std::max(I.slabs() * I.sstride, gated ? J.slabs() * J.sstride : 0L);
   if (!ensure(e->d_slab, e->slab_cap, slab_need)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(slabs) failed");
   const unsigned long long* gate = gated ? e->d_cnt + 4 : nullptr;
   rc = enqueue_spectra(e, I, rec_w, nw, st, gate, 0);

@@ -105,6 +105,7 @@ struct SpecArgs {
   const int* fbcells;         // F_FB launch: ascending indices of the cells with separable-fallback lanes
   const int* fbcount;         //   (k_fbscan, device-side) and their number
   int split0;                 // first cell split of this launch (F_TS launches cover the splits chunk by chunk)
+  int slab0;                  // split whose slab `slab` points at (folded F_TS chunks: a chunk's own slab buffer)
   // F_TS: the per-(cell, pT, phi) tables k_phitab wrote for this chunk of cells, rows [pT][cell - phc0][phrow]
   const double* phtab; long phn, phc0; int phrow;
   // device-side choice between two enqueued plans (engine.hip launch_end): the workgroups return at once unless
@@ -808,7 +809,7 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
   const int* const fbl = FB ? A.fbcells : nullptr;
   // this thread's slab entries, layout [split][pT][lane group][phi slot][lane] (see the stores at the end); F_MP:
   // lane group 0 of the lane's own pT, slot = its task
-  double* const out = A.slab + (long)split * A.sstride + ((long)ipt * A.nbx + lane_group) * (KJ * kBlock) +
+  double* const out = A.slab + (long)(split - A.slab0) * A.sstride + ((long)ipt * A.nbx + lane_group) * (KJ * kBlock) +
                       (MP ? task : (long)tid);
 
   // ---- phase A / B of one tile (records s_rec, ntx cells) into table buffer tb: {b', Phi} and PD (or
@@ -1045,15 +1046,16 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
         if constexpr (MODMAIN) {
           if ((IS3D_EARLY_SKIP & 2) && IS3D_MOD_SQ_BOUNDS && mod_skips(R, Y, mT, m2, pT, baryon, !LY)) continue;
           ModLane M;
-          mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, s_etab, M, !LY, !LY && KJ % 4 == 0);
-          if (M.skip) continue;
           const dbl2* MW = mwt + t * nphp + j0;
+          const double* MT = s_mt + ((long)t * nqw + row) * prow;
+          if constexpr (!LY && KJ % 4 == 0) mod_setup<KJ>(R, Y, mT, m2, pT, sign, baryon, rn_abs, s_etab, M, true, true, MW, MT);
+          else mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, s_etab, M, !LY, false);
+          if (M.skip) continue;
           if constexpr (LY) {        // no T2 rows: the lane's linear forms (mod_pair_lane_t)
             if (M.clamp) mod_phi_loop_lane<FLAGS, true, KJ>(M, CSl, MW, acc);
             else mod_phi_loop_lane<FLAGS, false, KJ>(M, CSl, MW, acc);
             continue;
           }
-          const double* MT = s_mt + ((long)t * nqw + row) * prow;
           if (M.clamp) mod_phi_loop_tab<FLAGS, true, KJ>(M, MW, MT, acc);
           else if (IS3D_MOD_TAIL && M.tail) mod_phi_loop_tab_tail<FLAGS, KJ>(M, MW, MT, acc);
           else mod_phi_loop_tab<FLAGS, false, KJ>(M, MW, MT, acc);

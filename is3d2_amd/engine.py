@@ -84,12 +84,13 @@ class Engine:
         self._chk(self.lib.is3d_set_params(self._e, C.byref(_lib.Params(**p))))
 
     def set_tuning(self, key, value):
-        """Engine knob (is3d_set_tuning): "phitab_one_bytes" / "phitab_chunk_bytes" (F_TS table chunking); a
-        negative value restores the default."""
+        """Engine knob (is3d_set_tuning): "phitab_one_bytes" / "phitab_chunk_bytes" (F_TS table chunking),
+        "max_splits" / "slab_bytes" / "split_bytes" (k_spectra's cell splits); a negative value restores the default."""
         self._chk(self.lib.is3d_set_tuning(self._e, key.encode(), int(value)))
 
     def get_tuning(self, key):
-        """is3d_get_tuning: the knobs above, or "phitab_chunks" (F_TS chunks of the last launch); -1 = unknown."""
+        """is3d_get_tuning: the knobs above, "phitab_chunks" (F_TS chunks of the last launch) or "splits" (cell splits
+        of the last launch); -1 = unknown."""
         return self.lib.is3d_get_tuning(self._e, key.encode())
 
     def set_species(self, mass, sign, degen, baryon):

@@ -1,3 +1,5 @@
+#include <cstdlib>
+#include <cstdio>
 // cf_emulator.cpp -- TEST INFRASTRUCTURE ONLY.
 //
 // Runs the engine's device math (is3d2_amd/csrc/cf_math.h, aniso_math.h) serially on
@@ -74,9 +76,17 @@ static long* g_census = nullptr;
 extern "C" void emu_set_census(long* counts) { g_census = counts; }
 // optional per-lane record (tools/lane_census.py --waves): [pT][cell][species][q] = 1 + (skip 0 / tail 1 / other 2)
 static signed char* g_census_lane = nullptr;
+// optional census of the modified (non-separable) lanes: counts of skipped, clamped, Boltzmann-tail and other lanes
+static long* g_census_mod = nullptr;
+extern "C" void emu_set_census_mod(long* counts) { g_census_mod = counts; }
 extern "C" void emu_set_census_lanes(signed char* buf) { g_census_lane = buf; }
 // lanes whose smallest exponent exceeds g_near_x (not tail) are recorded as 4 (tools/lane_census.py --near)
 static double g_near_x = 1e300;
+// optional check of sep_slow_cell (k_prep's per-cell bound, engine.hip launch_end): [0] separable lanes off the fast
+// path (smallest exponent below kExpFast), [1] such lanes in cells the bound did NOT flag (must stay 0), [2] cells
+// flagged, [3] live cells, [4] (as double bits) the smallest lane exponent x - zb seen in an unflagged cell
+static long* g_slow_check = nullptr;
+extern "C" void emu_set_slow_check(long* out) { g_slow_check = out; }
 extern "C" void emu_set_near_x(double x) { g_near_x = x; }
 
 extern "C" int emu_spectra_v(const orc_params* p, const orc_setup* su, const orc_surface* S, int chains, int op,
@@ -138,6 +148,21 @@ extern "C" int emu_spectra_v(const orc_params* p, const orc_setup* su, const orc
       int broken = 0;
       prep_famod_b(k, R, &aux[(size_t)c * 9], &sol[(size_t)c * 6], &broken);
       st_break += broken;
+    }
+  }
+  std::vector<char> slow_cell;
+  double slow_min_ok = 1e300;
+  if (g_slow_check && mode <= CE) {
+    double pmax = 0.0, bmax = 0.0;
+    for (int i = 0; i < npT; i++) pmax = fmax(pmax, su->pT[i]);
+    for (int s2 = 0; s2 < np; s2++) bmax = fmax(bmax, fabs(su->baryon[s2]));
+    slow_cell.assign(n, 0);
+    for (long c = 0; c < n; c++) {
+      const double* R = &rec[(size_t)c * NREC];
+      if (R[R_KIND] == 0.0) continue;
+      g_slow_check[3]++;
+      slow_cell[c] = sep_slow_cell(R, pmax, bmax) ? 1 : 0;
+      g_slow_check[2] += slow_cell[c];
     }
   }
   // --- spectra (same per-lane order as k_spectra: cells ascending, then l, then phi)
@@ -208,6 +233,10 @@ extern "C" int emu_spectra_v(const orc_params* p, const orc_setup* su, const orc
               sep_setup(sep_flavor(mode), R, Y, mT, mT * mT, m2, mT * baryon, pT, sign, baryon, kExp2Tab, L,
                         (use_tb || pd_tail) && tail, near);
               if (g_census) g_census[i * 3 + (L.skip ? 0 : (L.tail ? 1 : 2))]++;
+              if (!slow_cell.empty() && !L.skip) {
+                if (!L.fast) { g_slow_check[0]++; if (!slow_cell[c]) g_slow_check[1]++; }
+                if (!slow_cell[c]) slow_min_ok = fmin(slow_min_ok, L.x - pT * R[R_ZB]);
+              }
               if (g_census_lane)
                 g_census_lane[(((size_t)i * n + c) * np + s) * nq + kk * nl + l] =
                     (signed char)(1 + (L.skip ? 0 : (L.tail ? 1 : (L.near || L.x - pT * R[R_ZB] > g_near_x ? 3 : 2))));
@@ -333,17 +362,31 @@ extern "C" int emu_spectra_v(const orc_params* p, const orc_setup* su, const orc
               ModLane M;
               // variant 16 (with 4): k_spectra's Boltzmann-tail table lanes (IS3D_MOD_TAIL builds; per lane here)
               const bool mtail = (variant & 20) == 20 && op != 0 && nphi % 4 == 0;
-              mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, kExp2Tab, M, true, mtail);
-              if (M.skip) continue;
-              int j = 0;
-              if ((variant & 4) && op != 0) {   // k_spectra's table form: {PDm, Qv} and T2 rows
-                std::vector<dbl2> MW(nphi);
-                std::vector<double> MT(nphi);
+              // k_spectra's table lanes (variant 4) take the exact range of a wide lane's points (IS3D_MOD_EXACT)
+              std::vector<dbl2> MW(nphi);
+              std::vector<double> MT(nphi);
+              if ((variant & 4) && op != 0) {
                 for (int jj = 0; jj < nphi; jj++) {
                   MW[jj].x = modpdm(R, CS[jj]); MW[jj].y = QV[jj];
                   MT[jj] = modt2(R, Y, CS[jj]);
                 }
+                mod_setup<-1>(R, Y, mT, m2, pT, sign, baryon, rn_abs, kExp2Tab, M, true, mtail, MW.data(), MT.data(), nphi);
+              } else {
+                mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, kExp2Tab, M, true, mtail);
+              }
+              if (g_census_mod) g_census_mod[M.skip ? 0 : M.clamp ? 1 : M.tail ? 2 : 3]++;
+              if (g_census_mod && g_census_lane)
+                g_census_lane[(((size_t)i * n + c) * np + s) * nq + kk * nl + l] =
+                    (signed char)(11 + (M.skip ? 0 : M.clamp ? 1 : M.tail ? 2 : 3));
+              if (M.skip) continue;
+              int j = 0;
+              if ((variant & 4) && op != 0) {   // k_spectra's table form: {PDm, Qv} and T2 rows (MW, MT above)
                 const bool of = p->outflow != 0;
+                if (g_census_mod && M.clamp && getenv("EMU_SPAN")) {
+                  double xmn = 1e300, xmx = 0;
+                  for (int jj = 0; jj < nphi; jj++) { double X = fma(M.mT, MT[jj], M.E0 + MW[jj].y); xmn = fmin(xmn, sqrt(X)); xmx = fmax(xmx, sqrt(X)); }
+                  printf("SPAN %g %g %g chem %g\n", xmn / kExpTabN, xmx / kExpTabN, (xmx - xmn) / kExpTabN, M.chemm);
+                }
                 if (spectra_kj(nphi) % 4 == 0)
                   for (; j + 3 < nphi; j += 4) {
                     if (M.tail) { if (of) mod_quad_tab_tail_t<true>(M, &MW[j], &MT[j], &a[j]); else mod_quad_tab_tail_t<false>(M, &MW[j], &MT[j], &a[j]); }
@@ -409,6 +452,7 @@ extern "C" int emu_spectra_v(const orc_params* p, const orc_setup* su, const orc
       for (long c = 0; c < n; c++) out[(size_t)s * n + c] *= prefactor * su->degen[s];
   }
   if (stats) { stats[0] = st_break; stats[1] = st_pl; stats[2] = st_fail; stats[3] = st_it; }
+  if (g_slow_check) std::memcpy(&g_slow_check[4], &slow_min_ok, sizeof(double));
   return 0;
 }
 

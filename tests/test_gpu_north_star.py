@@ -26,12 +26,14 @@ def config4_spec(mode):
     return make_spec(hrg_eos=2, chosen="smash", df_mode=mode, dimension=3, pT="pT48", phi="phi32", y="y21")
 
 
-def run(spec, s, tuning=None, T_avg=None):
+def run(spec, s, tuning=None, T_avg=None, info=None):
     e = build_engine(spec, s, T_avg=T_avg)
     for k, v in (tuning or {}).items():
         e.set_tuning(k, v)
     out = e.calculate_spectra()
     chunks = e.get_tuning("phitab_chunks")
+    if info is not None:
+        info.update(splits=e.get_tuning("splits"), slabs=e.get_tuning("slabs"))
     e.close()
     return out, chunks
 
@@ -44,10 +46,15 @@ def test_chunked_scalar_tables_match_oracle_and_one_chunk(mode, chunk_bytes):
     splits' slabs; the chunking changes no summation order) and within the parity bars of the oracle."""
     s = synth.as_read(synth.surface(200, seed=41, dimension=3, full3d=True))
     spec = config4_spec(mode)
-    one, n1 = run(spec, s)
-    many, nk = run(spec, s, {"phitab_one_bytes": 0, "phitab_chunk_bytes": chunk_bytes})
+    i1, ik = {}, {}
+    one, n1 = run(spec, s, info=i1)
+    many, nk = run(spec, s, {"phitab_one_bytes": 0, "phitab_chunk_bytes": chunk_bytes}, info=ik)
     assert n1 == 1, n1
     assert nk >= 3, nk
+    # the chunks fold their slabs into one accumulator as they finish (k_fold, split order): same sums bit for bit
+    assert i1["slabs"] == i1["splits"] and ik["splits"] == i1["splits"], (i1, ik)
+    spc = -(-ik["splits"] // nk)
+    assert ik["slabs"] == 1 + 2 * spc, (ik, nk)
     assert np.array_equal(many, one)
     ref = O.spectra(spec, s, threads=8)
     rel, zr, zg = parity(many, ref)
@@ -79,6 +86,12 @@ def test_tuning_keys():
     assert e.get_tuning("phitab_chunk_bytes") == 12345
     e.set_tuning("phitab_chunk_bytes", -1)
     assert e.get_tuning("phitab_chunk_bytes") == 2 << 30
+    for key, dflt in (("max_splits", 1024), ("slab_bytes", 48 << 30), ("split_bytes", 512 << 10)):
+        assert e.get_tuning(key) == dflt
+        e.set_tuning(key, 7)
+        assert e.get_tuning(key) == 7
+        e.set_tuning(key, -1)
+        assert e.get_tuning(key) == dflt
     assert e.get_tuning("no_such_key") == -1
     with pytest.raises(Exception, match="unknown key"):
         e.set_tuning("no_such_key", 1)
@@ -95,6 +108,7 @@ def test_north_star_full_size_chunked_properties():
     e = build_engine(spec, s)
     full = e.calculate_spectra()
     nchunk = e.get_tuning("phitab_chunks")
+    splits, slabs = e.get_tuning("splits"), e.get_tuning("slabs")
     n = len(s["tau"])
     h = n // 2 + 4321
     e.set_surface({k: np.ascontiguousarray(v[:h]) for k, v in s.items()})
@@ -108,6 +122,7 @@ def test_north_star_full_size_chunked_properties():
     d = e.calculate_spectra()
     e.close()
     assert nchunk >= 3, nchunk
+    assert slabs <= 2 * (-(-splits // nchunk)) + 1 and 50 * 2**20 * slabs <= 10 * 2**30, (splits, slabs, nchunk)
     assert np.isfinite(full).all() and (full != 0).sum() > 0.5 * full.size
     m = np.abs(full) > 1e-290
     assert float((np.abs((a + b)[m] - full[m]) / np.abs(full[m])).max()) < TOL

@@ -242,3 +242,63 @@ def test_modified_table_lanes(mode, baryon):
     assert rel < 1e-8, rel
     assert zr == zg
     assert not np.array_equal(tail, got)
+
+
+def test_modified_wide_lanes_exact_range():
+    """Modified lanes whose momentum bounds |mT U| -+ pT |V|max span more than 250 binades (high pT, strong
+    modification): mod_setup<KJ> takes the exact range of the lane's points (IS3D_MOD_EXACT), so they run the
+    table / Boltzmann-tail fours instead of the clamped en form.  On the config-2 grid the clamped share falls from
+    ~5% of the lanes to ~0.1% (tools: /tmp census of round 5); the spectra still meet the oracle."""
+    s = synth.as_read(synth.surface(6, seed=31, dimension=3, full3d=True))
+    spec = make_spec(hrg_eos=2, chosen="smash", df_mode=3, dimension=3, pT="pT48", phi="phi32")
+    cnt = np.zeros(4, dtype=np.int64)
+    lib = emulator()
+    lib.emu_set_census_mod(cnt.ctypes.data_as(C.POINTER(C.c_long)))
+    try:
+        got, _ = emu_spectra(spec, s, variant=4 | 16)
+    finally:
+        lib.emu_set_census_mod(None)
+    skip, clamp, tail, other = (int(v) for v in cnt)
+    live = clamp + tail + other
+    assert tail > 0 and other > 0
+    assert clamp < 0.01 * live, cnt
+    ref = O.spectra(spec, s, threads=4)
+    rel, zr, zg = parity(got, ref, floor=1e-290)
+    assert rel < 1e-8, rel
+    assert zr == zg
+    assert rel_quantile(got, ref) < 1e-11
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_slow_cell_bound_sweep(mode):
+    """sep_slow_cell (k_prep's per-cell bound that sends a surface to the kernels with the slow per-point loop instead
+    of F_TS, engine.hip launch_end): swept across its threshold -- mu_B / T from 250 to 340 in 1-unit steps, flow
+    u_perp up to ~3 -- every separable lane whose smallest exponent x - zb falls below kExpFast = -300 must sit in a
+    flagged cell, and the bound flags nothing below mu_B / T = 290 (its margin of 10)."""
+    n = 91
+    s = synth.as_read(synth.surface(n, seed=37, dimension=3, baryon=True, full3d=True))
+    chem = 250.0 + np.arange(n)
+    s["T"] = np.full(n, 0.12)
+    s["muB"] = chem * 0.12
+    flow = 1.0 + 2.0 * (np.arange(n) % 7) / 6.0
+    s["ux"] = s["ux"] * flow
+    s["uy"] = s["uy"] * flow
+    spec = make_spec(hrg_eos=2, chosen="pikp", df_mode=mode, dimension=3, pT="pT24", phi="phi32", y="y21",
+                     include_baryon=1, include_baryondiff_deltaf=1)
+    T, muB, tab = spec["df"]
+    spec["df"] = (T, np.asarray(muB) * 100.0, tab)     # stretched mu_B axis: the tables reach mu_B / T = 375
+    out = np.zeros(5, dtype=np.int64)
+    lib = emulator()
+    lib.emu_set_slow_check(out.ctypes.data_as(C.POINTER(C.c_long)))
+    try:
+        emu_spectra(spec, s, variant=1 | 2)
+    finally:
+        lib.emu_set_slow_check(None)
+    off_fast, violations, flagged, live = (int(v) for v in out[:4])
+    min_ok = float(out[4:5].view(np.float64)[0])
+    assert live > 0.9 * n                  # (u.dsigma <= 0 cells are skipped)
+    assert off_fast > 0                    # the sweep reaches lanes off the fast path ...
+    assert violations == 0, out            # ... and every one of them is in a flagged cell
+    assert 0 < flagged < n                 # the threshold falls inside the sweep
+    assert min_ok > -300.0, min_ok         # unflagged cells keep every lane on the fast path
+    assert flagged <= int(np.sum(chem >= 289.0)), (flagged, out)   # nothing flagged well below mu_B / T = 290
