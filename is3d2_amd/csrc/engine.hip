@@ -186,6 +186,11 @@ struct AnisoArgs {
 __global__ __launch_bounds__(64, IS3D_NEWTON_WAVES ? IS3D_NEWTON_WAVES : 1) void k_aniso(AnisoArgs A) {
   const long chain = blockIdx.x;
   const int lane = threadIdx.x;
+  __shared__ double s_etab[kExpTabN];                       // aniso_math.h aexp (IS3D_ANISO_FAST)
+  for (int i = lane; i < kExpTabN; i += 64) s_etab[i] = kExp2Tab[i];
+  __syncthreads();
+  Hadrons h = A.h;
+  h.etab = s_etab;
   double state[4] = {0.0, 0.0, 0.0, 0.0};
   long cnt[3] = {0, 0, 0};
   for (long c = A.c0 + chain; c < A.c0 + A.n; c += A.chains) {
@@ -194,7 +199,7 @@ __global__ __launch_bounds__(64, IS3D_NEWTON_WAVES ? IS3D_NEWTON_WAVES : 1) void
 #pragma unroll
     for (int f = 0; f < 4; f++) ain[f] = A.ain[(long)f * A.stride + c];
     double out[6];
-    aniso_cell(ain, A.h, lane, 64, WaveSum(), A.fp2, state, out, cnt);
+    aniso_cell(ain, h, lane, 64, WaveSum(), A.fp2, state, out, cnt);
     if (lane == 0) {
 #pragma unroll
       for (int f = 0; f < 6; f++) A.sol[(long)f * A.stride + c] = out[f];
@@ -254,7 +259,7 @@ __device__ __forceinline__ bool state_eq(const double* a, const double* b) {
 
 // Run segment `seg` from `state` (its start): re-run mode (sync) stops at the first cell whose new state equals
 // the stored one and returns true (end state unchanged); otherwise the state after the last cell is in `state`.
-__device__ bool chain_segment_run(const ChainArgs& A, long seg, double* state, bool sync) {
+__device__ bool chain_segment_run(const ChainArgs& A, Hadrons h, long seg, double* state, bool sync) {
   const int lane = threadIdx.x;
   __shared__ double s_red[kRedN * IS3D_CHAIN_W];
   const long c = seg / A.nspc, s = seg % A.nspc;
@@ -273,7 +278,7 @@ __device__ bool chain_segment_run(const ChainArgs& A, long seg, double* state, b
     for (int f = 0; f < 4; f++) old[f] = A.sta[(long)f * A.n + cell];
     double out[6];
     long cnt[3] = {0, 0, 0};
-    aniso_cell(ain, A.h, lane, 64 * IS3D_CHAIN_W, BlockSum<IS3D_CHAIN_W>{s_red}, A.fp2, state, out, cnt);
+    aniso_cell(ain, h, lane, 64 * IS3D_CHAIN_W, BlockSum<IS3D_CHAIN_W>{s_red}, A.fp2, state, out, cnt);
     const bool same = sync && state_eq(state, old);
     if (lane == 0) {
 #pragma unroll
@@ -287,6 +292,15 @@ __device__ bool chain_segment_run(const ChainArgs& A, long seg, double* state, b
   return false;
 }
 
+// the chain kernels' Hadrons with the LDS exp table of aniso_math.h's aexp (filled by the whole workgroup)
+__device__ __forceinline__ Hadrons chain_hadrons(const ChainArgs& A, double* s_etab) {
+  for (int i = threadIdx.x; i < kExpTabN; i += blockDim.x) s_etab[i] = kExp2Tab[i];
+  __syncthreads();
+  Hadrons h = A.h;
+  h.etab = s_etab;
+  return h;
+}
+
 // one workgroup of IS3D_CHAIN_W wavefronts per segment (the lanes share each Newton evaluation's terms); every
 // branch below is uniform over the workgroup (the reductions hand all lanes the same bits)
 __global__ __launch_bounds__(64 * IS3D_CHAIN_W, IS3D_NEWTON_WAVES ? IS3D_NEWTON_WAVES : 1) void k_chain_pass(ChainArgs A, int pass) {
@@ -297,6 +311,8 @@ __global__ __launch_bounds__(64 * IS3D_CHAIN_W, IS3D_NEWTON_WAVES ? IS3D_NEWTON_
   // converged: the remaining passes are no-ops (a shard with a predecessor always checks its starts: the boundary
   // pushed in may still move)
   if (pass > 0 && A.changed[pass - 1] == 0 && !A.has_pred) return;
+  __shared__ double s_etab[kExpTabN];
+  const Hadrons h = chain_hadrons(A, s_etab);
   const double* prev = A.send + (long)((pass + 1) & 1) * 4 * nseg;
   double* cur = A.send + (long)(pass & 1) * 4 * nseg;
   double state[4] = {0.0, 0.0, 0.0, 0.0};                   // cold: no previous success in this chain
@@ -324,7 +340,7 @@ __global__ __launch_bounds__(64 * IS3D_CHAIN_W, IS3D_NEWTON_WAVES ? IS3D_NEWTON_
   }
   if (!done) {
     if (lane == 0) for (int f = 0; f < 4; f++) A.sstart[f * nseg + seg] = state[f];
-    const bool synced = chain_segment_run(A, seg, state, pass > 0);
+    const bool synced = chain_segment_run(A, h, seg, state, pass > 0);
     if (lane == 0) {
       if (synced) {
         for (int f = 0; f < 4; f++) cur[f * nseg + seg] = prev[f * nseg + seg];
@@ -376,6 +392,8 @@ __global__ __launch_bounds__(64 * IS3D_CHAIN_W) void k_chain_finish(ChainArgs A)
     }
     return;
   }
+  __shared__ double s_etab[kExpTabN];
+  const Hadrons h = chain_hadrons(A, s_etab);
   // the running end state stays in registers (uniform over the wavefront): no memory round trip between
   // segments, and every array element this kernel reads was written by an earlier launch or not at all
   double carry[4] = {0.0, 0.0, 0.0, 0.0};
@@ -396,7 +414,7 @@ __global__ __launch_bounds__(64 * IS3D_CHAIN_W) void k_chain_finish(ChainArgs A)
     } else {
       if (lane == 0) for (int f = 0; f < 4; f++) A.sstart[f * nseg + seg] = carry[f];
       double state[4] = {carry[0], carry[1], carry[2], carry[3]};
-      if (chain_segment_run(A, seg, state, true)) {
+      if (chain_segment_run(A, h, seg, state, true)) {
 #pragma unroll
         for (int f = 0; f < 4; f++) carry[f] = cur[f * nseg + seg];
       } else {
@@ -838,15 +856,14 @@ struct is3d_engine {
   const double* d_aniso_h = nullptr;   // [3][n_aniso_h] merged (mass, sign, degeneracy) of the PTMA hadrons
   int n_aniso_h = 0;
   int* d_sorig = nullptr;
-  // PTM renormalisation classes: sorted species with identical (mass, sign, degeneracy, baryon) share one
-  // n_linear / n_mod per cell (ptm_renorm depends on nothing else): d_rcls[s] = class of sorted species s,
+  // PTM renormalisation classes: sorted species with identical (mass, sign, baryon) and a zero / nonzero degeneracy
+  // share one n_linear / n_mod per cell (ptm_renorm depends on nothing else, ptm_gkey): d_rcls[s] = class of sorted species s,
   // d_rrep[k] = a representative sorted species of class k (SMASH 444 -> nrcls classes)
   int* d_rcls = nullptr;
   int* d_rrep = nullptr;
   int nrcls = 0;
   // integrand classes (is3d_set_species_classes, default on): the momentum integrals see a species only through
-  // its (mass, sign, baryon) -- plus its degeneracy in PTM, whose renormalisation is evaluated per (mass, sign,
-  // degeneracy, baryon) -- and the engine applies the degeneracy once, to the cell sum, in k_reduce (the reference
+  // its (mass, sign, baryon) -- plus, in PTM, whether its degeneracy is zero (ptm_gkey) -- and the engine applies the degeneracy once, to the cell sum, in k_reduce (the reference
   // multiplies every cell's term by prefactor x degeneracy, MomentumSpectra.cpp:365: the same product up to
   // rounding), so sorted species with identical keys have bit-identical cell sums: k_spectra / k_dndx integrate one lane species per class (SMASH 444 -> 193, UrQMD 305 -> 124) and the
   // reduction writes every member.  d_cmass/d_csign/d_cbaryon: class values, d_crcls: class -> renorm class,
@@ -1302,6 +1319,18 @@ static SpectraPlan spectra_plan(const is3d_engine* e, bool allow_ts = true) {
   return P;
 }
 
+// PTM's renormalisation n_linear / n_mod (MomentumSpectra.cpp:790-832) is a ratio of two sums that both carry the
+// degeneracy as a factor, so it depends on (mass, sign, baryon) alone -- except g = 0, where it is 0 / 0 = NaN and the
+// species is skipped.  The renormalisation classes and PTM's integrand classes therefore key on whether g is zero
+// (IS3D_PTM_GCLASS 0: SMASH 205 -> 193 PTM lane classes, the same as the other modes; the class representative's g
+// cancels to rounding, ~1e-16); IS3D_PTM_GCLASS 1 keys on g itself (round 3 / 4)
+#ifndef IS3D_PTM_GCLASS
+#define IS3D_PTM_GCLASS 0
+#endif
+static uint64_t ptm_gkey(double g) {
+  return IS3D_PTM_GCLASS ? __builtin_bit_cast(uint64_t, g) : (uint64_t)(g == 0.0 ? 1 : 0);
+}
+
 static int finalize_tables(is3d_engine* e) {
   if (!e->have_params) return e->fail(IS3D_ERR_STATE, "is3d_set_params not called");
   if (!e->have_species) return e->fail(IS3D_ERR_STATE, "is3d_set_species not called");
@@ -1385,8 +1414,7 @@ static int finalize_tables(is3d_engine* e) {
     std::map<std::array<uint64_t, 4>, int> cls;
     for (int i = 0; i < np; i++) {
       const std::array<uint64_t, 4> key{__builtin_bit_cast(uint64_t, sm[i]), __builtin_bit_cast(uint64_t, ss[i]),
-                                        __builtin_bit_cast(uint64_t, sb[i]),
-                                        mode == PTM ? __builtin_bit_cast(uint64_t, sd[i]) : (uint64_t)0};
+                                        __builtin_bit_cast(uint64_t, sb[i]), mode == PTM ? ptm_gkey(sd[i]) : (uint64_t)0};
       int c = (int)crep.size();
       if (e->classes) {
         auto it = cls.find(key);
@@ -1456,7 +1484,7 @@ static int finalize_tables(is3d_engine* e) {
     std::map<std::array<uint64_t, 4>, int> cls;
     for (int i = 0; i < np; i++) {
       const std::array<uint64_t, 4> key{__builtin_bit_cast(uint64_t, sm[i]), __builtin_bit_cast(uint64_t, ss[i]),
-                                        __builtin_bit_cast(uint64_t, sd[i]), __builtin_bit_cast(uint64_t, sb[i])};
+                                        ptm_gkey(sd[i]), __builtin_bit_cast(uint64_t, sb[i])};
       auto it = cls.find(key);
       if (it == cls.end()) { it = cls.emplace(key, (int)rrep.size()).first; rrep.push_back(i); }
       rcls[i] = it->second;
@@ -1673,7 +1701,9 @@ static int launch_begin(is3d_engine* e, double* dev_out, void* stream, long q0, 
       const long npos = std::max(1L, ca.q1 - ca.q0);
       // ~IS3D_CHAIN_SLOTS segments of at least IS3D_CHAIN_L positions (sized to the GPU's resident k_chain_pass
       // wavefronts instead -- 2048, L = 49 at 10^5 cells -- measured the same: profiles/round4_r4b_ab_newton.log)
-      const long spc_max = std::max(1L, (long)IS3D_CHAIN_SLOTS / ca.C);
+      long slots = IS3D_CHAIN_SLOTS;
+      if (const char* v = std::getenv("IS3D_CHAIN_SLOTS")) slots = std::max(1L, std::atol(v));   // A/B knob
+      const long spc_max = std::max(1L, slots / ca.C);
       ca.L = std::max((long)IS3D_CHAIN_L, (npos + spc_max - 1) / spc_max);
       ca.nspc = (npos + ca.L - 1) / ca.L;
       ca.npass = kChainPasses;
