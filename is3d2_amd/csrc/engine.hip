@@ -502,30 +502,63 @@ __global__ __launch_bounds__(256) void k_cell_cost(const double* rec, long n, do
 
 // Modified modes: the cells whose lanes may take the separable fallback (breakdown: R_KIND == 1; narrow
 // rapidity windows: R_NARROW != 0, MomentumSpectra.cpp:863-871), listed in ascending order for the F_FB
-// launch.  One workgroup: each thread counts a contiguous chunk, an LDS scan gives the offsets, the chunks
-// are written in order -- deterministic, and no host round trip (the count stays on the device).
-__global__ __launch_bounds__(1024) void k_fbscan(const double* rec, long n, int* cells, int* count) {
-  __shared__ int s_off[1024];
-  const int t = threadIdx.x;
-  const long ch = (n + 1023) / 1024, lo = min(n, t * ch), hi = min(n, lo + ch);
-  auto fb = [&](long c) {
-    const double* R = rec + c * NREC;
-    return R[R_KIND] == 1.0 || (R[R_KIND] == 2.0 && R[R_NARROW] != 0.0);
-  };
+// launch.  kFbBlocks workgroups each own a contiguous cell range: k_fbcount counts each range's cells, k_fbwrite
+// writes them in order after the counts of the ranges before it (wave ballots + an LDS prefix per 256 cells) --
+// deterministic, and no host round trip (the count stays on the device).  (One workgroup walking per-thread chunks
+// took 44 ms per config-5 pass, 5e6 cells.)
+constexpr int kFbBlocks = 1024;
+
+__device__ __forceinline__ bool fb_cell(const double* rec, long c) {
+  const double* R = rec + c * NREC;
+  return R[R_KIND] == 1.0 || (R[R_KIND] == 2.0 && R[R_NARROW] != 0.0);
+}
+
+__global__ __launch_bounds__(256) void k_fbcount(const double* rec, long n, int* bcnt) {
+  const long ch = (n + kFbBlocks - 1) / kFbBlocks, lo = min(n, (long)blockIdx.x * ch), hi = min(n, lo + ch);
   int cnt = 0;
-  for (long c = lo; c < hi; c++) cnt += fb(c) ? 1 : 0;
-  s_off[t] = cnt;
+  for (long c = lo + threadIdx.x; c < hi; c += 256) cnt += fb_cell(rec, c) ? 1 : 0;
+  __shared__ int s[256];
+  s[threadIdx.x] = cnt;
   __syncthreads();
-  for (int d = 1; d < 1024; d <<= 1) {     // inclusive Hillis-Steele scan
-    const int v = (t >= d) ? s_off[t - d] : 0;
-    __syncthreads();
-    s_off[t] += v;
+  for (int d = 128; d > 0; d >>= 1) {
+    if (threadIdx.x < d) s[threadIdx.x] += s[threadIdx.x + d];
     __syncthreads();
   }
-  int o = s_off[t] - cnt;
-  for (long c = lo; c < hi; c++)
-    if (fb(c)) cells[o++] = (int)c;
-  if (t == 1023) *count = s_off[1023];
+  if (threadIdx.x == 0) bcnt[blockIdx.x] = s[0];
+}
+
+__global__ __launch_bounds__(256) void k_fbwrite(const double* rec, long n, const int* bcnt, int* cells, int* count) {
+  const long ch = (n + kFbBlocks - 1) / kFbBlocks, lo = min(n, (long)blockIdx.x * ch), hi = min(n, lo + ch);
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  __shared__ int s_base, s_w[4];
+  if (t == 0) {
+    int o = 0;
+    for (int b = 0; b < (int)blockIdx.x; b++) o += bcnt[b];
+    s_base = o;
+    if (blockIdx.x == kFbBlocks - 1) *count = o + bcnt[blockIdx.x];
+  }
+  __syncthreads();
+  for (long c0 = lo; c0 < hi; c0 += 256) {
+    const long c = c0 + t;
+    const bool f = c < hi && fb_cell(rec, c);
+    const unsigned long long m = __ballot(f);
+    if (lane == 0) s_w[wave] = __popcll(m);
+    __syncthreads();
+    int o = s_base;
+    for (int w = 0; w < wave; w++) o += s_w[w];
+    if (f) cells[o + __popcll(m & ((1ull << lane) - 1ull))] = (int)c;
+    __syncthreads();
+    if (t == 0) s_base += s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    __syncthreads();
+  }
+}
+
+// the ascending fallback-cell list of nw records into list[1 ..], its length into list[0]; list holds nw + 1 +
+// kFbBlocks ints (the per-range counts after the list)
+static void enqueue_fbscan(const double* rec, long nw, int* list, hipStream_t st) {
+  int* bcnt = list + 1 + nw;
+  hipLaunchKernelGGL(k_fbcount, dim3(kFbBlocks), dim3(256), 0, st, rec, nw, bcnt);
+  hipLaunchKernelGGL(k_fbwrite, dim3(kFbBlocks), dim3(256), 0, st, rec, nw, (const int*)bcnt, list + 1, list);
 }
 
 struct ReduceArgs {
@@ -877,7 +910,7 @@ struct is3d_engine {
   double* d_chain = nullptr; long chain_cap = 0;   // PTMA warm-start chain segments (k_chain_pass)
   double *d_rec = nullptr, *d_aux = nullptr, *d_sol = nullptr, *d_renorm = nullptr, *d_slab = nullptr, *d_out = nullptr;
   long rec_cap = 0, aux_cap = 0, sol_cap = 0, renorm_cap = 0, slab_cap = 0, out_cap = 0;
-  int* d_fb = nullptr;        // modified modes: [0] fallback cell count, [1..] k_fbscan's cell list
+  int* d_fb = nullptr;        // modified modes: [0] fallback cell count, [1..] k_fbwrite's cell list
   long fb_cap = 0;
   double* d_phtab = nullptr;  // F_TS launches: k_phitab's per-(cell, pT, phi) rows of one chunk of cells
   long phtab_cap = 0;
@@ -1832,7 +1865,7 @@ static int integral_plan(is3d_engine* e, const SpectraPlan& P, long nw, Integral
   cps = ((cps + kTile - 1) / kTile) * kTile;
   nsplit = std::max(1L, (nw + cps - 1) / cps);
   I.P = P; I.ntask = ntask; I.bx = bx; I.wgs = wgs; I.nsplit = nsplit; I.cps = cps; I.sstride = sstride;
-  // modified modes: the F_FB launch (separable-fallback lanes, cells listed by k_fbscan) writes its own
+  // modified modes: the F_FB launch (separable-fallback lanes, cells listed by k_fbcount / k_fbwrite) writes its own
   // nsplit_fb slabs after the main ones; k_reduce sums both
   I.nsplit_fb = (mode >= PTM) ? std::max(1L, std::min(nsplit, 8L)) : 0;
   if (P.ts) ts_chunking(e, I);
@@ -1851,8 +1884,8 @@ static int enqueue_spectra(is3d_engine* e, const IntegralPlan& I, const double* 
   const int KJ = P.KJ, njb = P.njb, nc = e->ncls;
   const long nsplit = I.nsplit, cps = I.cps, wgs = I.wgs;
   if (mode >= PTM) {
-    if (!ensure(e->d_fb, e->fb_cap, nw + 1)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(fallback list) failed");
-    hipLaunchKernelGGL(k_fbscan, dim3(1), dim3(1024), 0, st, rec_w, nw, e->d_fb + 1, e->d_fb);
+    if (!ensure(e->d_fb, e->fb_cap, nw + 1 + kFbBlocks)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(fallback list) failed");
+    enqueue_fbscan(rec_w, nw, e->d_fb, st);
     HIPCHK(e, hipGetLastError());
   }
   SpecArgs sa{};
@@ -2319,11 +2352,11 @@ extern "C" int is3d_calculate_dN_dX(is3d_engine* e, double* dN_taudtaudy, double
     }
     HIPCHK(e, hipGetLastError());
     if (mode >= PTM) {
-      // the separable-fallback lanes of the cells k_fbscan lists (breakdown, narrow rapidity windows) in their own
+      // the separable-fallback lanes of the cells k_fbwrite lists (breakdown, narrow rapidity windows) in their own
       // launch (kernels.h k_dndx F_FB), added to ycell; the list's length stays on the device, so the grid is sized
       // for the whole surface and the workgroups split whatever the list holds
-      if (!ensure(e->d_fb, e->fb_cap, n + 1)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(fallback list) failed");
-      hipLaunchKernelGGL(k_fbscan, dim3(1), dim3(1024), 0, st, (const double*)e->d_rec, n, e->d_fb + 1, e->d_fb);
+      if (!ensure(e->d_fb, e->fb_cap, n + 1 + kFbBlocks)) return e->fail(IS3D_ERR_DEVICE, "hipMalloc(fallback list) failed");
+      enqueue_fbscan((const double*)e->d_rec, n, e->d_fb, st);
       DndxArgs fa = da;
       fa.fbcells = e->d_fb + 1; fa.fbcount = e->d_fb;
       fa.nchunk = std::max(1L, std::min(da.nchunk, (4096L + da.nbx - 1) / da.nbx));

@@ -103,7 +103,7 @@ struct SpecArgs {
   int regulate, outflow, dim;
   int op;                     // 1 spectra / 0 spacetime (yterms variants)
   const int* fbcells;         // F_FB launch: ascending indices of the cells with separable-fallback lanes
-  const int* fbcount;         //   (k_fbscan, device-side) and their number
+  const int* fbcount;         //   (k_fbcount / k_fbwrite, device-side) and their number
   int split0;                 // first cell split of this launch (F_TS launches cover the splits chunk by chunk)
   int slab0;                  // split whose slab `slab` points at (folded F_TS chunks: a chunk's own slab buffer)
   // F_TS: the per-(cell, pT, phi) tables k_phitab wrote for this chunk of cells, rows [pT][cell - phc0][phrow]
@@ -124,7 +124,7 @@ __device__ __forceinline__ bool gate_closed(const unsigned long long* gate, int 
 // lane builds its own y-term row in LDS and the modified lanes use their linear forms, no q-row tables
 // F_T8 (modified path): 8-cell tiles instead of IS3D_KTILE_MOD (q-row tables of many rows, config 1's shape)
 // F_FB (modified path): the separable-fallback launch -- only the lanes the modified launch leaves out (breakdown
-// cells, narrow rapidity windows), over the cells listed by k_fbscan, per-lane y-term rows as F_LY.  Keeping
+// cells, narrow rapidity windows), over the cells listed by k_fbwrite, per-lane y-term rows as F_LY.  Keeping
 // the separable code out of the modified launch takes its k_spectra from 241 to 164 VGPRs (3 waves per SIMD
 // instead of 2) and removes the 32-64 v_mov_b64 per lane and cell that merged two register assignments of acc
 // F_MP (Grad / RTA-CE with few lane tasks per pT: np x nq <= 128, e.g. pikp 2+1D = 72): a lane owns a whole
@@ -259,7 +259,7 @@ struct DndxArgs {
   long cells_per_wg, nchunk;
   int dim;
   const int* fbcells;         // F_FB launch (modified modes): ascending indices of the cells with separable-fallback
-  const int* fbcount;         //   lanes (k_fbscan) and their number; the launch adds those lanes' sums to ycell
+  const int* fbcount;         //   lanes (k_fbwrite) and their number; the launch adds those lanes' sums to ycell
 };
 
 // k_phitab: the F_TS tables of one chunk of cells (every pT), rows [pT][cell - c0][phitab_row]
@@ -1148,7 +1148,7 @@ __device__ __forceinline__ double mod_phi_wsum(const ModLane& M, const dbl2* CS,
 // species' slot columns are summed in slot order.  No atomics: bit-reproducible.
 // Modified modes (PTM / PTB) run two launches, as k_spectra does: the main one integrates the modified lanes only
 // and writes ycell, the F_FB one integrates the separable-fallback lanes (breakdown cells, narrow rapidity windows:
-// MomentumSpectra.cpp:863-929) of the cells k_fbscan lists and adds them to ycell.  With both in one kernel the
+// MomentumSpectra.cpp:863-929) of the cells k_fbwrite lists and adds them to ycell.  With both in one kernel the
 // PTM / PTB instances spilled 147 VGPRs at 2 waves per SIMD (5.6e11 B of scratch traffic per config-2 pass).
 template <int MODE, int FLAGS, int KJ>
 __global__ __launch_bounds__(kBlock, (dndx_waves_f<MODE, FLAGS>())) void k_dndx(DndxArgs A) {
