@@ -183,3 +183,26 @@ def test_group_launch_is_asynchronous():
     assert still_busy
     # two shard sums + their sum: near-cancelling SMASH entries move by rounding (test_gpu_group.py: 6.5e-12)
     assert parity(got, ref)[0] < 1e-10
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_chunked_plan_with_slow_cells(mode):
+    """A surface with lanes off the fast path (mu_B / T = 375 in half the cells, through a stretched mu_B axis) and
+    the F_TS tables forced into chunks: the device-side gate runs the slow-loop fallback plan, whose cell splits are
+    capped to the folded F_TS plan's slab footprint (engine.hip launch_end), instead of the folded chunks."""
+    s = synth.as_read(synth.surface(96, seed=29, dimension=3, baryon=True, full3d=True))
+    hot = np.arange(96) % 2 == 0
+    s["T"] = np.where(hot, 0.12, s["T"])
+    s["muB"] = np.where(hot, 45.0, s["muB"])
+    spec = make_spec(hrg_eos=2, chosen="smash", df_mode=mode, dimension=3, pT="pT24", phi="phi32", y="y21",
+                     include_baryon=1)
+    T, muB, tab = spec["df"]
+    spec["df"] = (T, np.asarray(muB) * 100.0, tab)
+    info = {}
+    got, nk = run(spec, s, {"phitab_one_bytes": 0, "phitab_chunk_bytes": 1}, info=info)
+    assert nk >= 3, nk
+    ref = O.spectra(spec, s, threads=8)
+    rel, zr, zg = parity(got, ref)
+    assert rel < TOL, (rel, zr, zg)
+    assert rel_quantile(got, ref) < P99
+    assert zr == zg

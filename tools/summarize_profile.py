@@ -94,13 +94,12 @@ def main():
     meta = out.pop("_meta")
     # the dominant k_spectra kernel (the modified modes also run the short F_FB fallback launch); an F_TS launch
     # over a surface whose tables exceed one chunk runs it several times per pass (engine.hip): per-pass totals =
-    # per-launch averages x launches per pass, passes = the reduction launches (one per pass)
-    # (operation 0: k_dndx, one launch per pass)
+    # per-launch averages x launches per pass, passes = the record prepass launches (k_prep, one per pass: since
+    # round 5 a Grad / RTA-CE pass also enqueues the gated fallback plan's k_spectra / k_reduce, which return at once)
+    # (operation 0: k_dndx, its main launch once per pass beside the F_FB one)
     dom = "k_dndx" if any(k.startswith("k_dndx") for k in out) else "k_spectra"
     spec = sorted((k for k in out if k.startswith(dom)), key=lambda k: -out[k].get("avg_ns_pmc_pass", 0.0))
-    passes = sum(out[k].get("launches", 0) for k in out if k.startswith("k_reduce"))
-    if dom == "k_dndx":
-        passes = sum(out[k].get("launches", 0) for k in out if k.startswith("k_dndx"))
+    passes = sum(out[k].get("launches", 0) for k in out if k.startswith("k_prep"))
     key = "%s_mode%d" % (config, mode)
     lpp = 1.0
     if spec and passes:
