@@ -1,7 +1,8 @@
 """GPU tier: integrand classes (is3d_set_species_classes, include/is3d_amd.h).
 
-The momentum integrals see a chosen species only through its (mass, sign, baryon) -- plus its degeneracy in
-PTM, whose n_linear / n_mod renormalisation carries it (MomentumSpectra.cpp:800-808) -- and the degeneracy
+The momentum integrals see a chosen species only through its (mass, sign, baryon) -- plus, in PTM, whether its
+degeneracy is zero: the n_linear / n_mod renormalisation (MomentumSpectra.cpp:800-808) is a ratio of two sums that
+both carry g, except for g = 0 (0 / 0: the species is skipped) -- and the degeneracy
 multiplies the result (MomentumSpectra.cpp:365).  The engine therefore integrates one lane species per class
 (SMASH 444 -> 193, UrQMD 305 -> 124) and its reduction writes every member.  These tests check that the
 spectra, dN/dX and per-cell yields are bit-identical to the per-species integration (classes off) wherever
@@ -126,3 +127,26 @@ def test_classes_device_group():
     ref = O.spectra(spec, s, threads=8)
     assert parity(got, ref, floor=1e-290)[0] < 1e-8
     assert parity(off, ref, floor=1e-290)[0] < 1e-8
+
+
+def test_ptm_classes_ignore_the_degeneracy_except_zero():
+    """PTM's classes key on g == 0 only (engine.hip ptm_gkey): SMASH species that differ only in g share a class,
+    and a species given g = 0 keeps its own (its renormalisation is 0 / 0 = NaN, so the reference skips it and its
+    spectrum stays 0) -- against the oracle, which evaluates every species with its own g."""
+    s = synth.as_read(synth.surface(12, seed=61, dimension=3, full3d=True))
+    spec = make_spec(hrg_eos=2, chosen="smash", df_mode=3, dimension=3, pT="pT24", phi="phi32", y="y21")
+    sp = dict(spec["species"])
+    g = np.array(sp["degen"], dtype=float)
+    z = int(np.argmax(np.array(sp["mass"]) > 1.0))      # the first species above 1 GeV
+    g[z] = 0.0
+    sp["degen"] = g
+    spec = dict(spec, species=sp)
+    out, n_on, _ = spectra(spec, s, True)
+    key = set(zip(sp["mass"], sp["sign"], sp["baryon"], [v == 0 for v in g]))
+    assert n_on == len(key)
+    ref = O.spectra(spec, s, threads=8)
+    rel, zr, zg = parity(out, ref)
+    assert rel < 1e-8, (rel, zr, zg)
+    assert zr == zg
+    nph = out.size // len(g)
+    assert not np.any(out.reshape(len(g), nph)[z])      # the g = 0 species: skipped, all zero
