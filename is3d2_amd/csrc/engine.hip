@@ -1338,8 +1338,11 @@ static SpectraPlan spectra_plan(const is3d_engine* e, bool allow_ts = true) {
   P.ts = ts_ok() ? F_TS : 0;
   P.by = (P.ts && e->p.include_baryon) ? F_BY : 0;
   if (P.ts && kTile != IS3D_KTILE_TS) {     // spectra_tile<MODE, F_TB | F_TS>()
+    const int t = kTile;
     kTile = IS3D_KTILE_TS;
-    P.shmem = lds_bytes(P.nqmax);
+    const size_t sm = lds_bytes(P.nqmax);
+    if (sm <= IS3D_LDS_QROW_LIMIT) P.shmem = sm;
+    else { kTile = t; P.ts = 0; P.by = 0; }     // the larger tile's T1 rows do not fit: the F_TB launch
   }
   P.tile = kTile;
   if (mode >= PTM) {

@@ -23,7 +23,11 @@ constexpr int kTile = IS3D_KTILE;   // cells per LDS tile
 // r2t; the modified path's F_T8 and F_LY launches keep 8 where 16 cells' q-row tables would not fit:
 // config 1's shape in F_LY ran 11.2 ms with 8-cell tiles, 13.6 ms with 16)
 #ifndef IS3D_KTILE_TS
-#define IS3D_KTILE_TS 8       // F_TS launches (LDS: records, y-terms and T1 rows only)
+#define IS3D_KTILE_TS 12      // F_TS launches (LDS: records, y-terms and T1 rows only). Each k_phitab row a
+                              // wave reads through the scalar cache serves the tile's cells: config 2 Grad
+                              // 155.5 ms at 8 cells, 154.2 at 10, 151.5 at 12 and 14, 188.5 at 16 (LDS
+                              // occupancy); RTA-CE 241.6 / 239.0 / 237.8 / 240.3; config 4 flat at 8-14
+                              // (profiles/round5_r5h_ab_ts_tile.log)
 #endif
 template <int MODE, int FLAGS>
 constexpr int spectra_tile() {
