@@ -1338,11 +1338,10 @@ static SpectraPlan spectra_plan(const is3d_engine* e, bool allow_ts = true) {
   P.ts = ts_ok() ? F_TS : 0;
   P.by = (P.ts && e->p.include_baryon) ? F_BY : 0;
   if (P.ts && kTile != IS3D_KTILE_TS) {     // spectra_tile<MODE, F_TB | F_TS>()
-    const int t = kTile;
     kTile = IS3D_KTILE_TS;
-    const size_t sm = lds_bytes(P.nqmax);
-    if (sm <= IS3D_LDS_QROW_LIMIT) P.shmem = sm;
-    else { kTile = t; P.ts = 0; P.by = 0; }     // the larger tile's T1 rows do not fit: the F_TB launch
+    P.shmem = lds_bytes(P.nqmax);
+    // the F_TS tile's LDS past the limit (a y / eta grid of thousands of nodes): the plan without F_TS
+    if (P.shmem > IS3D_LDS_QROW_LIMIT) return spectra_plan(e, false);
   }
   P.tile = kTile;
   if (mode >= PTM) {

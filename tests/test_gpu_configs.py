@@ -106,12 +106,13 @@ def test_config5_miniature():
     check(spec, s)
 
 
-@pytest.mark.parametrize("nsp", [80, 90, 110, 127])
+@pytest.mark.parametrize("nsp", [190, 195, 260, 320])
 @pytest.mark.parametrize("mode", [1, 2])
 def test_table_launch_q_rows(nsp, mode):
-    # k_spectra's F_TB launch sizes its y-term / {PD, T1} LDS rows for kTbQ = 4 q values per workgroup,
-    # which holds when (256 - 1) / nsp + 2 <= 4, i.e. nsp >= 86: 90 / 110 / 127 species put 3 or 4 q rows
-    # in one workgroup; 80 species must take the per-lane (non-table) launch
+    # k_spectra's F_TB / F_TS launches size their y-term / T1 LDS rows for kTbQ = 4 q values per workgroup,
+    # which holds when (256 - 1) / ncls + 2 <= 4 over the lanes' integrand classes, i.e. ncls >= 86: the first
+    # 195 / 260 / 320 SMASH species are 86 / 114 / 130 classes (4, 4 and 3 q rows per workgroup); 190 species
+    # (85 classes, 5 rows) must take the per-lane (non-table) launch
     s = synth.as_read(synth.surface(8, seed=37, dimension=3, full3d=True))
     mcids = hrg.chosen_mcids("smash")[:nsp]
     spec = make_spec(hrg_eos=2, chosen=mcids, df_mode=mode, dimension=3, pT="pT24", phi="phi32", y="y21")

@@ -14,7 +14,7 @@ import numpy as np
 import pytest
 
 from helpers import parity, rel_quantile
-from is3d2_amd import build_engine, make_spec, synth
+from is3d2_amd import build_engine, hrg, make_spec, synth
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -234,4 +234,28 @@ def test_split_knobs_change_only_the_summation_order(mode):
     rel, zr, zg = parity(few, ref)
     assert rel < TOL, (rel, zr, zg)
     assert rel_quantile(few, ref) < P99
+    assert zr == zg
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_scalar_table_tile_past_the_lds_limit(mode):
+    """F_TS launches take 12-cell record tiles (kernels.h IS3D_KTILE_TS).  A y grid of thousands of nodes (LDS holds
+    it beside the records, y-terms and T1 rows) puts that tile past IS3D_LDS_QROW_LIMIT -- 6001 nodes: 86 KB at 12
+    cells, 74 KB at 8 -- and the plan is then made without F_TS (engine.hip spectra_plan) instead of launching a
+    kernel sized for a smaller tile.  320 SMASH species (130 classes: 3 q rows per workgroup, the table shape), one
+    pT x 24 phi: the 21-node grid runs the scalar-table launch, the 6001-node one does not, and its spectra meet
+    the oracle."""
+    s = synth.as_read(synth.surface(2, seed=43, dimension=3, full3d=True))
+    spec = make_spec(hrg_eos=2, chosen=hrg.chosen_mcids("smash")[:320], df_mode=mode, dimension=3, pT="pT24",
+                     phi="phi24", y="y21")
+    spec["pT"], spec["pT_w"] = spec["pT"][5:6].copy(), spec["pT_w"][5:6].copy()
+    _, n21 = run(spec, s)
+    assert n21 == 1, n21
+    spec["y"] = np.linspace(-8.0, 8.0, 6001)
+    got, n = run(spec, s)
+    assert n == 0, n
+    ref = O.spectra(spec, s, threads=8)
+    rel, zr, zg = parity(got, ref)
+    assert rel < TOL, (rel, zr, zg)
+    assert rel_quantile(got, ref) < P99
     assert zr == zg
