@@ -213,7 +213,16 @@ __host__ __device__ constexpr int phitab_row(int mode, int nphp, bool by = false
 #define IS3D_TAIL_DNDX 1      // operation 0 (k_dndx): Boltzmann-tail Grad lanes in pairs (sep_pair_tail_t)
 #endif
 #ifndef IS3D_TS_PF
-#define IS3D_TS_PF 1          // F_TS: the table rows of tile i + 2 are touched into L2 (LDS-DMA of one dword per 128 B)
+#define IS3D_TS_PF 1          // F_TS: the table rows of tile i + PFD are touched into L2 (LDS-DMA of one dword per 128 B)
+#endif
+// F_TS prefetch distance in tiles (Grad / RTA-CE): one tile of lane work covers the HBM latency, and the nearer tile
+// keeps fewer rows in L2 (12-cell tiles, distance 1 vs 2: config 2 Grad 152.4 / 152.7 ms, RTA-CE 239.4 / 240.6,
+// config 3 RTA-CE 258.4 / 261.5, config 4 2399 / 2435; 3 slower still; profiles/round5_r5j_ab_ts_prefetch.log)
+#ifndef IS3D_TS_PF_DIST_GRAD
+#define IS3D_TS_PF_DIST_GRAD 1
+#endif
+#ifndef IS3D_TS_PF_DIST_CE
+#define IS3D_TS_PF_DIST_CE 1
 #endif
 // F_TS: the operands of the next four loaded before this four's arithmetic (bit 1 tail lanes, bit 2 other
 // lanes), per mode: RTA-CE 260.8 -> 250.8 ms (config 2), 2663 -> 2511 ms (config 4); Grad 167.5 -> 168.9 ms (r4d)
@@ -929,13 +938,14 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
     const int ntx = tile_nt(i), tb = PIPE ? (i & 1) : 0;
     wait_fetch();
     lds_barrier();     // X: this tile's records (and, pipelined, its A / B tables) visible; the last tile is done
-    if (i + kRecBufs - 1 < ntiles) {
-      fetch_tile<kTile>(A.rec, tile_cb(i + kRecBufs - 1), c_end, recbuf(i + kRecBufs - 1), fbl);
+    if (i + kRecBufs - 1 < ntiles) fetch_tile<kTile>(A.rec, tile_cb(i + kRecBufs - 1), c_end, recbuf(i + kRecBufs - 1), fbl);
+    constexpr int PFD = (MODE == GRAD) ? IS3D_TS_PF_DIST_GRAD : IS3D_TS_PF_DIST_CE;
+    if (i + PFD < ntiles) {
       if constexpr (TS && IS3D_TS_PF) {
-        // the k_phitab rows of that tile (contiguous: cells x RW doubles of this pT) into L2, so the scalar loads of
+        // the k_phitab rows of tile i + PFD (contiguous: cells x RW doubles of this pT) into L2, so the scalar loads of
         // its first points miss the K$ into L2 instead of HBM; one dword per 128-byte line, landing in a dummy LDS row
         constexpr int RW = phitab_row(MODE, KJ, (FLAGS & F_BY) != 0);
-        const long cbp = tile_cb(i + kRecBufs - 1);
+        const long cbp = tile_cb(i + PFD);
         const long nb = (min(c_end, cbp + kTile) - cbp) * RW * 8;
         const char* src = (const char*)(A.phtab + ((long)ipt * A.phn + (cbp - A.phc0)) * RW);
         double* pfd = s_t1 + (long)kTile * nqm * prow2;
