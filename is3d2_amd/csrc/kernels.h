@@ -229,8 +229,13 @@ __host__ __device__ constexpr int phitab_row(int mode, int nphp, bool by = false
 #ifndef IS3D_TS_AHEAD_CE
 #define IS3D_TS_AHEAD_CE 1
 #endif
+// Grad without baryon terms ahead on every four since round 5 (12-cell tiles, prefetch distance 1: config 2 Grad
+// 151.9 -> 150.6 ms; the same for RTA-CE and F_BY Grad lost 1-4%: profiles/round5_r5k_ab_tiles_ahead.log)
 #ifndef IS3D_TS_AHEAD_GRAD
-#define IS3D_TS_AHEAD_GRAD 1
+#define IS3D_TS_AHEAD_GRAD 3
+#endif
+#ifndef IS3D_TS_AHEAD_GRAD_BY
+#define IS3D_TS_AHEAD_GRAD_BY 1
 #endif
 #ifndef IS3D_TS_SLOW
 #define IS3D_TS_SLOW 0        // F_TS kernels with the slow-path loop (0: such surfaces take F_TB, sep_slow_cell)
@@ -496,7 +501,8 @@ __device__ __forceinline__ void sep_phi_loop_ts(const SepLane& L, double mT, dou
     }
     f.pt[0].y = t01.x; f.pt[1].y = t01.y; f.pt[2].y = t23.x; f.pt[3].y = t23.y;
   };
-  constexpr bool AHEAD = (((MODE == GRAD) ? IS3D_TS_AHEAD_GRAD : IS3D_TS_AHEAD_CE) >> (TAIL || NEAR ? 0 : 1)) & 1;
+  constexpr int AH = (MODE == GRAD) ? (BY ? IS3D_TS_AHEAD_GRAD_BY : IS3D_TS_AHEAD_GRAD) : IS3D_TS_AHEAD_CE;
+  constexpr bool AHEAD = (AH >> (TAIL || NEAR ? 0 : 1)) & 1;
   Four fq[2];
   if (AHEAD) load(0, fq[0]);
 #pragma unroll
