@@ -74,6 +74,12 @@ constexpr int dndx_waves() { return (MODE == CE || MODE >= PTM) ? 2 : spectra_wa
 #define IS3D_DNDX_MOD_UNROLL 2     // k_dndx modified lanes: phi pairs per loop trip (fully unrolled, 16 at 32 points, the
                                    // PTM / PTB launch held 256 VGPRs + 95 spilled; two: 129 VGPRs, 3 waves per SIMD)
 #endif
+#ifndef IS3D_DNDX_QUAD
+#define IS3D_DNDX_QUAD 1           // k_dndx lanes in fours (one reciprocal per four points; modified lanes: staged exp).
+                                   // Config 2 operation 0 against pairs: Grad 345 -> 322 ms (168 VGPRs with 15-37
+                                   // spilled -> 124), RTA-CE 506 -> 480, PTM 834 -> 741, PTB 732 -> 660 ms
+                                   // (profiles/round5_r5m_ab_dndx_quad.log)
+#endif
 template <int MODE, int FLAGS>
 constexpr int dndx_waves_f() { return (MODE >= PTM && !(FLAGS & 32)) ? IS3D_DNDX_WAVES_MOD : dndx_waves<MODE>(); }
 
@@ -1101,6 +1107,19 @@ __device__ __forceinline__ double sep_phi_wsum(const SepLane& L, const dbl2* CS,
   constexpr int FL = (MODE == GRAD) ? SEP_GRAD : (MODE == CE || MODE == PTM) ? SEP_CE : (MODE == PTB) ? SEP_PTB : SEP_FEQ;
   constexpr bool REG = (FLAGS & F_REG) != 0, OUT = (FLAGS & F_OUT) != 0;
   double a0 = 0.0, a1 = 0.0;
+  if constexpr (FAST && IS3D_PAIR_RCP && IS3D_DNDX_QUAD && KJ % 4 == 0) {
+    // fours with one reciprocal (sep_quad_t, as k_spectra's lane-form launches)
+#pragma unroll
+    for (int jj = 0; jj < KJ; jj += 4) {
+      const dbl2 c[4] = {CS[jj], CS[jj + 1], CS[jj + 2], CS[jj + 3]}, b[4] = {BP[jj], BP[jj + 1], BP[jj + 2], BP[jj + 3]};
+      const dbl2 wa = W[jj >> 1], wb = W[(jj >> 1) + 1];
+      double v[4];
+      sep_quad_t<FL, REG, OUT>(L, c, b, v);
+      a0 = fma(wa.x, v[0], a0); a1 = fma(wa.y, v[1], a1);
+      a0 = fma(wb.x, v[2], a0); a1 = fma(wb.y, v[3], a1);
+    }
+    return a0 + a1;
+  }
   if (FAST && IS3D_PAIR_RCP) {
     dbl2 c0 = CS[0], b0 = BP[0], c1 = CS[1], b1 = BP[1];
 #pragma unroll
@@ -1144,6 +1163,30 @@ template <int FLAGS, bool CLAMP, int KJ>
 __device__ __forceinline__ double mod_phi_wsum(const ModLane& M, const dbl2* CS, const dbl2* QV, const dbl2* W) {
   constexpr bool OUT = (FLAGS & F_OUT) != 0;
   double a0 = 0.0, a1 = 0.0;
+  if constexpr (IS3D_DNDX_QUAD && KJ % 4 == 0) {
+    // fours: the staged table exp of mod_nq4 (four LDS reads per wait) and one reciprocal per four points
+#pragma unroll IS3D_DNDX_MOD_UNROLL
+    for (int jj = 0; jj < KJ; jj += 4) {
+      const dbl2 c[4] = {CS[jj], CS[jj + 1], CS[jj + 2], CS[jj + 3]};
+      const dbl2 qa = QV[jj >> 1], qb = QV[(jj >> 1) + 1], wa = W[jj >> 1], wb = W[(jj >> 1) + 1];
+      const double qv[4] = {qa.x, qa.y, qb.x, qb.y};
+      double X[4], num[4], q[4], rq[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) X[i] = fma(M.Ec, c[i].x, fma(M.Es, c[i].y, M.E0 + qv[i]));
+      mod_nq4<CLAMP>(M, X, num, q);
+      mod_quad_rq(q, rq);
+      double v[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const double pds = lin(M.D0, M.Dc, M.Ds, c[i]);
+        const double g = pds * (num[i] * rq[i]);
+        v[i] = (OUT && pds <= 0.0) ? 0.0 : g;
+      }
+      a0 = fma(wa.x, v[0], a0); a1 = fma(wa.y, v[1], a1);
+      a0 = fma(wb.x, v[2], a0); a1 = fma(wb.y, v[3], a1);
+    }
+    return a0 + a1;
+  }
   dbl2 c0 = CS[0], c1 = CS[1], q = QV[0];
 #pragma unroll IS3D_DNDX_MOD_UNROLL
   for (int jj = 0; jj < KJ; jj += 2) {
