@@ -13,6 +13,11 @@ owns its own 10^5-cell shard of an N x 10^5-cell surface; the per-rank spectra a
 summed with one RCCL all-reduce (torch.distributed 'nccl' = RCCL over xGMI).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config config2] [--df-mode 1..5]
+
+Ranks: under a launcher (torch.distributed.run sets WORLD_SIZE / RANK / LOCAL_RANK) the world comes from the
+environment and --gpus must agree with it; a plain `python bench.py --gpus N` with N > 1 starts the N rank
+processes itself (spawn_ranks: fresh interpreters with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, started
+before anything touches the GPU) and exits with the first failing rank's status.
 """
 import argparse
 import json
@@ -48,6 +53,62 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def spawn_ranks(n, argv):
+    """`bench.py --gpus N` without a launcher: run N rank processes of this script (rank r on GPU r, rendezvous on
+    127.0.0.1) and return the exit status -- 0, or the first failing rank's (the other ranks are then terminated,
+    so a rank stuck in a collective cannot hang the run).  Called before torch is imported: the parent never
+    touches the GPU and never replaces itself (no exec)."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), IS3D_BENCH_LAUNCHER="bench.py --gpus")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    try:
+        while any(p.poll() is None for p in procs):
+            bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+            if bad:
+                rc = bad[0]
+                break
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signal.SIGTERM)
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    if rc == 0:
+        rc = next((p.returncode for p in procs if p.returncode != 0), 0)
+    if rc:
+        log("bench.py: a rank exited with status %s" % rc)
+    return 1 if rc < 0 else rc
+
+
+def resolve_world(gpus, environ):
+    """(world, spawn) from --gpus and the launcher's environment.  Under a launcher WORLD_SIZE decides and a
+    different --gpus is an error (a SCALE run must never time fewer ranks than it names); without one, --gpus N
+    (default 1) ranks, spawned by this script when N > 1."""
+    if environ.get("WORLD_SIZE"):
+        world = int(environ["WORLD_SIZE"])
+        if gpus is not None and gpus != world:
+            raise SystemExit("bench.py: --gpus %d but the launcher started WORLD_SIZE=%d ranks" % (gpus, world))
+        return world, False
+    n = 1 if gpus is None else gpus
+    if n < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    return n, n > 1
+
+
 def make_surface(cfg, rank, world, dim, baryon, whole=False):
     """This rank's cells: weak scaling -- its own surface (seed 7 + rank); strong scaling -- its cost-balanced
     contiguous range of the one surface (dist.shard_bounds), or the whole surface (whole=True, PTMA warm-start
@@ -81,6 +142,9 @@ def _host_cpu():
     return model, os.cpu_count() or 1, len(os.sched_getaffinity(0)), quota
 
 
+_NATIVE_ORACLE = {}     # the -march=native oracle built on this host by the first CPU leg (compiler line)
+
+
 def cpu_baseline(spec, surf, units_per_cell, n_full, target_s=25.0, operation=1):
     """Oracle (a C/OpenMP 'port' of the reference loop, oracle/Makefile flags) on the host cores, on a
     cell prefix of the same workload sized to >= target_s, extrapolated linearly to the full shard
@@ -91,7 +155,7 @@ def cpu_baseline(spec, surf, units_per_cell, n_full, target_s=25.0, operation=1)
     import tempfile
     # -O3 -fopenmp -march=native, built here on the box's own host (a -march=native binary cannot
     # ship from the build container); the portable in-tree build if no compiler is at hand
-    compiler = None
+    compiler = _NATIVE_ORACLE.get("compiler")
     if not os.environ.get("IS3D_ORACLE_LIB"):
         out = os.path.join(tempfile.gettempdir(), "is3d_oracle_native_%d.so" % os.getpid())
         try:
@@ -100,6 +164,7 @@ def cpu_baseline(spec, surf, units_per_cell, n_full, target_s=25.0, operation=1)
             if r.returncode == 0 and os.path.exists(out):
                 os.environ["IS3D_ORACLE_LIB"] = out
                 compiler = r.stdout.strip().splitlines()[-1] + " (built on this host)"
+                _NATIVE_ORACLE["compiler"] = compiler
         except (OSError, subprocess.SubprocessError):
             pass
     from oracle import oracle as O
@@ -270,7 +335,14 @@ def run_workload(args, cfg_name, mode, steps, warmup, rank, world, local_rank, d
                 dist.all_reduce(binned)
             return eng.stats()
         if qrange is not None:
-            D.launch_chained(eng, out.data_ptr(), stream, rank, world, dist, device=dev)
+            if args.backend == "nccl":
+                # boundary states in HBM; copies, sends and receives ordered on the launch stream
+                D.launch_chained(eng, out.data_ptr(), stream, rank, world, dist, device=dev)
+            else:
+                # gloo's transport is the host: host boundary buffers, and the launch stream synchronised after each
+                # copy out of the engine so a send never reads a buffer before the copy has landed
+                D.launch_chained(eng, out.data_ptr(), stream, rank, world, dist, device=None,
+                                 sync=torch.cuda.current_stream(dev).synchronize)
         else:
             eng.launch(out.data_ptr(), stream)
         if world > 1:
@@ -305,28 +377,45 @@ def run_workload(args, cfg_name, mode, steps, warmup, rank, world, local_rank, d
     kernel = "k_spectra" if operation == 1 else "k_dndx"
     sub = argparse.Namespace(config=cfg_name, operation=operation, cells=args.cells if cfg_name == args.config else 0)
     roofline = executed_roofline(sub, mode, ms_spectra, ms_total, neta, units_local, n_local, outsize, kernel)
+    extras = []
+    if flags.get("include_baryon"):
+        extras.append("baryon on" + (" + baryon diffusion delta-f" if flags.get("include_baryondiff_deltaf") else ""))
+    if cfg.get("gla", 32) != 32:
+        extras.append("%d-pt Gauss-Laguerre" % cfg["gla"])
+    if mode == 5 and spec["params"]["famod_chains"] > 0:
+        extras.append("%d warm-start Newton chain%s" % (spec["params"]["famod_chains"],
+                                                       "" if spec["params"]["famod_chains"] == 1 else "s"))
+    backend_name = {"nccl": "RCCL"}.get(args.backend, args.backend)
     config = {
-        "workload": "%s%s: %s %s synthetic freeze-out cells%s x %s HRG (%d species) x %s delta-f, %d pT x %d phi x %d y%s"
+        "workload": "%s%s: %s %s synthetic freeze-out cells%s x %s HRG (%d species) x %s delta-f%s, %d pT x %d phi x %d y%s"
                     % (cfg_name, " operation 0 (dN/dX)" if operation == 0 else "", cfg["cells"],
                        "3+1D" if cfg["dim"] == 3 else "2+1D", " per GPU" if cfg["scaling"] == "weak" else " total",
-                       "SMASH" if cfg["hrg"] == 2 else "UrQMD", nsp, MODE_NAMES[mode], npT, nphi, ny,
-                       "" if neta == 1 else " x %d eta" % neta),
+                       "SMASH" if cfg["hrg"] == 2 else "UrQMD", nsp, MODE_NAMES[mode],
+                       "".join(" (%s)" % e for e in extras[:1]) + "".join(", %s" % e for e in extras[1:]),
+                       npT, nphi, ny, "" if neta == 1 else " x %d eta" % neta),
         "operation": operation,
         "cells_per_gpu": n_local, "species": nsp, "grid": [npT, nphi, ny, neta], "df_mode": mode,
         "species_integrated": n_integrated,
         "famod_chains": spec["params"]["famod_chains"] if mode == 5 else None,
         "cell_splits": nsplit if operation == 1 else None,
-        "parallelism": ("dp%d (cell shards + RCCL all-reduce of spectra%s)"
-                        % (world, "; PTMA chain positions split, boundary states sent rank to rank per pass" if chained else "")
+        "parallelism": ("dp%d (cell shards + %s all-reduce of spectra%s)"
+                        % (world, backend_name,
+                           "; PTMA chain positions split, boundary states sent rank to rank per pass" if chained else "")
                         if world > 1 else "1 GPU"),
     }
+    if world > 1:
+        config["backend"] = args.backend
+        config["launcher"] = os.environ.get("IS3D_BENCH_LAUNCHER", "external (WORLD_SIZE from the environment)")
+        if os.environ.get("IS3D_BENCH_DEVICE") is not None:
+            config["rehearsal"] = "every rank on device %s (IS3D_BENCH_DEVICE)" % os.environ["IS3D_BENCH_DEVICE"]
     return dict(value=total_units / elapsed, elapsed=elapsed, steps=steps, warmup=warmup, cfg=cfg, config=config,
                 roofline=roofline, spec=spec, surf=surf, units_per_cell=units_per_cell, n_local=n_local)
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); default 1, or WORLD_SIZE under a launcher (which must then agree)")
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="config2", choices=sorted(CONFIGS))
@@ -344,19 +433,26 @@ def main():
     ap.add_argument("--north-star-steps", type=int, default=3,
                     help="timed passes of the north_star workload (config4: 10^6 3+1D cells, SMASH, RTA-CE, "
                          "sharded over the ranks) reported beside the main line; 0 skips it")
+    ap.add_argument("--north-star-cpu-seconds", type=float, default=20.0,
+                    help="CPU-leg sample length of the north_star workload (rank 0, N = 1); 0 skips that leg")
     args = ap.parse_args()
 
+    world, spawn = resolve_world(args.gpus, os.environ)
+    if spawn:
+        sys.exit(spawn_ranks(world, sys.argv[1:]))
     rank = int(os.environ.get("RANK", 0))
-    world = int(os.environ.get("WORLD_SIZE", 1))
     local_rank = int(os.environ.get("LOCAL_RANK", 0))
 
     import torch
     import torch.distributed as dist
     # rehearsal knobs for a 1-GPU box (never set by the driver): every rank on one device, gloo
-    backend = os.environ.get("IS3D_BENCH_BACKEND", "nccl")
+    args.backend = os.environ.get("IS3D_BENCH_BACKEND", "nccl") if world > 1 else "none"
     local_rank = int(os.environ.get("IS3D_BENCH_DEVICE", local_rank))
+    ndev = torch.cuda.device_count()
+    if local_rank >= ndev:
+        raise SystemExit("bench.py: rank %d needs GPU %d but %d GPU(s) are visible" % (rank, local_rank, ndev))
     if world > 1:
-        dist.init_process_group(backend, init_method="env://")
+        dist.init_process_group(args.backend, init_method="env://")
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
 
@@ -365,15 +461,15 @@ def main():
     m = run_workload(args, args.config, args.df_mode, args.steps, args.warmup, rank, world, local_rank, dev, dist)
     per_species = None
     if not args.no_per_species and m["config"]["species_integrated"] < m["config"]["species"]:
-        # the same workload with one integral per species (integrand classes off): bit-identical spectra, the
-        # kernel's per-species rate (tests/test_gpu_classes.py)
+        # the same workload with one integral per species (integrand classes off): the same spectra to rounding
+        # (< 1e-9, tests/test_gpu_classes.py), the kernel's per-species rate
         o = run_workload(args, args.config, args.df_mode, args.steps, 1, rank, world, local_rank, dev, dist,
                          classes=False)
         per_species = {"value": o["value"], "ms_per_step": 1e3 * o["elapsed"] / o["steps"], "steps": o["steps"],
                        "species_integrated": o["config"]["species_integrated"],
                        "kernel_ms": o["roofline"]["kernel_ms"],
                        "note": "same workload and clock rules with integrand classes off (is3d_set_species_classes(e, 0)): "
-                               "every species integrated separately; the same spectra (bit for bit at the BASELINE sizes, tests/test_gpu_classes.py)"}
+                               "every species integrated separately; equal to rounding (< 1e-9), tests/test_gpu_classes.py"}
     ns = None
     if args.north_star_steps > 0 and args.config != "config4" and args.operation == 1:
         n = run_workload(args, "config4", 0, args.north_star_steps, 1, rank, world, local_rank, dev, dist)
@@ -382,6 +478,14 @@ def main():
               "ms_per_step": 1e3 * n["elapsed"] / n["steps"], "scaling": n["cfg"]["scaling"], "config": n["config"],
               "roofline": n["roofline"],
               "note": "north_star target workload (BASELINE config 4) timed in this same run, same clock rules"}
+        if rank == 0 and world == 1 and not args.no_cpu_baseline and args.north_star_cpu_seconds > 0:
+            # north_star: ">= 10x the reference OpenMP continuous-spectra path on a 10^6-cell synthetic surface", the
+            # CPU timed on this box's host cores in the same run -- the oracle (MomentumSpectra.cpp:32-415, df_mode 2)
+            # on a cell prefix of the same 10^6-cell surface, extrapolated to the whole surface
+            cb = cpu_baseline(n["spec"], n["surf"], n["units_per_cell"], n["n_local"], args.north_star_cpu_seconds, 1)
+            cb["speedup"] = n["value"] / cb["value"]
+            cb["gpu_s_per_pass"] = n["elapsed"] / n["steps"]
+            ns["cpu_baseline"] = cb
     if rank == 0:
         res = {
             "metric": "freezeout-cell-species-mom-points/sec",

@@ -642,7 +642,9 @@ __global__ __launch_bounds__(256) void k_reduce_wave(ReduceArgs A) {
 // Chunk-wise slab fold (folded F_TS launches, enqueue_spectra): acc[i] = (init ? 0 : acc[i]) + src[0][i] + ... +
 // src[ns - 1][i], added in split order, so the folded accumulator equals k_reduce's sequential sum over all splits
 // bit for bit (3+1D: one term per split and output).  Memory-bound: ns + 2 doubles per entry.
-__global__ __launch_bounds__(256) void k_fold(double* acc, const double* src, long sstride, int ns, int init) {
+__global__ __launch_bounds__(256) void k_fold(double* acc, const double* src, long sstride, int ns, int init,
+                                              const unsigned long long* gate, int gate_want) {
+  if (gate_closed(gate, gate_want)) return;      // the other plan of a gated pair runs (launch_end)
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < sstride; i += (long)gridDim.x * blockDim.x) {
     double a = init ? 0.0 : acc[i];
     for (int z = 0; z < ns; z++) a += src[(long)z * sstride + i];
@@ -1850,13 +1852,13 @@ static int integral_plan(is3d_engine* e, const SpectraPlan& P, long nw, Integral
   const long by_fill = ((P.mp ? IS3D_FILL_WGS_MP : IS3D_FILL_WGS) + wgs - 1) / wgs;
   const long by_l2 = ((long)NREC * 8 * nw + e->split_bytes - 1) / e->split_bytes;
   const long sstride = (long)npT * bx * KJ * kBlock;
-  // slab memory: the tuning cap, and at most half of what the device has free (plus the slabs this engine already
-  // holds) -- a smaller GPU, or several engines on one device, get fewer splits instead of a failed allocation
+  // slab memory: the tuning cap, and at most half of the device's total memory -- deterministic inputs only, since
+  // the split count sets the summation order (free memory changes from launch to launch with other engines, ranks
+  // and torch's cache; it decides only the F_TS chunking and folding below, which leave the bits unchanged)
   long slab_budget = e->slab_bytes;
   {
     size_t fr = 0, tot = 0;
-    if (hipMemGetInfo(&fr, &tot) == hipSuccess && tot > 0)
-      slab_budget = std::min(slab_budget, (long)(fr / 2) + e->slab_cap * (long)sizeof(double));
+    if (hipMemGetInfo(&fr, &tot) == hipSuccess && tot > 0) slab_budget = std::min(slab_budget, (long)(tot / 2));
   }
   long max_slabs = std::max(8L, std::min(e->max_splits, (slab_budget / 8) / std::max(1L, sstride)));
   if (cap_slabs > 0) max_slabs = std::min(max_slabs, cap_slabs);
@@ -1958,7 +1960,7 @@ static int enqueue_spectra(is3d_engine* e, const IntegralPlan& I, const double* 
         HIPCHK(e, hipEventRecord(e->ev_spec[ic & 1], cs));
         HIPCHK(e, hipStreamWaitEvent(e->fold_st, e->ev_spec[ic & 1], 0));
         hipLaunchKernelGGL(k_fold, dim3((unsigned)fgrid), dim3(256), 0, e->fold_st, e->d_slab, (const double*)buf,
-                           I.sstride, (int)ns, ic == 0 ? 1 : 0);
+                           I.sstride, (int)ns, ic == 0 ? 1 : 0, gate, want);
         HIPCHK(e, hipGetLastError());
         HIPCHK(e, hipEventRecord(e->ev_fold[ic & 1], e->fold_st));
       }
@@ -2142,6 +2144,14 @@ extern "C" int is3d_launch_begin(is3d_engine* e, double* dev_out, void* stream) 
   if (e->chain_q1 >= 0 && (e->p.df_mode != PTMA || e->p.famod_chains <= 0))
     return e->fail(IS3D_ERR_STATE, "a chain range needs PTMA with famod_chains > 0 (params changed since)");
   const bool range = e->chain_q1 >= 0;
+  if (range) {
+    // the integration window follows the chain positions under the current famod_chains C (set_params may have
+    // changed C since is3d_set_chain_range): cells [q0 C, q1 C), so the ranks' windows still tile the surface
+    const long n = e->ncell, C = std::max(1L, std::min<long>(e->p.famod_chains, std::max(n, 1L))), P = (n + C - 1) / C;
+    if (e->chain_q1 > P) return e->fail(IS3D_ERR_ARG, "chain range outside the surface's chain positions (famod_chains changed)");
+    e->win_lo = std::min(n, e->chain_q0 * C);
+    e->win_hi = std::min(n, e->chain_q1 * C);
+  }
   return launch_begin(e, dev_out, stream, range ? e->chain_q0 : 0, range ? e->chain_q1 : -1, range && e->chain_q0 > 0);
 }
 extern "C" int is3d_chain_passes(const is3d_engine* e) { return e && !e->grp ? is3d_internal_chain_npass(e) : 0; }

@@ -106,6 +106,11 @@ def chain_bounds(surf, rank, world, chains, costs=None):
     for k in range(world - 1):
         q.append(max(q[-1], min(P, (r[k][1] + C // 2) // C)))
     q.append(P)
+    if P >= world:
+        # every rank holds at least one position (launch_chained needs a live range on each rank): clamp the inner
+        # boundaries into [k, P - (world - k)] -- a no-op unless the cost balance collapsed a range
+        for k in range(1, world):
+            q[k] = min(max(q[k], q[k - 1] + 1), P - (world - k))
     return q[rank], q[rank + 1]
 
 
@@ -117,12 +122,24 @@ def launch_chained(eng, out_ptr, stream_ptr, rank, world, dist, device=None, syn
     is ordered on the GPU streams (torch's current stream = the launch stream) and the host never waits; with
     'gloo' the boundary buffers live on the host (device=None) and sync() -- e.g. the launch stream's synchronize --
     runs after each copy out of the engine, before the send reads the buffer.  Every rank's range must hold at
-    least one position.  The caller then all-reduces the spectra and calls eng.finish()."""
+    least one position (chain_bounds gives one whenever there are >= world positions); a rank whose range is empty
+    or whose launch_begin fails makes every rank raise -- the check is one collective before the first send, so no
+    successor is left waiting in recv.  The caller then all-reduces the spectra and calls eng.finish()."""
     import torch
-    eng.launch_begin(out_ptr, stream_ptr)
-    npass, nb = eng.chain_passes(), eng.chain_boundary_size()
-    if npass <= 0 or nb <= 0:
-        raise RuntimeError("launch_chained: rank %d has no PTMA chain positions (empty chain range)" % rank)
+    err = None
+    try:
+        eng.launch_begin(out_ptr, stream_ptr)
+        npass, nb = eng.chain_passes(), eng.chain_boundary_size()
+        if npass <= 0 or nb <= 0:
+            err = "rank %d has no PTMA chain positions (empty chain range)" % rank
+    except Exception as exc:       # noqa: BLE001 -- re-raised below on this rank, after the collective
+        err, npass, nb = exc, 0, 0
+    ok = torch.tensor([0.0 if err is not None else 1.0], dtype=torch.float64, device=device)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if err is not None:
+        raise err if isinstance(err, Exception) else RuntimeError("launch_chained: " + err)
+    if ok.item() < 1.0:
+        raise RuntimeError("launch_chained: another rank could not start its chain range (see its error)")
     pred = rank - 1 if rank > 0 else None
     succ = rank + 1 if rank + 1 < world else None
     rbuf = [torch.zeros(nb, dtype=torch.float64, device=device) for _ in range(3)]
