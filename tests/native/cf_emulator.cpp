@@ -80,6 +80,9 @@ static signed char* g_census_lane = nullptr;
 static long* g_census_mod = nullptr;
 extern "C" void emu_set_census_mod(long* counts) { g_census_mod = counts; }
 extern "C" void emu_set_census_lanes(signed char* buf) { g_census_lane = buf; }
+// optional per-lane margin of the modified table lanes (tools/mod_census.py), same indexing as g_census_lane
+static unsigned char* g_census_margin = nullptr;
+extern "C" void emu_set_census_margin(unsigned char* buf) { g_census_margin = buf; }
 // lanes whose smallest exponent exceeds g_near_x (not tail) are recorded as 4 (tools/lane_census.py --near)
 static double g_near_x = 1e300;
 // optional check of sep_slow_cell (k_prep's per-cell bound, engine.hip launch_end): [0] separable lanes off the fast
@@ -378,6 +381,14 @@ extern "C" int emu_spectra_v(const orc_params* p, const orc_setup* su, const orc
               if (g_census_mod && g_census_lane)
                 g_census_lane[(((size_t)i * n + c) * np + s) * nq + kk * nl + l] =
                     (signed char)(11 + (M.skip ? 0 : M.clamp ? 1 : M.tail ? 2 : 3));
+              // margin record (tools/mod_census.py): binades between the lane's smallest E = e^x 2^-k and |s| =
+              // e^chem 2^-k, i.e. k - chem log2(e), clipped to [0, 120]; 255 for skipped / clamped lanes
+              if (g_census_mod && g_census_margin) {
+                const double kk2 = (6755399441055744.0 - M.shiftk) / kExpTabN;
+                const double mg = M.tail ? 120.0 : (kk2 - M.chemm * 1.4426950408889634);
+                g_census_margin[(((size_t)i * n + c) * np + s) * nq + kk * nl + l] =
+                    (M.skip || M.clamp) ? 255 : (unsigned char)std::max(0.0, std::min(120.0, std::floor(mg)));
+              }
               if (M.skip) continue;
               int j = 0;
               if ((variant & 4) && op != 0) {   // k_spectra's table form: {PDm, Qv} and T2 rows (MW, MT above)
