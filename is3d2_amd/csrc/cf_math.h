@@ -1012,8 +1012,26 @@ IS3D_HD void sep_cell_consts(int mode, double* R) {
 // Sc = mT SC1 + b R_SCB,  Ss = mT SS1 + b R_SSB,  L0 = mT L1 + b R_L0B  (see sep_setup).
 // mu_slots = false: rows of kYRowLY doubles (k_spectra's per-lane rows), without Y_MU2 / Y_MU (mod_setup
 // then takes |sig U| itself, ymu = false)
-IS3D_HD void yterms(int mode, int op, const double* R, double y, double eta, double w, double* Y, bool mu_slots = true) {
+IS3D_HD void yterms(int mode, int op, const double* R, double y, double eta, double w, double* Y, bool mu_slots = true,
+                    bool mod_only = false) {
   const int quirk = quirk_pds(mode, op);
+  if (mode >= PTM && mod_only) {
+    // the modified launch's rows (k_spectra MODMAIN): its lanes read the modified slots, Y_NARROW and Y_W only --
+    // the separable slots serve the F_FB launch, which builds its own rows
+    const double es = R[R_ETASCALE];
+    double shm, chm;
+    sinh_cosh(y - es * eta, &shm, &chm);
+    const double ux = chm * R[R_UCX] + shm * R[R_USX];
+    const double uy = chm * R[R_UCY] + shm * R[R_USY];
+    const double uz = chm * R[R_UCZ] + shm * R[R_USZ];
+    Y[Y_MUX] = ux; Y[Y_MUY] = uy; Y[Y_MUZ] = uz;
+    Y[Y_MD] = quirk ? (w * chm * R[R_DAT] + shm * R[R_DANT]) : w * (chm * R[R_DAT] + shm * R[R_DANT]);
+    Y[Y_NARROW] = (R[R_NARROW] != 0.0 && fabs(y - eta) < R[R_DET]) ? 1.0 : 0.0;
+    Y[Y_MU2] = fma(ux, ux, fma(uy, uy, uz * uz));
+    Y[Y_MU] = sqrt(Y[Y_MU2]);
+    Y[Y_W] = w;
+    return;
+  }
   // separable part: p^tau = mT cosh(y-eta) (spectra Grad/CE: sqrt(1+sinh^2), MomentumSpectra.cpp:307-308;
   // the spacetime path uses cosh, SpacetimeDistribution.cpp:313)
   double sh, chx;
@@ -2041,6 +2059,15 @@ IS3D_HD double modt2(const double* R, const double* Y, dbl2 cs) {
 #ifndef IS3D_MOD_STAGED
 #define IS3D_MOD_STAGED 1
 #endif
+#ifndef IS3D_MOD_IEXP
+#define IS3D_MOD_IEXP 0
+#endif
+// m 2^k for a normal m and a k that keeps the result normal: k added to the exponent field of the high word
+IS3D_HD double exp_field_add(double m, int k) {
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, m);
+  const unsigned hi = (unsigned)(b >> 32) + ((unsigned)k << 20), lo = (unsigned)b;
+  return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
 template <bool CLAMP, bool TAIL = false>
 IS3D_HD void mod_nq4(const ModLane& L, const double* X, double* num, double* q) {
   if (!TAIL && (CLAMP || !IS3D_MOD_STAGED)) {
@@ -2071,7 +2098,12 @@ IS3D_HD void mod_nq4(const ModLane& L, const double* X, double* num, double* q) 
   }
 #pragma unroll
   for (int i = 0; i < 4; i++) {
-    const double e = ldexp(fma(T[i], p[i], T[i]), ki[i] >> IS3D_EXP_TAB_BITS);
+    const double m = fma(T[i], p[i], T[i]);
+    // plus-form normal lanes: E = m 2^K lies in [~1/2, 2^251] (mod_setup's k), so the scale can go straight into
+    // the exponent field (one INT32 shift-add on the high word instead of v_ldexp_f64: IS3D_MOD_IEXP); the tail
+    // and en forms can underflow and keep ldexp
+    const double e = (IS3D_MOD_IEXP && IS3D_MOD_PLUS && !TAIL) ? exp_field_add(m, ki[i] >> IS3D_EXP_TAB_BITS)
+                                                                : ldexp(m, ki[i] >> IS3D_EXP_TAB_BITS);
     if (TAIL) { num[i] = e; q[i] = 1.0; }
     else if (IS3D_MOD_PLUS) { num[i] = 1.0; q[i] = e + L.sign; }
     else { num[i] = e; q[i] = fma(L.sign, e, 1.0); }

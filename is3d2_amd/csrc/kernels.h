@@ -262,12 +262,39 @@ __host__ __device__ constexpr int phitab_row(int mode, int nphp, bool by = false
 #ifndef IS3D_EARLY_SKIP
 // k_spectra tests a lane's overflow skip before its setup, so a wavefront whose lanes all skip a cell branches
 // past the setup: bit 1 separable lanes (sep_skips; config 2 Grad 222.0 -> 215.4 ms, RTA-CE 320.4 -> 317.5 ms),
-// bit 2 modified lanes (mod_skips; PTM 465.1 -> 471.8 ms, PTMA unchanged: off), profiles/round3_r3i_ab_skip.log
-#define IS3D_EARLY_SKIP 1
+// bit 2 modified lanes (mod_skips; round 3: PTM 465.1 -> 471.8 ms, PTMA unchanged, profiles/round3_r3i_ab_skip.log;
+// round 6, on the g-free classes and the table-only modified tiles: PTM 405.9 -> 397.3 ms, PTMA 397.5 -> 391.2 ms,
+// profiles/round6_r6d_ab_tables.log -- on)
+#define IS3D_EARLY_SKIP 3
 #endif
 #ifndef IS3D_PAIR_RCP
 #define IS3D_PAIR_RCP 1       // fast path: two phi points per reciprocal (sep_pair_t)
 #endif
+// timing ablations of k_spectra (wrong results; tools/ab.sh variants only, never a product build): 1 = lanes stop
+// after their setup (no phi loop), 2 = lanes stop before their setup, 3 = modified lanes run the tail fours,
+// 4 = no per-lane cell work at all (tiles, tables, barriers only), 5 = 4 without the per-tile tables
+#ifndef IS3D_ABLATE
+#define IS3D_ABLATE 0
+#endif
+// the modified launch builds only the per-tile tables its lanes read: no {b', Phi} rows and no separable y-term
+// slots (those serve the F_FB launch, which builds its own)
+#ifndef IS3D_MOD_TABLES
+#define IS3D_MOD_TABLES 1
+#endif
+// per-tile table loops split their flat index into (cell, row, phi) with a float reciprocal of the runtime row count
+// instead of integer divisions
+#ifndef IS3D_TAB_FDIV
+#define IS3D_TAB_FDIV 1
+#endif
+
+// q = r / d, m = r % d for 0 <= r < 2^24, d >= 1 (rd = 1 / d in float): float(r) is exact and the float quotient is
+// within (r / d) 2^-23 < 1 of the true one, so one correction step makes it exact
+__device__ __forceinline__ void fdivmod(int r, int d, float rd, int& q, int& m) {
+  q = (int)((float)r * rd);
+  m = r - q * d;
+  if (m < 0) { q--; m += d; }
+  if (m >= d) { q++; m -= d; }
+}
 
 
 struct DndxArgs {
@@ -841,6 +868,7 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
   // the modified path's {PDm, Qv}) per (cell, phi), {TE, T2} for RTA-CE's table launch, y-terms per
   // (cell, row)
   auto tables_ab = [&](const double* s_rec, int ntx, int tb) __attribute__((always_inline)) {
+    if (IS3D_ABLATE >= 5) return;
     dbl2* bp = s_bp + tb * bpsz;
     double* qvt = s_qv + tb * qvsz;
     dbl2* mw = (dbl2*)qvt;
@@ -858,10 +886,11 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
       double qv = 0.0;
       if (j < A.nphi && R[R_KIND] != 0.0) {
         const dbl2 tr = s_trig[j];
-        v = phiterms(MODE, R, pTl, tr.x, tr.y, s_etab);
+        // the modified launch reads only {PDm, Qv}: {b', Phi} serve the separable lanes (the F_FB launch)
+        if constexpr (!(MODMAIN && IS3D_MOD_TABLES)) v = phiterms(MODE, R, pTl, tr.x, tr.y, s_etab);
         if (MODE >= PTM && R[R_KIND] == 2.0) qv = modqv(R, csj);
       }
-      bp[o] = v;
+      if constexpr (!(MODMAIN && IS3D_MOD_TABLES)) bp[o] = v;
       if constexpr (MODE >= PTM) {
         dbl2 m; m.x = modpdm(R, csj); m.y = qv;           // zero rows / padding give 0
         mw[o] = m;
@@ -883,39 +912,57 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
         const int kk = q / A.nl, l = q % A.nl;
         const double y = s_grid[kk];
         const double eta = (A.dim == 3) ? R[R_ETA] : s_grid[A.nk + l];
-        yterms(MODE, A.op, R, y, eta, s_grid[A.nk + A.nl + l], yb + ((long)t * nyr + qq) * kYRow);
+        yterms(MODE, A.op, R, y, eta, s_grid[A.nk + A.nl + l], yb + ((long)t * nyr + qq) * kYRow, true,
+               MODMAIN && IS3D_MOD_TABLES);
       }
     }
   };
   // ---- phase C: the per-(cell, row, phi) tables of one tile from its buffer-tb tables (single buffer)
+  // flat per-tile table index -> phi slot jj, (cell t, row qq), phi block jb and q = (r0 + qq) % nq
+  const float rnqw = 1.0f / (float)nqw, rnq = 1.0f / (float)A.nq;
+  auto tab_index = [&](int idx, int& jj, int& t, int& qq, int& jb, int& qm) __attribute__((always_inline)) {
+    jj = idx % KJ;
+    const int r = idx / KJ;
+    if (IS3D_TAB_FDIV) {
+      fdivmod(r, nqw, rnqw, t, qq);
+      fdivmod((int)r0 + qq, A.nq, rnq, jb, qm);
+    } else {
+      qq = r % nqw; t = r / nqw;
+      jb = (int)((r0 + qq) / A.nq); qm = (int)((r0 + qq) % A.nq);
+    }
+  };
   auto tables_c = [&](const double* s_rec, int ntx, int tb) __attribute__((always_inline)) {
+    if (IS3D_ABLATE >= 5) return;
     const double* qvt = s_qv + tb * qvsz;
     const double* yb = s_y + tb * ysz;
     if constexpr (MODE >= PTM && !LY) {
       // T2 = 2 U_q . W per (cell, q, phi) of the modified cells (mod_quad_tab_t)
       for (int idx = tid; idx < ntx * nqw * KJ; idx += kBlock) {
-        const int jj = idx % KJ, r = idx / KJ, qq = r % nqw, t = r / nqw;
-        const int j = (int)((r0 + qq) / A.nq) * KJ + jj;
+        int jj, t, qq, jb, qm;
+        tab_index(idx, jj, t, qq, jb, qm);
+        const int j = jb * KJ + jj;
         const double* R = s_rec + t * NREC;
         if (R[R_KIND] != 2.0) continue;
-        const int yr = allq ? (int)((r0 + qq) % A.nq) : qq;
+        const int yr = allq ? qm : qq;
         s_mt[((long)t * nqw + qq) * prow + jj] = modt2(R, yb + ((long)t * nyr + yr) * kYRow, s_cs[j]);
       }
     }
     if constexpr (TS) {
       // T1 = SC1 pc + SS1 ps per (cell, q row, phi) (one phi block: phi slot jj)
       for (int idx = tid; idx < ntx * nqw * KJ; idx += kBlock) {
-        const int jj = idx % KJ, r = idx / KJ, qq = r % nqw, t = r / nqw;
-        const double* Y = yb + ((long)t * nyr + (allq ? (int)((r0 + qq) % A.nq) : qq)) * kYRow;
+        int jj, t, qq, jb, qm;
+        tab_index(idx, jj, t, qq, jb, qm);
+        const double* Y = yb + ((long)t * nyr + (allq ? qm : qq)) * kYRow;
         const dbl2 c = s_cs[jj];
         s_t1[((long)t * nqw + qq) * prow2 + jj] = fma(Y[Y_SC1], c.x, Y[Y_SS1] * c.y);
       }
     } else if constexpr (TB) {
       // {PD, T1 = SC1 pc + SS1 ps} per (cell, q, phi) (rows of skipped cells are never read)
       for (int idx = tid; idx < ntx * nqw * KJ; idx += kBlock) {
-        const int jj = idx % KJ, r = idx / KJ, qq = r % nqw, t = r / nqw;
-        const int j = (int)((r0 + qq) / A.nq) * KJ + jj;
-        const double* Y = yb + ((long)t * nyr + (allq ? (int)((r0 + qq) % A.nq) : qq)) * kYRow;
+        int jj, t, qq, jb, qm;
+        tab_index(idx, jj, t, qq, jb, qm);
+        const int j = jb * KJ + jj;
+        const double* Y = yb + ((long)t * nyr + (allq ? qm : qq)) * kYRow;
         const dbl2 c = s_cs[j];
         dbl2 v;
         v.x = qvt[t * nphp + j];
@@ -989,6 +1036,7 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
       double rn_next = (MODE == PTM && ntx > 0) ? rn_load(0) : 0.0;
       for (int t = 0; t < ntx; t++) {
         const double rn_cell = rn_next;
+        if (IS3D_ABLATE >= 4) { acc[0] += s_rec[t * NREC]; continue; }
         if (MODE == PTM && t + 1 < ntx) rn_next = rn_load(t + 1);
         const double* R = s_rec + t * NREC;
         const double kind = R[R_KIND];
@@ -1017,6 +1065,7 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
         if (FB && !sep) continue;
         if constexpr (!MODMAIN) {     // Grad / RTA-CE lanes (sep throughout), the F_FB launch's separable lanes
           if ((IS3D_EARLY_SKIP & 1) && sep_skips(R, Y, mT, pT, baryon)) continue;
+          if (IS3D_ABLATE == 2) { acc[0] += R[R_KIND] * Y[0]; continue; }
           SepLane L;
           // near-tail lanes: F_TS Grad launches without regulate or baryon (IS3D_NEAR: config 2 166.2 -> 162.7 ms;
           // the F_BY launch, config 3, 176.8 -> 179.5 ms: off there)
@@ -1025,6 +1074,7 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
                     ((TB && IS3D_TAIL && (MODE == GRAD || IS3D_TAIL_CE || TS)) || PDT) ? (IS3D_TAIL_WAVE ? 2 : 1) : 0,
                     NEAR ? 2 : 0);
           if (L.skip) continue;
+          if (IS3D_ABLATE == 1) { acc[0] += L.a + L.D0 + L.S0 + L.Sc + L.Ss + L.E0 + L.L0 + L.escw + L.ssc + L.Dc + L.Ds; continue; }
           if constexpr (TS) {
             // this cell's k_phitab row (wave-uniform: ipt, the tile and t are) and the lane's T1 row
             constexpr int RW = phitab_row(MODE, KJ, (FLAGS & F_BY) != 0);   // one phi block: nphp = KJ
@@ -1071,12 +1121,17 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
         }
         if constexpr (MODMAIN) {
           if ((IS3D_EARLY_SKIP & 2) && IS3D_MOD_SQ_BOUNDS && mod_skips(R, Y, mT, m2, pT, baryon, !LY)) continue;
+          if (IS3D_ABLATE == 2) { acc[0] += R[R_KIND] * Y[0]; continue; }
           ModLane M;
           const dbl2* MW = mwt + t * nphp + j0;
           const double* MT = s_mt + ((long)t * nqw + row) * prow;
           if constexpr (!LY && KJ % 4 == 0) mod_setup<KJ>(R, Y, mT, m2, pT, sign, baryon, rn_abs, s_etab, M, true, true, MW, MT);
           else mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, s_etab, M, !LY, false);
           if (M.skip) continue;
+          if (IS3D_ABLATE == 1) { acc[0] += M.E0 + M.D0 + M.Dw + M.mT + M.shiftk + M.sign + M.tail + M.clamp; continue; }
+          if constexpr (IS3D_ABLATE == 3 && !LY && KJ % 4 == 0) {
+            if (!M.clamp) { mod_phi_loop_tab_tail<FLAGS, KJ>(M, MW, MT, acc); continue; }
+          }
           if constexpr (LY) {        // no T2 rows: the lane's linear forms (mod_pair_lane_t)
             if (M.clamp) mod_phi_loop_lane<FLAGS, true, KJ>(M, CSl, MW, acc);
             else mod_phi_loop_lane<FLAGS, false, KJ>(M, CSl, MW, acc);
