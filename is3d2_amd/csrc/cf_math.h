@@ -1016,7 +1016,8 @@ IS3D_HD void yterms(int mode, int op, const double* R, double y, double eta, dou
                     bool mod_only = false) {
   const int quirk = quirk_pds(mode, op);
   if (mode >= PTM && mod_only) {
-    // the modified launch's rows (k_spectra MODMAIN): its lanes read the modified slots, Y_NARROW and Y_W only --
+    // the modified launches' rows (k_spectra / k_dndx MODMAIN): their lanes read the modified slots, Y_WDX / Y_WDY,
+    // Y_NARROW and Y_W only --
     // the separable slots serve the F_FB launch, which builds its own rows
     const double es = R[R_ETASCALE];
     double shm, chm;
@@ -1026,9 +1027,12 @@ IS3D_HD void yterms(int mode, int op, const double* R, double y, double eta, dou
     const double uz = chm * R[R_UCZ] + shm * R[R_USZ];
     Y[Y_MUX] = ux; Y[Y_MUY] = uy; Y[Y_MUZ] = uz;
     Y[Y_MD] = quirk ? (w * chm * R[R_DAT] + shm * R[R_DANT]) : w * (chm * R[R_DAT] + shm * R[R_DANT]);
+    Y[Y_WDX] = w * R[R_DAX]; Y[Y_WDY] = w * R[R_DAY];        // the lane forms' p.dsigma (k_dndx, mod_setup Dc / Ds)
     Y[Y_NARROW] = (R[R_NARROW] != 0.0 && fabs(y - eta) < R[R_DET]) ? 1.0 : 0.0;
-    Y[Y_MU2] = fma(ux, ux, fma(uy, uy, uz * uz));
-    Y[Y_MU] = sqrt(Y[Y_MU2]);
+    if (mu_slots) {
+      Y[Y_MU2] = fma(ux, ux, fma(uy, uy, uz * uz));
+      Y[Y_MU] = sqrt(Y[Y_MU2]);
+    }
     Y[Y_W] = w;
     return;
   }
@@ -1141,6 +1145,12 @@ static constexpr double kExpFast = -300.0;
 // (the rounding of the reciprocal it replaces: rcp1, ~2e-15); a Grad lane whose smallest exponent exceeds it
 // takes (1 - u) (1 + (1 - u) S) = (1 + S) - u (1 + 2 S) per point, no reciprocal (sep_quad_tb_near_t)
 static constexpr double kNearX = 18.0;
+// IS3D_SEP_INVA: sep_setup's default for inv_a (tail / near lanes take 1/a from one table exp of -xs instead of a and
+// its reciprocal).  MI355X (profiles/round6_r6e_ab_inva.log): config 2 operation 0 Grad k_dndx 319.6 -> 313.0 ms, but
+// the F_TS Grad k_spectra 151.0 -> 155.7 ms (same VGPRs, more SGPR spills) -- so off by default, on in k_dndx
+#ifndef IS3D_SEP_INVA
+#define IS3D_SEP_INVA 0
+#endif
 
 // 1/d for finite normal d: v_rcp_f64 (measured max rel. error 4.5e-8 on gfx950) + one
 // Newton step (~2e-15); IEEE division on the host.  Callers guarantee d is finite.
@@ -1189,7 +1199,7 @@ IS3D_HD bool sep_slow_cell(const double* R, double pT_max, double b_max) {
 
 IS3D_HD void sep_setup(int flavor, const double* R, const double* Y, double mT, double mT2, double m2, double mTb,
                        double pT, double sign, double baryon, const double* etab, SepLane& L, int allow_tail = 0,
-                       int allow_near = 0) {
+                       int allow_near = 0, bool inv_a = IS3D_SEP_INVA) {
   L.sign = sign;
   L.x = fma(mT, Y[Y_AT], -baryon * R[R_CHEM]);
   const double zb = pT * R[R_ZB];                 // >= max_j |pT B_j / T|
@@ -1224,7 +1234,16 @@ IS3D_HD void sep_setup(int flavor, const double* R, const double* Y, double mT, 
   }
 #endif
   const int k = (L.fast && xs > 150.0) ? (int)((xs - 150.0) * 1.4426950408889634) : 0;
-  L.a = L.fast ? exp_tab(exp_tab_coef(), etab, xs * kInvLn2xN, k) : 0.0;
+  // tail and near lanes (xs > kNearX, so fast) use only 1/a = e^-xs 2^k: one table exp of -xs instead of a = e^xs 2^-k
+  // and its reciprocal (IS3D_SEP_INVA; a is left 0, none of their loops reads it)
+  const bool inva = inv_a && (L.tail || L.near);
+  double ra = 0.0;
+  if (inva) {
+    ra = exp_tab(exp_tab_coef(), etab, -xs * kInvLn2xN, -k);
+    L.a = 0.0;
+  } else {
+    L.a = L.fast ? exp_tab(exp_tab_coef(), etab, xs * kInvLn2xN, k) : 0.0;
+  }
   const double esc = ldexp(1.0, -k);
   L.ssc = sign * esc;
   L.escw = esc * Y[Y_W];
@@ -1239,7 +1258,7 @@ IS3D_HD void sep_setup(int flavor, const double* R, const double* Y, double mT, 
   L.L0 = sa * fma(mT, Y[Y_L1], baryon * R[R_L0B]); L.Lc = sa * R[R_LC]; L.Ls = sa * R[R_LS];
   L.c0 = (flavor == SEP_PTB) ? R[R_DZ] - 3.0 * R[R_DLAM] : 0.0;
   if (L.tail || L.near) {   // f_eq = b' / a: fold 1/a into the p.dsigma coefficients (both carry the same 2^-k)
-    const double ra = rcp1(L.a);
+    if (!inva) ra = rcp1(L.a);
     L.D0 *= ra; L.Dc *= ra; L.Ds *= ra; L.escw *= ra;
     if (L.near) L.ssc *= ra;         // u = ssc b' (sep_quad_tb_near_t)
   }

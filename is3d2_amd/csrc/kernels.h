@@ -1345,7 +1345,7 @@ __global__ __launch_bounds__(kBlock, (dndx_waves_f<MODE, FLAGS>())) void k_dndx(
         const double y = s_grid[ky];
         const double eta = (A.dim == 3) ? R[R_ETA] : s_grid[A.nk + l];
         const double w = s_grid[A.nk + A.nl + l];
-        yterms(MODE, 0, R, y, eta, w, s_y + ((long)t * A.nq + q) * kYRowLY, false);
+        yterms(MODE, 0, R, y, eta, w, s_y + ((long)t * A.nq + q) * kYRowLY, false, MODMAIN && IS3D_MOD_TABLES);
       }
     }
     for (int ipt = 0; ipt < A.npT; ipt++) {
@@ -1364,13 +1364,14 @@ __global__ __launch_bounds__(kBlock, (dndx_waves_f<MODE, FLAGS>())) void k_dndx(
         double qv = 0.0;
         if (j < A.nphi && R[R_KIND] != 0.0) {
           const dbl2 tr = s_trig[j];
-          v = phiterms(MODE, R, pT, tr.x, tr.y, s_etab);
+          // the modified launch reads Qv only ({b', Phi} serve the separable lanes of the F_FB launch)
+          if constexpr (!(MODMAIN && IS3D_MOD_TABLES)) v = phiterms(MODE, R, pT, tr.x, tr.y, s_etab);
           if (MODE >= PTM && R[R_KIND] == 2.0) {
             dbl2 c; c.x = pT * tr.x; c.y = pT * tr.y;
             qv = modqv(R, c);
           }
         }
-        s_bp[t * nphp + j] = v;
+        if constexpr (!(MODMAIN && IS3D_MOD_TABLES)) s_bp[t * nphp + j] = v;
         if (MODE >= PTM) s_qv[t * nphp + j] = qv;
       }
       __syncthreads();
@@ -1401,7 +1402,7 @@ __global__ __launch_bounds__(kBlock, (dndx_waves_f<MODE, FLAGS>())) void k_dndx(
             // (Grad only: RTA-CE's tail pairs, one 1/E per pair, were slower -- 508 -> 560 ms at config 2 against
             // Grad's 404 -> 333 ms, profiles/round3_r3x_ab_split_dndx_tail.log)
             constexpr bool TL = IS3D_TAIL_DNDX && MODE == GRAD;
-            sep_setup(sep_flavor(MODE), R, Y, mT, mT2, m2, mTb, pT, sign, baryon, s_etab, L, TL ? 2 : 0);
+            sep_setup(sep_flavor(MODE), R, Y, mT, mT2, m2, mTb, pT, sign, baryon, s_etab, L, TL ? 2 : 0, 0, true);
             if (L.skip) continue;
             if (TL && L.tail) cell += sep_phi_wsum_tail<MODE, FLAGS, KJ>(L, s_cs + j0, BP, W);
             else cell += L.fast ? sep_phi_wsum<MODE, FLAGS, true, KJ>(L, s_cs + j0, BP, W)
