@@ -213,6 +213,46 @@ static constexpr int kExpTabN = 64, kExpTabDeg = 5;
 static constexpr double kInvLn2xN = kInvLn2x64;
 #endif
 
+// degree of the modified lanes' 2^(r/N) polynomial with the 256-entry table: 3 (minimax, 3.5e-14 relative) or 4 (Taylor, ~1 ulp)
+#ifndef IS3D_MOD_EXP_DEG
+#define IS3D_MOD_EXP_DEG 3
+#endif
+// the modified lanes' exp table: IS3D_MOD_TAB_BITS = 8 shares exp_tab's 256 entries (degree-3 polynomial); 11 gives them
+// their own 2^(j/2048) table (16 KB of LDS in the modified launches, which in turn drop their unused {b', Phi} rows:
+// IS3D_MOD_TABLES) and a degree-2 polynomial -- one FMA fewer per point, 2.1e-13 instead of 3.5e-14 relative
+#ifndef IS3D_MOD_TAB_BITS
+#define IS3D_MOD_TAB_BITS 8
+#endif
+// the modified launch builds only the per-tile tables its lanes read: no {b', Phi} rows and no separable y-term
+// slots (those serve the F_FB launch, which builds its own)
+#ifndef IS3D_MOD_TABLES
+#define IS3D_MOD_TABLES 1
+#endif
+#if IS3D_MOD_TAB_BITS == 11
+#if !IS3D_MOD_TABLES
+#error "IS3D_MOD_TAB_BITS = 11 needs IS3D_MOD_TABLES (the modified launches then read no exp_tab table)"
+#endif
+#include "exp2_tab2048.h"
+static constexpr int kModTabN = 2048, kModExpDeg = 2;
+#define kModExp2Tab kExp2Tab2048
+static constexpr double kModInvLn2xN = kInvLn2x2048;
+#define kModExpA kExpTabA2048
+#elif IS3D_MOD_TAB_BITS == IS3D_EXP_TAB_BITS
+static constexpr int kModTabN = kExpTabN;
+#define kModExp2Tab kExp2Tab
+static constexpr double kModInvLn2xN = kInvLn2xN;
+#if IS3D_EXP_TAB_BITS == 8 && IS3D_MOD_EXP_DEG == 3
+static constexpr int kModExpDeg = 3;
+// near-minimax (Chebyshev) coefficients of (2^(r/256) - 1) / r on |r| <= 1/2: 1 + r p(r) within 3.5e-14
+static constexpr double kModExpA[3] = {0.0027076061740622863, 3.6655660167967235e-06, 3.308302907918888e-09};
+#else
+static constexpr int kModExpDeg = kExpTabDeg;
+#define kModExpA kExpTabCoefs
+#endif
+#else
+#error "IS3D_MOD_TAB_BITS: 11, or equal to IS3D_EXP_TAB_BITS"
+#endif
+
 struct ExpTabCoef { double shift, a[kExpTabDeg]; };
 
 IS3D_HD ExpTabCoef exp_tab_coef() {
@@ -546,11 +586,11 @@ IS3D_HD void modified_directions(const double* Asym, double tau, double Xt, doub
 }
 
 // Last step of the modified-path prologues (R_INVTM, R_CHEMM, R_VB and the directions set): Uc, Us, Vc,
-// Vs and R_VB in exp-table units, scaled by sig = (1/T_mod) kExpTabN/ln2, so that every E_mod^2 the
-// lanes build (mod_setup, modqv, modt2) is (sig E_mod)^2 and its square root is exp_tab's argument
+// Vs and R_VB in the modified lanes' exp-table units, scaled by sig = (1/T_mod) kModTabN/ln2, so that every
+// E_mod^2 the lanes build (mod_setup, modqv, modt2) is (sig E_mod)^2 and its square root is their exp's argument
 // without a multiply
 IS3D_HD void mod_scale_record(double* R) {
-  const double sig = R[R_INVTM] * kInvLn2xN;
+  const double sig = R[R_INVTM] * kModInvLn2xN;
   for (int f = R_UCX; f <= R_VSZ; f++) R[f] *= sig;
   R[R_VB] *= sig;
 }
@@ -1775,7 +1815,7 @@ IS3D_HD double sqrt_nr(double v) {
 // en = exp(chem - E_mod/T_mod): u.p > 0 bounds en by e^chem and, for bosons (no baryon number),
 // below 1, so 1 + sign en lies in ~[1e-3, 2] and two points can share one reciprocal; en -> 0
 // where the reference's exp overflows to 1/inf = 0.  |renorm| is folded into p.dsigma.
-// Exp-table units: the record's directions are scaled by sig = (1/T_mod) kExpTabN/ln2
+// Exp-table units: the record's directions are scaled by sig = (1/T_mod) kModTabN/ln2
 // (mod_scale_record), so E0 + Qv + ... = (sig E_mod)^2 and sqrt of it is exp_tab's argument; on the
 // table lanes (!clamp) e^chem is folded out of the exponential into sign and the p.dsigma
 // coefficients (en = e^chem e^-E/T: en / (1 + sign en) = e^chem e / (1 + (sign e^chem) e)), so a point
@@ -1790,7 +1830,6 @@ IS3D_HD double sqrt_nr(double v) {
 #ifndef IS3D_MOD_PLUS
 #define IS3D_MOD_PLUS 1
 #endif
-// degree of the modified lanes' 2^(r/N) polynomial: 3 (minimax, 3.5e-14 relative) or 4 (Taylor, ~1 ulp)
 // Boltzmann-tail lanes (IS3D_MOD_TAIL): where |s| < 2^-55 <= 2^-55 E at every point, E + s == E exactly, so
 // f = 2^-k / E = e^-(x - k ln2) 2^-k: the point evaluates that exponential directly (the shift constant
 // 1.5 2^52 + N k) and skips the denominators and the shared reciprocal (mod_quad_tab_tail_t).  Decided once
@@ -1804,26 +1843,15 @@ IS3D_HD double sqrt_nr(double v) {
 #ifndef IS3D_MOD_EXACT
 #define IS3D_MOD_EXACT 1
 #endif
-#ifndef IS3D_MOD_EXP_DEG
-#define IS3D_MOD_EXP_DEG 3
-#endif
-#if IS3D_EXP_TAB_BITS == 8 && IS3D_MOD_EXP_DEG == 3
-static constexpr int kModExpDeg = 3;
-// near-minimax (Chebyshev) coefficients of (2^(r/256) - 1) / r on |r| <= 1/2: 1 + r p(r) within 3.5e-14
-static constexpr double kModExpA[3] = {0.0027076061740622863, 3.6655660167967235e-06, 3.308302907918888e-09};
-#else
-static constexpr int kModExpDeg = kExpTabDeg;
-#define kModExpA kExpTabCoefs
-#endif
 struct ModExpCoef { double a[kModExpDeg]; };
 
 struct ModLane {
   double E0, Ec, Es, D0, Dc, Ds, chemm, sign;   // table lanes: sign = sign e^chem, D = |renorm| e^chem D
                                                 // (plus form: both x 2^-k)
   double mT, Dw;               // table form (mod_quad_tab_t): E_mod^2 = E0 + Qv + mT T2, p.dsigma = D0 + Dw PDm
-  double shiftk;               // plus form: 1.5 2^52 - kExpTabN k (the lane's 2^-k in the range reduction)
+  double shiftk;               // plus form: 1.5 2^52 - kModTabN k (the lane's 2^-k in the range reduction)
   ModExpCoef et;               // pinned once per lane setup, reused by every phi point
-  const double* etab;          // 2^(j/kExpTabN) table (LDS on the device)
+  const double* etab;          // 2^(j/kModTabN) table (LDS on the device)
   int skip, clamp;   // clamp: some point's exp argument may leave the table lanes' domain (exp_clamped instead)
   int tail;          // IS3D_MOD_TAIL: Boltzmann-tail table lane (shiftk = 1.5 2^52 + N k, mod_quad_tab_tail_t)
 };
@@ -1836,8 +1864,8 @@ IS3D_HD double modqv(const double* R, dbl2 cs) {
   return fma(wx, wx, fma(wy, wy, wz * wz));
 }
 
-// ln2 / kExpTabN: sig E_mod x this = E_mod / T_mod
-static constexpr double kLn2overN = 1.0 / kInvLn2xN;
+// ln2 / kModTabN: sig E_mod x this = E_mod / T_mod
+static constexpr double kLn2overN = 1.0 / kModInvLn2xN;
 // table lanes: E_mod / T_mod below 1e6 (exp_tab's integer part fits the low word; beyond e^-745 en is
 // 0 anyway) and |chem| < 30: where e^(-E/T) underflows (E/T > 745) the reference's exp(E/T - chem)
 // overflows too (E/T - chem > 715), so folding e^chem out loses nothing, and four 1 + sign e^chem e
@@ -1850,14 +1878,28 @@ static constexpr double kModTabX = 1.0e6, kModTabChem = 30.0;
 #define IS3D_MOD_SQ_BOUNDS 1
 #endif
 
+// e^x for xN = x kModTabN/ln2 with the modified lanes' table and polynomial (mod_setup's e^chem)
+IS3D_HD double mod_exp(const double* etab, double xN) {
+  if (IS3D_MOD_TAB_BITS == IS3D_EXP_TAB_BITS) return exp_tab(exp_tab_coef(), etab, xN);   // the shared table
+  const double sh = 6755399441055744.0;
+  const double t = xN + sh;
+  const double rs = xN - (t - sh);
+  const int ki = (int)(unsigned)__builtin_bit_cast(unsigned long long, t);
+  double p = kModExpA[kModExpDeg - 1];
+#pragma unroll
+  for (int i = kModExpDeg - 2; i >= 0; i--) p = fma(p, rs, kModExpA[i]);
+  const double T = etab[ki & (kModTabN - 1)];
+  return ldexp(fma(T, rs * p, T), ki >> IS3D_MOD_TAB_BITS);
+}
+
 // mod_setup's skip test alone (same operations, IS3D_MOD_SQ_BOUNDS form), for an early branch past the setup
 IS3D_HD bool mod_skips(const double* R, const double* Y, double mT, double m2, double pT, double baryon, bool ymu = true) {
   const double ux = Y[Y_MUX], uy = Y[Y_MUY], uz = Y[Y_MUZ];
   const double u2 = ymu ? Y[Y_MU2] : fma(ux, ux, fma(uy, uy, uz * uz));
-  const double sig = R[R_INVTM] * kInvLn2xN, m2s = m2 * (sig * sig);
+  const double sig = R[R_INVTM] * kModInvLn2xN, m2s = m2 * (sig * sig);
   const double mu = mT * (ymu ? Y[Y_MU] : sqrt(u2));
   const double lo = mu - pT * R[R_VB];
-  const double thr = (kExpMax + 1.0 + baryon * R[R_CHEMM]) * kInvLn2xN;
+  const double thr = (kExpMax + 1.0 + baryon * R[R_CHEMM]) * kModInvLn2xN;
   return thr < 0.0 || (lo > 0.0 && (m2s + lo * lo) * (1.0 - 2e-12) > thr * thr);
 }
 
@@ -1871,7 +1913,7 @@ IS3D_HD void mod_setup(const double* R, const double* Y, double mT, double m2, d
                        const dbl2* MW = nullptr, const double* MT = nullptr, int nx = KJX) {
   const double ux = Y[Y_MUX], uy = Y[Y_MUY], uz = Y[Y_MUZ];   // sig U
   const double u2 = ymu ? Y[Y_MU2] : fma(ux, ux, fma(uy, uy, uz * uz));
-  const double sig = R[R_INVTM] * kInvLn2xN, m2s = m2 * (sig * sig);
+  const double sig = R[R_INVTM] * kModInvLn2xN, m2s = m2 * (sig * sig);
   L.E0 = fma(mT * mT, u2, m2s);
   const double tm = 2.0 * mT;
   L.Ec = tm * fma(ux, R[R_VCX], fma(uy, R[R_VCY], uz * R[R_VCZ]));
@@ -1888,7 +1930,7 @@ IS3D_HD void mod_setup(const double* R, const double* Y, double mT, double m2, d
 #if IS3D_MOD_SQ_BOUNDS
   // the same two tests on squares (no sqrt): skip when sig E_min (1 - 1e-12) exceeds
   // thr = (kExpMax + 1 + chem) N/ln2 -- always when thr < 0, as E_min >= 0
-  const double thr = (kExpMax + 1.0 + L.chemm) * kInvLn2xN, xm = kModTabX * kInvLn2xN;
+  const double thr = (kExpMax + 1.0 + L.chemm) * kModInvLn2xN, xm = kModTabX * kModInvLn2xN;
   L.skip = (thr < 0.0 || (lo > 0.0 && (m2s + lo * lo) * (1.0 - 2e-12) > thr * thr)) ? 1 : 0;
   L.clamp = ((m2s + hi * hi) < xm * xm && fabs(L.chemm) < kModTabChem) ? 0 : 1;
 #else
@@ -1909,8 +1951,8 @@ IS3D_HD void mod_setup(const double* R, const double* Y, double mT, double m2, d
 #else
       const double emin = sqrt(e2);
 #endif
-      k = (int)(emin * ((1.0 - 1e-6) / kExpTabN));
-      const double xk = (k + 250.0) * kExpTabN;
+      k = (int)(emin * ((1.0 - 1e-6) / kModTabN));
+      const double xk = (k + 250.0) * kModTabN;
       wide = (e2h < xk * xk) ? 0 : 1;
     };
     scale();
@@ -1955,9 +1997,9 @@ IS3D_HD void mod_setup(const double* R, const double* Y, double mT, double m2, d
   if (wide && !L.tail) L.clamp = 1;
   // e^chem of the table lanes (1 for mesons and without baryon chemistry: a wave-uniform skip there)
   double ec = 1.0;
-  if (!L.clamp && L.chemm != 0.0) ec = exp_tab(exp_tab_coef(), etab, L.chemm * kInvLn2xN);
+  if (!L.clamp && L.chemm != 0.0) ec = mod_exp(etab, L.chemm * kModInvLn2xN);
   if (L.clamp) k = 0;
-  L.shiftk = 6755399441055744.0 + (L.tail ? 1.0 : -1.0) * ((double)k * kExpTabN);
+  L.shiftk = 6755399441055744.0 + (L.tail ? 1.0 : -1.0) * ((double)k * kModTabN);
   const double d = ldexp(renorm_abs * ec, -k);
   L.sign = ldexp(sign * ec, -k);
   L.D0 = d * (mT * Y[Y_MD]); L.Dc = d * Y[Y_WDX]; L.Ds = d * Y[Y_WDY];
@@ -1996,8 +2038,8 @@ IS3D_HD void mod_nq_x(const ModLane& L, double X, double& num, double& q) {
   double p = L.et.a[kModExpDeg - 1];
 #pragma unroll
   for (int i = kModExpDeg - 2; i >= 0; i--) p = fma(p, rs, L.et.a[i]);
-  const double T = L.etab[ki & (kExpTabN - 1)];
-  const double e = ldexp(fma(T, rs * p, T), ki >> IS3D_EXP_TAB_BITS);
+  const double T = L.etab[ki & (kModTabN - 1)];
+  const double e = ldexp(fma(T, rs * p, T), ki >> IS3D_MOD_TAB_BITS);
   if (IS3D_MOD_PLUS) { num = 1.0; q = e + L.sign; }
   else { num = e; q = fma(L.sign, e, 1.0); }
 }
@@ -2107,7 +2149,7 @@ IS3D_HD void mod_nq4(const ModLane& L, const double* X, double* num, double* q) 
     ki[i] = (int)(unsigned)__builtin_bit_cast(unsigned long long, t[i]);
   }
 #pragma unroll
-  for (int i = 0; i < 4; i++) T[i] = L.etab[ki[i] & (kExpTabN - 1)];
+  for (int i = 0; i < 4; i++) T[i] = L.etab[ki[i] & (kModTabN - 1)];
 #pragma unroll
   for (int i = 0; i < 4; i++) {
     double a = L.et.a[kModExpDeg - 1];
@@ -2121,8 +2163,8 @@ IS3D_HD void mod_nq4(const ModLane& L, const double* X, double* num, double* q) 
     // plus-form normal lanes: E = m 2^K lies in [~1/2, 2^251] (mod_setup's k), so the scale can go straight into
     // the exponent field (one INT32 shift-add on the high word instead of v_ldexp_f64: IS3D_MOD_IEXP); the tail
     // and en forms can underflow and keep ldexp
-    const double e = (IS3D_MOD_IEXP && IS3D_MOD_PLUS && !TAIL) ? exp_field_add(m, ki[i] >> IS3D_EXP_TAB_BITS)
-                                                                : ldexp(m, ki[i] >> IS3D_EXP_TAB_BITS);
+    const double e = (IS3D_MOD_IEXP && IS3D_MOD_PLUS && !TAIL) ? exp_field_add(m, ki[i] >> IS3D_MOD_TAB_BITS)
+                                                                : ldexp(m, ki[i] >> IS3D_MOD_TAB_BITS);
     if (TAIL) { num[i] = e; q[i] = 1.0; }
     else if (IS3D_MOD_PLUS) { num[i] = 1.0; q[i] = e + L.sign; }
     else { num[i] = e; q[i] = fma(L.sign, e, 1.0); }

@@ -1256,8 +1256,13 @@ static SpectraPlan spectra_plan(const is3d_engine* e, bool allow_ts = true) {
   // k_spectra's LDS layout (kernels.h): record tiles x kRecBufs, per-tile tables x kTabBufs
   // F_TS (kernels.h TS): an F_TB launch with one phi block of 24 or 32 points
   auto ts_ok = [&]() { return IS3D_TS && allow_ts && P.tb && P.njb == 1 && (P.KJ == 24 || P.KJ == 32); };
+  bool fb_layout = false;               // sizing the F_FB launch (separable lanes of a modified mode)
   auto lds_bytes = [&](int qrows) {     // qrows = 0: F_LY layout (one y-term row per lane)
     const size_t nphp = (size_t)P.njb * P.KJ, tile = (size_t)kTile;
+    // modified launches (kernels.h MODMAIN): the modified lanes' exp table, no {b', Phi} rows (IS3D_MOD_TABLES)
+    const bool modmain = mode >= PTM && !fb_layout;
+    const size_t etab = modmain ? (size_t)is3d::kModTabN : (size_t)kExpTabN;
+    const size_t bprows = (modmain && IS3D_MOD_TABLES) ? 0 : 1;
     if (ts_ok()) {
       // records x 3, trig + {pc, ps}, grid, y-term rows x 2, exp table, T1 rows [tile][qrows][KJ + 2] (+ 1: alignment)
       return sizeof(double) * (3 * tile * NREC + 4 * nphp + (size_t)(nk + 2 * nl) +
@@ -1268,9 +1273,9 @@ static SpectraPlan spectra_plan(const is3d_engine* e, bool allow_ts = true) {
     const bool pipe = IS3D_PIPE && (P.tb || (mode >= PTM && qrows && !P.t8 && !P.ly));
     const size_t rb = pipe ? 3 : 2, tb = pipe ? 2 : 1, qvf = (mode >= PTM || !pipe) ? 2 : 1;
     const size_t w = (size_t)P.npw;     // F_MP: pT blocks of {pc, ps} and of the per-(cell, phi) tables
-    return sizeof(double) * (rb * tile * NREC + (2 + 2 * w) * nphp + tb * 2 * w * tile * nphp + tb * qvf * w * tile * nphp +
+    return sizeof(double) * (rb * tile * NREC + (2 + 2 * w) * nphp + bprows * tb * 2 * w * tile * nphp + tb * qvf * w * tile * nphp +
                              (size_t)(nk + 2 * nl) +
-                             (qrows ? tb * tile * std::min(qrows, P.nq) * kYRow : (size_t)kBlock * kYRowLY) + kExpTabN +
+                             (qrows ? tb * tile * std::min(qrows, P.nq) * kYRow : (size_t)kBlock * kYRowLY) + etab +
                              (P.tb ? 2 * tile * qrows * (P.KJ + 1) + 1 : 0) +
                              (P.tb && mode == CE ? tb * 2 * tile * nphp : 0) +
                              // the per-lane RTA-CE launch's {TE, T2} table (kernels.h PDE)
@@ -1350,7 +1355,9 @@ static SpectraPlan spectra_plan(const is3d_engine* e, bool allow_ts = true) {
     const int t = kTile, ly = P.ly, tb = P.tb, t8 = P.t8;
     kTile = is3d::kern::kTile;
     P.ly = F_LY; P.tb = 0; P.t8 = 0;
+    fb_layout = true;
     P.shmem_fb = lds_bytes(0);
+    fb_layout = false;
     kTile = t; P.ly = ly; P.tb = tb; P.t8 = t8;
   }
   return P;
@@ -2350,7 +2357,9 @@ extern "C" int is3d_calculate_dN_dX(is3d_engine* e, double* dN_taudtaudy, double
     da.npart = nc; da.npT = npT; da.nphi = nphi; da.nk = nk; da.nl = nl; da.nq = nk * nl; da.njb = njb; da.dim = dim;
     const size_t nphp = (size_t)njb * KJ;
     const size_t shmem = sizeof(double) * ((size_t)kTile * NREC + 2 * nphp + 2 * nphp + nphp + 3 * (size_t)kTile * nphp +
-                                           (size_t)kTile * kBlock + (size_t)(nk + 2 * nl) + (size_t)kTile * da.nq * kYRowLY + kExpTabN +
+                                           (size_t)kTile * kBlock + (size_t)(nk + 2 * nl) + (size_t)kTile * da.nq * kYRowLY +
+                                           // the modified launch's own exp table (kernels.h k_dndx kET; F_FB uses less)
+                                           (size_t)(mode >= PTM ? std::max(is3d::kModTabN, kExpTabN) : kExpTabN) +
                                            (mode == PTM ? (size_t)kTile * kBlock : 0));
     if (shmem > 160 * 1024) return e->fail(IS3D_ERR_ARG, "momentum grid too large for the LDS tile");
     const long nwg = (long)da.nbx * da.nchunk;

@@ -276,11 +276,7 @@ __host__ __device__ constexpr int phitab_row(int mode, int nphp, bool by = false
 #ifndef IS3D_ABLATE
 #define IS3D_ABLATE 0
 #endif
-// the modified launch builds only the per-tile tables its lanes read: no {b', Phi} rows and no separable y-term
-// slots (those serve the F_FB launch, which builds its own)
-#ifndef IS3D_MOD_TABLES
-#define IS3D_MOD_TABLES 1
-#endif
+// IS3D_MOD_TABLES (cf_math.h): the modified launch builds only the per-tile tables its lanes read
 // per-tile table loops split their flat index into (cell, row, phi) with a float reciprocal of the runtime row count
 // instead of integer divisions
 #ifndef IS3D_TAB_FDIV
@@ -748,18 +744,22 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
   constexpr int kQvF = (MODE >= PTM || !PIPE) ? 2 : 1;    // doubles per (cell, phi) of s_qv
   const int nqm = A.nqmax;                                // rows per cell (>= every workgroup's nqw)
   const long recsz = (long)kTile * NREC, bpsz = TS ? 0L : (long)npw * kTile * nphp, qvsz = kQvF * bpsz;
+  // the {b', Phi} rows: none in F_TS launches, nor in modified launches that build only the tables their lanes read
+  const long bpa = (MODMAIN && IS3D_MOD_TABLES) ? 0L : bpsz;
+  // exp table entries at LDS offset 0: the modified lanes' own table in the modified launches (IS3D_MOD_TAB_BITS)
+  constexpr int kET = MODMAIN ? kModTabN : kExpTabN;
   // y-term rows per cell: per row, or per q once the rows cover every q (nyr below): min(nqm, nq);
   // LY launches: one y-term row per lane instead ([kBlock][kYRowLY], single; odd row stride: no conflicts)
   const long ysz = LY ? (long)kBlock * kYRowLY : (long)kTile * min(nqm, A.nq) * kYRow;
   // the exp table first: at LDS offset 0 its address is the table index alone (no base register, which
   // the modified loop otherwise re-read from an SGPR spill lane at every point)
-  double* s_etab = smem;                                  // [kExpTabN] 2^(j/kExpTabN)
-  double* s_recb = smem + kExpTabN;                       // [kRecBufs][kTile][NREC]
+  double* s_etab = smem;                                  // [kET] 2^(j/kET)
+  double* s_recb = smem + kET;                            // [kRecBufs][kTile][NREC]
   dbl2* s_trig = (dbl2*)(s_recb + kRecBufs * recsz);      // [nphp]        {cos, sin}
   dbl2* s_cs = s_trig + nphp;                             // [npw][nphp]   {pT cos, pT sin}
   dbl2* s_bp = s_cs + npw * nphp;                         // [kTabBufs][npw][kTile][nphp] {b', Phi}
   // Grad / RTA-CE: [kTabBufs][kTile][nphp] PD table; modified path: {PDm, Qv} pairs (s_mw)
-  double* s_qv = (double*)(s_bp + kTabBufs * bpsz);
+  double* s_qv = (double*)(s_bp + kTabBufs * bpa);
   double* s_grid = s_qv + kTabBufs * qvsz;                // y[nk] | eta[nl] | eta_w[nl]
   double* s_y = s_grid + A.nk + 2 * A.nl;                 // [kTabBufs (LY: 1)][kTile][min(nqm, nq)][kYRow]
   // TB: [kTile][nqm][prow] {PD, T1}, 16-byte aligned for ds_read_b128 (s_grid's nk + 2 nl doubles
@@ -777,7 +777,7 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
   double* s_t1 = (double*)s_pt;
 
   const int tid = threadIdx.x;
-  for (int i = tid; i < kExpTabN; i += kBlock) s_etab[i] = kExp2Tab[i];
+  for (int i = tid; i < kET; i += kBlock) s_etab[i] = MODMAIN ? kModExp2Tab[i] : kExp2Tab[i];
   // XCD-aware block order (cdna_hip_programming.md T1): blocks that share an XCD (same
   // blockIdx % 8) take one contiguous range of logical ids, and logical ids run split-major, so
   // each XCD's L2 sees only its own cell splits (sized to fit) instead of every split
@@ -919,7 +919,7 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
   };
   // ---- phase C: the per-(cell, row, phi) tables of one tile from its buffer-tb tables (single buffer)
   // flat per-tile table index -> phi slot jj, (cell t, row qq), phi block jb and q = (r0 + qq) % nq
-  const float rnqw = 1.0f / (float)nqw, rnq = 1.0f / (float)A.nq;
+  const float rnqw = MODMAIN ? 1.0f / (float)nqw : 0.0f, rnq = MODMAIN ? 1.0f / (float)A.nq : 0.0f;
   auto tab_index = [&](int idx, int& jj, int& t, int& qq, int& jb, int& qm) __attribute__((always_inline)) {
     jj = idx % KJ;
     const int r = idx / KJ;
@@ -947,22 +947,22 @@ __global__ __launch_bounds__(kBlock, (spectra_waves_f<MODE, FLAGS, KJ>())) void 
         s_mt[((long)t * nqw + qq) * prow + jj] = modt2(R, yb + ((long)t * nyr + yr) * kYRow, s_cs[j]);
       }
     }
+    // the separable launches keep their round-5 index arithmetic (integer divisions): with tab_index the F_TS kernels
+    // compiled to the same loops but ran 1-1.5% slower (profiles/round6_r6j_ab_bisect.log)
     if constexpr (TS) {
       // T1 = SC1 pc + SS1 ps per (cell, q row, phi) (one phi block: phi slot jj)
       for (int idx = tid; idx < ntx * nqw * KJ; idx += kBlock) {
-        int jj, t, qq, jb, qm;
-        tab_index(idx, jj, t, qq, jb, qm);
-        const double* Y = yb + ((long)t * nyr + (allq ? qm : qq)) * kYRow;
+        const int jj = idx % KJ, r = idx / KJ, qq = r % nqw, t = r / nqw;
+        const double* Y = yb + ((long)t * nyr + (allq ? (int)((r0 + qq) % A.nq) : qq)) * kYRow;
         const dbl2 c = s_cs[jj];
         s_t1[((long)t * nqw + qq) * prow2 + jj] = fma(Y[Y_SC1], c.x, Y[Y_SS1] * c.y);
       }
     } else if constexpr (TB) {
       // {PD, T1 = SC1 pc + SS1 ps} per (cell, q, phi) (rows of skipped cells are never read)
       for (int idx = tid; idx < ntx * nqw * KJ; idx += kBlock) {
-        int jj, t, qq, jb, qm;
-        tab_index(idx, jj, t, qq, jb, qm);
-        const int j = jb * KJ + jj;
-        const double* Y = yb + ((long)t * nyr + (allq ? qm : qq)) * kYRow;
+        const int jj = idx % KJ, r = idx / KJ, qq = r % nqw, t = r / nqw;
+        const int j = (int)((r0 + qq) / A.nq) * KJ + jj;
+        const double* Y = yb + ((long)t * nyr + (allq ? (int)((r0 + qq) % A.nq) : qq)) * kYRow;
         const dbl2 c = s_cs[j];
         dbl2 v;
         v.x = qvt[t * nphp + j];
@@ -1285,13 +1285,14 @@ __global__ __launch_bounds__(kBlock, (dndx_waves_f<MODE, FLAGS>())) void k_dndx(
   // y-term rows without the Y_MU2 / Y_MU slots (kYRowLY): two more doubles per row took config 2's Grad
   // launch past the LDS of three workgroups per CU (k_dndx 647 -> 784 ms)
   double* s_y = s_grid + A.nk + 2 * A.nl;                 // [kTile][nq][kYRowLY]
-  double* s_etab = s_y + (long)kTile * A.nq * kYRowLY;    // [kExpTabN] exp_tab's 2^(j/kExpTabN)
+  constexpr int kET = MODMAIN ? kModTabN : kExpTabN;      // the modified lanes' own table (IS3D_MOD_TAB_BITS)
+  double* s_etab = s_y + (long)kTile * A.nq * kYRowLY;    // [kET] 2^(j/kET)
   // PTM: each lane's renormalisation factor of the tile's cells, loaded once per tile instead of once per pT (the
   // per-pT loads re-read the [cell][class] array 48 times: 7.3e11 B per config-2 pass)
-  double* s_rn = s_etab + kExpTabN;                        // [kTile][kBlock]
+  double* s_rn = s_etab + kET;                             // [kTile][kBlock]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int i = tid; i < kExpTabN; i += kBlock) s_etab[i] = kExp2Tab[i];
+  for (int i = tid; i < kET; i += kBlock) s_etab[i] = MODMAIN ? kModExp2Tab[i] : kExp2Tab[i];
   const long nwg = (long)A.nbx * A.nchunk;
   const long bid = blockIdx.x, q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
   const long lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;

@@ -373,9 +373,9 @@ extern "C" int emu_spectra_v(const orc_params* p, const orc_setup* su, const orc
                   MW[jj].x = modpdm(R, CS[jj]); MW[jj].y = QV[jj];
                   MT[jj] = modt2(R, Y, CS[jj]);
                 }
-                mod_setup<-1>(R, Y, mT, m2, pT, sign, baryon, rn_abs, kExp2Tab, M, true, mtail, MW.data(), MT.data(), nphi);
+                mod_setup<-1>(R, Y, mT, m2, pT, sign, baryon, rn_abs, kModExp2Tab, M, true, mtail, MW.data(), MT.data(), nphi);
               } else {
-                mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, kExp2Tab, M, true, mtail);
+                mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, kModExp2Tab, M, true, mtail);
               }
               if (g_census_mod) g_census_mod[M.skip ? 0 : M.clamp ? 1 : M.tail ? 2 : 3]++;
               if (g_census_mod && g_census_lane)
@@ -384,7 +384,7 @@ extern "C" int emu_spectra_v(const orc_params* p, const orc_setup* su, const orc
               // margin record (tools/mod_census.py): binades between the lane's smallest E = e^x 2^-k and |s| =
               // e^chem 2^-k, i.e. k - chem log2(e), clipped to [0, 120]; 255 for skipped / clamped lanes
               if (g_census_mod && g_census_margin) {
-                const double kk2 = (6755399441055744.0 - M.shiftk) / kExpTabN;
+                const double kk2 = (6755399441055744.0 - M.shiftk) / kModTabN;
                 const double mg = M.tail ? 120.0 : (kk2 - M.chemm * 1.4426950408889634);
                 g_census_margin[(((size_t)i * n + c) * np + s) * nq + kk * nl + l] =
                     (M.skip || M.clamp) ? 255 : (unsigned char)std::max(0.0, std::min(120.0, std::floor(mg)));
@@ -396,7 +396,7 @@ extern "C" int emu_spectra_v(const orc_params* p, const orc_setup* su, const orc
                 if (g_census_mod && M.clamp && getenv("EMU_SPAN")) {
                   double xmn = 1e300, xmx = 0;
                   for (int jj = 0; jj < nphi; jj++) { double X = fma(M.mT, MT[jj], M.E0 + MW[jj].y); xmn = fmin(xmn, sqrt(X)); xmx = fmax(xmx, sqrt(X)); }
-                  printf("SPAN %g %g %g chem %g\n", xmn / kExpTabN, xmx / kExpTabN, (xmx - xmn) / kExpTabN, M.chemm);
+                  printf("SPAN %g %g %g chem %g\n", xmn / kModTabN, xmx / kModTabN, (xmx - xmn) / kModTabN, M.chemm);
                 }
                 if (spectra_kj(nphi) % 4 == 0)
                   for (; j + 3 < nphi; j += 4) {
