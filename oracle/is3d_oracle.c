@@ -225,6 +225,15 @@ static void inverse3(const double A[9], double Ainv[3][3]) {
   }
 }
 
+/* test hook (tests/test_oracle_gsl_pins.py): the restated gsl_linalg_LU_decomp + gsl_linalg_LU_solve on one 3x3
+   system A x = b (A row-major); perm = the row permutation the decomposition chose */
+void orc_lu3_solve(const double *A, const double *b, double *x, int *perm) {
+  double LU[9];
+  memcpy(LU, A, sizeof(LU));
+  lu3_decomp(LU, perm);
+  lu3_solve(LU, perm, b, x);
+}
+
 /* Arsenal.cpp:167-208 */
 static void matvec3(double M[3][3], const double x[3], double y[3]) {
   for (int i = 0; i < 3; i++) { y[i] = 0; for (int j = 0; j < 3; j++) y[i] += M[i][j] * x[j]; }

@@ -129,6 +129,7 @@ double orc_gauss1d_mod(int kind, const double *root, const double *weight, int p
                        double mbar, double lambda, double sign);
 void orc_milne_lrf(const double *in15, double *out14);
 void orc_dsigma_lrf(const double *in9, double *out5);
+void orc_lu3_solve(const double *A9, const double *b3, double *x3, int *perm3);
 int orc_df_coefficients(const orc_params *p, const orc_setup *s, double T, double muB,
                         double E, double P, double bulkPi, double *out15, char *err, int errlen);
 int orc_jonah_table(const orc_setup *s, double *lambda2, double *z, double *bulk_over_P,

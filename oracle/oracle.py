@@ -69,6 +69,7 @@ def load():
         lib.orc_gauss1d_mod.argtypes = [C.c_int, PD, PD, C.c_int, C.c_double, C.c_double, C.c_double]
         lib.orc_milne_lrf.argtypes = [PD, PD]
         lib.orc_dsigma_lrf.argtypes = [PD, PD]
+        lib.orc_lu3_solve.argtypes = [PD, PD, PD, C.POINTER(C.c_int)]
         lib.orc_df_coefficients.argtypes = [C.POINTER(OrcParams), C.POINTER(OrcSetup), C.c_double, C.c_double,
                                             C.c_double, C.c_double, C.c_double, PD, C.c_char_p, C.c_int]
         lib.orc_jonah_table.argtypes = [C.POINTER(OrcSetup), PD, PD, PD, PD]
@@ -180,6 +181,15 @@ def df_coefficients(spec, T, muB, E, P, bulkPi, T_avg=0.0):
     err = C.create_string_buffer(256)
     rc = lib.orc_df_coefficients(C.byref(inp.params), C.byref(inp.setup), T, muB, E, P, bulkPi, _p(out), err, 256)
     return rc, out
+
+
+def lu3_solve(A, b):
+    """The restated GSL 3x3 LU solve (gsl_linalg_LU_decomp / _solve): x and the row permutation."""
+    lib = load()
+    A, b, x = _a(np.asarray(A).ravel()), _a(b), np.zeros(3)
+    perm = (C.c_int * 3)()
+    lib.orc_lu3_solve(_p(A), _p(b), _p(x), perm)
+    return x, list(perm)
 
 
 def jonah_table(spec, T_avg):

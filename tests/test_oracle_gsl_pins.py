@@ -53,3 +53,28 @@ def test_jonah_table_splines_match_natural_cubic_spline():
         lam = np.sqrt(s_l2(x)) * np.sign(x)
         worst = max(worst, abs(out[11] - lam) / max(abs(lam), 1e-3), abs(out[12] - s_z(x)) / abs(s_z(x)))
     assert worst < 1e-12, worst
+
+
+def test_lu3_matches_lapack_partial_pivoting():
+    # gsl_linalg_LU_decomp / _solve (AnisoVariables.cpp:470-480 Newton steps, MomentumSpectra.cpp:1132-1135 A^-1):
+    # partial pivoting on the first largest |a_ij| of the column, as LAPACK's dgetrf (scipy.linalg.lu_factor)
+    from scipy.linalg import lu_factor, lu_solve
+    rng = np.random.default_rng(11)
+    mats = [rng.normal(size=(3, 3)) for _ in range(200)]
+    # modified-momentum transforms A = 1 + shear + bulk (close to the identity) and Newton Jacobians (wide scales)
+    mats += [np.eye(3) + 0.3 * rng.normal(size=(3, 3)) for _ in range(100)]
+    mats += [rng.normal(size=(3, 3)) * np.array([1e3, 1.0, 1e-3])[:, None] for _ in range(100)]
+    worst = 0.0
+    for A in mats:
+        b = rng.normal(size=3)
+        x, perm = O.lu3_solve(A, b)
+        lu, piv = lu_factor(A)
+        ref = lu_solve((lu, piv), b)
+        # LAPACK's row swaps (piv: row i swapped with piv[i]) applied to the identity order give GSL's permutation
+        order = list(range(3))
+        for i, p in enumerate(piv):
+            order[i], order[p] = order[p], order[i]
+        assert order == perm
+        # forward error in units of eps x cond(A): rounding of two different operation orders only
+        worst = max(worst, np.max(np.abs(x - ref)) / np.max(np.abs(ref)) / (np.finfo(float).eps * np.linalg.cond(A)))
+    assert worst < 4.0, worst
