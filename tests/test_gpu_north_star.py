@@ -221,7 +221,10 @@ def test_split_knobs_change_only_the_summation_order(mode):
     the parity bars of the oracle; the reported split count follows.  (max_splits caps the L2-sized count of large
     surfaces; below the ~8k-workgroup fill count it does not bind, engine.hip integral_plan.)"""
     s = synth.as_read(synth.surface(400, seed=59, dimension=3, full3d=True))
-    spec = make_spec(hrg_eos=2, chosen="smash", df_mode=mode, dimension=3, pT="pT24", phi="phi32", y="y21",
+    # PTMA: the oracle's one warm-start chain is serial, so its check runs on the first 80 SMASH species (the Newton
+    # sums still cover the whole PDG; 444 species took the GPU tier 173 s here)
+    chosen = "smash" if mode != 5 else hrg.chosen_mcids("smash")[:80]
+    spec = make_spec(hrg_eos=2, chosen=chosen, df_mode=mode, dimension=3, pT="pT24", phi="phi32", y="y21",
                      famod_chains=1)
     i0, i1 = {}, {}
     base, _ = run(spec, s, info=i0)
