@@ -2345,6 +2345,8 @@ extern "C" int is3d_calculate_dN_dX(is3d_engine* e, double* dN_taudtaudy, double
     da.Sl = std::min(nc, 64);
     da.Yl = 64 / da.Sl;
     da.nbx = (nc + da.Sl - 1) / da.Sl;
+    static_assert(is3d::kern::kTile % IS3D_DNDX_TILE_MOD == 0 && is3d::kern::kTile % IS3D_DNDX_TILE == 0,
+                  "k_dndx's cells per workgroup (multiples of kTile) hold whole record tiles");
     long cpw = 4L * kTile;
     if ((long)da.nbx * ((n + cpw - 1) / cpw) < 4096) cpw = kTile;
     da.cells_per_wg = cpw;
@@ -2356,12 +2358,19 @@ extern "C" int is3d_calculate_dN_dX(is3d_engine* e, double* dN_taudtaudy, double
     da.yv = e->d_y; da.etav = e->d_eta; da.etaw = e->d_etaw;
     da.npart = nc; da.npT = npT; da.nphi = nphi; da.nk = nk; da.nl = nl; da.nq = nk * nl; da.njb = njb; da.dim = dim;
     const size_t nphp = (size_t)njb * KJ;
-    const size_t shmem = sizeof(double) * ((size_t)kTile * NREC + 2 * nphp + 2 * nphp + nphp + 3 * (size_t)kTile * nphp +
-                                           (size_t)kTile * kBlock + (size_t)(nk + 2 * nl) + (size_t)kTile * da.nq * kYRowLY +
-                                           // the modified launch's own exp table (kernels.h k_dndx kET; F_FB uses less)
-                                           (size_t)(mode >= PTM ? std::max(is3d::kModTabN, kExpTabN) : kExpTabN) +
-                                           (mode == PTM ? (size_t)kTile * kBlock : 0));
-    if (shmem > 160 * 1024) return e->fail(IS3D_ERR_ARG, "momentum grid too large for the LDS tile");
+    // kernels.h k_dndx's layout: records, trig / {pc, ps} / phi weights, {b', Phi} rows (not in the modified launch:
+    // IS3D_MOD_TABLES), Qv rows, per-lane cell sums, grid, y-term rows, exp table, PTM's renorm factors [kTile][Sl]
+    auto dndx_lds = [&](bool modmain, bool fb = false) {
+      const bool bp = !(modmain && IS3D_MOD_TABLES);
+      // kernels.h dndx_tile: the launch's record tile
+      const size_t kTile = fb ? is3d::kern::kTile : modmain ? IS3D_DNDX_TILE_MOD : IS3D_DNDX_TILE;
+      return sizeof(double) * ((size_t)kTile * NREC + 2 * nphp + 2 * nphp + nphp + (bp ? 2 : 0) * (size_t)kTile * nphp +
+                               (size_t)kTile * nphp + (size_t)kTile * kBlock + (size_t)(nk + 2 * nl) +
+                               (size_t)kTile * da.nq * kYRowLY + (size_t)(modmain ? is3d::kModTabN : kExpTabN) +
+                               (mode == PTM ? (size_t)kTile * da.Sl : 0));
+    };
+    const size_t shmem = dndx_lds(mode >= PTM), shmem_fb = dndx_lds(false, true);
+    if (std::max(shmem, shmem_fb) > 160 * 1024) return e->fail(IS3D_ERR_ARG, "momentum grid too large for the LDS tile");
     const long nwg = (long)da.nbx * da.nchunk;
     if (nwg > 0x7fffffffL) return e->fail(IS3D_ERR_ARG, "surface too large for one dN/dX launch");
     const int kflags = (e->p.regulate_deltaf ? F_REG : 0) | (e->p.outflow ? F_OUT : 0);
@@ -2382,8 +2391,8 @@ extern "C" int is3d_calculate_dN_dX(is3d_engine* e, double* dN_taudtaudy, double
       fa.fbcells = e->d_fb + 1; fa.fbcount = e->d_fb;
       fa.nchunk = std::max(1L, std::min(da.nchunk, (4096L + da.nbx - 1) / da.nbx));
       const long nfw = (long)da.nbx * fa.nchunk;
-      if (mode == PTM) launch_dndx<PTM>(dim3((unsigned)nfw), shmem, st, fa, kflags | F_FB, KJ);
-      else launch_dndx<PTB>(dim3((unsigned)nfw), shmem, st, fa, kflags | F_FB, KJ);
+      if (mode == PTM) launch_dndx<PTM>(dim3((unsigned)nfw), shmem_fb, st, fa, kflags | F_FB, KJ);
+      else launch_dndx<PTB>(dim3((unsigned)nfw), shmem_fb, st, fa, kflags | F_FB, KJ);
       HIPCHK(e, hipGetLastError());
     }
     e->ycell_n = n;

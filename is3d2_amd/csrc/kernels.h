@@ -82,6 +82,18 @@ constexpr int dndx_waves() { return (MODE == CE || MODE >= PTM) ? 2 : spectra_wa
 #endif
 template <int MODE, int FLAGS>
 constexpr int dndx_waves_f() { return (MODE >= PTM && !(FLAGS & 32)) ? IS3D_DNDX_WAVES_MOD : dndx_waves<MODE>(); }
+#ifndef IS3D_DNDX_TILE_MOD
+#define IS3D_DNDX_TILE_MOD 4       // k_dndx's modified launch: cells per record tile (engine.hip sizes its LDS the same way).
+                                   // 4: ~28 KB of LDS and 126-128 VGPRs, 4 workgroups per CU; config 2 operation 0 against
+                                   // 8-cell tiles (53 KB, 3 per CU): PTM 661 -> 645 ms, PTB 661 -> 640 ms
+                                   // (profiles/round6_r6q_ab_dndx_tile.log)
+#endif
+#ifndef IS3D_DNDX_TILE
+#define IS3D_DNDX_TILE 8           // k_dndx's Grad / RTA-CE launches: cells per record tile
+#endif
+// cells per record tile of a k_dndx launch (the F_FB launch keeps kTile)
+template <int MODE, int FLAGS>
+constexpr int dndx_tile() { return (FLAGS & 32) ? kTile : (MODE >= PTM ? IS3D_DNDX_TILE_MOD : IS3D_DNDX_TILE); }
 
 // LDS row stride of the y-terms (doubles): NYT | 1 is odd, so the 8-byte stores of one y-term field
 // by consecutive lanes (rows 152 B apart) spread over the 64 banks instead of hitting two of them
@@ -1273,13 +1285,15 @@ __global__ __launch_bounds__(kBlock, (dndx_waves_f<MODE, FLAGS>())) void k_dndx(
   constexpr bool FB = MODE >= PTM && (FLAGS & F_FB) != 0;   // separable-fallback launch of a modified mode
   constexpr bool MODMAIN = MODE >= PTM && !FB;              // modified launch: separable lanes left to F_FB
   extern __shared__ double smem[];
+  constexpr int kTile = dndx_tile<MODE, FLAGS>();         // cells per record tile of this launch
   const int nphp = A.njb * KJ;
   double* s_rec = smem;                                   // [kTile][NREC]
   dbl2* s_trig = (dbl2*)(s_rec + kTile * NREC);           // [nphp] {cos, sin}
   dbl2* s_cs = s_trig + nphp;                             // [nphp] {pT cos, pT sin} of the current pT
   double* s_w = (double*)(s_cs + nphp);                   // [nphp] phi weights (0 in the padding)
   dbl2* s_bp = (dbl2*)(s_w + nphp);                       // [kTile][nphp] {b', Phi} of the current pT
-  double* s_qv = (double*)(s_bp + kTile * nphp);         // [kTile][nphp] Qv of the current pT (modified path)
+  // (none in the modified launch, which builds only the tables its lanes read: IS3D_MOD_TABLES)
+  double* s_qv = (double*)(s_bp + ((MODMAIN && IS3D_MOD_TABLES) ? 0 : kTile * nphp));   // [kTile][nphp] Qv (modified path)
   double* s_red = s_qv + kTile * nphp;                    // [kTile][kBlock] per-lane cell sums
   double* s_grid = s_red + kTile * kBlock;                // y[nk] | eta[nl] | eta_w[nl]
   // y-term rows without the Y_MU2 / Y_MU slots (kYRowLY): two more doubles per row took config 2's Grad
@@ -1287,9 +1301,11 @@ __global__ __launch_bounds__(kBlock, (dndx_waves_f<MODE, FLAGS>())) void k_dndx(
   double* s_y = s_grid + A.nk + 2 * A.nl;                 // [kTile][nq][kYRowLY]
   constexpr int kET = MODMAIN ? kModTabN : kExpTabN;      // the modified lanes' own table (IS3D_MOD_TAB_BITS)
   double* s_etab = s_y + (long)kTile * A.nq * kYRowLY;    // [kET] 2^(j/kET)
-  // PTM: each lane's renormalisation factor of the tile's cells, loaded once per tile instead of once per pT (the
-  // per-pT loads re-read the [cell][class] array 48 times: 7.3e11 B per config-2 pass)
-  double* s_rn = s_etab + kET;                             // [kTile][kBlock]
+  // PTM: the renormalisation factor of the tile's cells for the workgroup's Sl species, loaded once per tile instead of
+  // once per pT (the per-pT loads re-read the [cell][class] array 48 times: 7.3e11 B per config-2 pass); one entry
+  // per species, not per lane (the lanes of a species share it): 4 KB instead of 16 KB, which takes PTM's launch to
+  // the LDS of three workgroups per CU, as PTB's
+  double* s_rn = s_etab + kET;                             // [kTile][Sl]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   for (int i = tid; i < kET; i += kBlock) s_etab[i] = MODMAIN ? kModExp2Tab[i] : kExp2Tab[i];
@@ -1333,9 +1349,11 @@ __global__ __launch_bounds__(kBlock, (dndx_waves_f<MODE, FLAGS>())) void k_dndx(
     for (int i = tid; i < nt * NREC; i += kBlock) s_rec[i] = A.rec[cell_of(cb + i / NREC) * NREC + i % NREC];
 #pragma unroll
     for (int t = 0; t < kTile; t++) s_red[t * kBlock + tid] = 0.0;
-    if (MODE == PTM && active) {
-      const int rc = A.rcls[s];
-      for (int t = 0; t < nt; t++) s_rn[t * kBlock + tid] = A.renorm[cell_of(cb + t) * A.nrcls + rc];
+    if (MODE == PTM) {
+      for (int idx = tid; idx < nt * A.Sl; idx += kBlock) {
+        const int t = idx / A.Sl, sl = idx % A.Sl, s2 = grp * A.Sl + sl;
+        if (s2 < A.npart) s_rn[idx] = A.renorm[cell_of(cb + t) * A.nrcls + A.rcls[s2]];
+      }
     }
     __syncthreads();
     for (int idx = tid; idx < nt * A.nq; idx += kBlock) {
@@ -1383,7 +1401,7 @@ __global__ __launch_bounds__(kBlock, (dndx_waves_f<MODE, FLAGS>())) void k_dndx(
         if (kind == 0.0) continue;
         double rn_abs = R[R_RENORM];
         if (MODE == PTM || MODE == PTB) {
-          const double rn = (MODE == PTM) ? s_rn[t * kBlock + tid] : R[R_RENORM];
+          const double rn = (MODE == PTM) ? s_rn[t * A.Sl + s_l] : R[R_RENORM];
           if (!isfinite(rn)) continue;    // cell skipped for this species (SpacetimeDistribution.cpp:972-976)
           rn_abs = fabs(rn);
         }
