@@ -2365,7 +2365,8 @@ extern "C" int is3d_calculate_dN_dX(is3d_engine* e, double* dN_taudtaudy, double
       // kernels.h dndx_tile: the launch's record tile
       const size_t kTile = fb ? is3d::kern::kTile : modmain ? IS3D_DNDX_TILE_MOD : IS3D_DNDX_TILE;
       return sizeof(double) * ((size_t)kTile * NREC + 2 * nphp + 2 * nphp + nphp + (bp ? 2 : 0) * (size_t)kTile * nphp +
-                               (size_t)kTile * nphp + (size_t)kTile * kBlock + (size_t)(nk + 2 * nl) +
+                               (modmain && IS3D_DNDX_PDM && KJ % 4 == 0 ? 2 : 1) * (size_t)kTile * nphp +
+                               (size_t)kTile * kBlock + (size_t)(nk + 2 * nl) +
                                (size_t)kTile * da.nq * kYRowLY + (size_t)(modmain ? is3d::kModTabN : kExpTabN) +
                                (mode == PTM ? (size_t)kTile * da.Sl : 0));
     };

@@ -91,6 +91,17 @@ constexpr int dndx_waves_f() { return (MODE >= PTM && !(FLAGS & 32)) ? IS3D_DNDX
 #ifndef IS3D_DNDX_TILE
 #define IS3D_DNDX_TILE 8           // k_dndx's Grad / RTA-CE launches: cells per record tile
 #endif
+#ifndef IS3D_DNDX_PD
+#define IS3D_DNDX_PD 2             // k_dndx's separable launches with per-(cell, phi) PD = p.dsigma_perp b' rows (k_spectra's
+                                   // PD-table fours: w p.dsigma f_eq = fma(D0, b', escw PD), one op fewer per point); bit 1
+                                   // Grad, bit 2 RTA-CE.  Config 2 operation 0 (profiles/round6_r6v_ab_dndx_pd.log): RTA-CE
+                                   // 485.2 -> 474.7 ms; Grad 317.6 -> 330.3 ms (its Boltzmann-tail pairs become fours): off
+#endif
+template <int MODE>
+constexpr bool dndx_pd() { return (MODE == GRAD && (IS3D_DNDX_PD & 1)) || (MODE == CE && (IS3D_DNDX_PD & 2)); }
+#ifndef IS3D_DNDX_PDM
+#define IS3D_DNDX_PDM 1            // k_dndx's modified launch: per-(cell, phi) {PDm, Qv} rows, p.dsigma = fma(Dw, PDm, D0)
+#endif
 // cells per record tile of a k_dndx launch (the F_FB launch keeps kTile)
 template <int MODE, int FLAGS>
 constexpr int dndx_tile() { return (FLAGS & 32) ? kTile : (MODE >= PTM ? IS3D_DNDX_TILE_MOD : IS3D_DNDX_TILE); }
@@ -1226,6 +1237,78 @@ __device__ __forceinline__ double sep_phi_wsum_tail(const SepLane& L, const dbl2
   return a0 + a1;
 }
 
+// sep_phi_wsum for fast lanes with the per-(cell, phi) PD rows (IS3D_DNDX_PD): sep_quad_pd_t's fours
+template <int MODE, int FLAGS, int KJ>
+__device__ __forceinline__ double sep_phi_wsum_pd(const SepLane& L, const dbl2* CS, const dbl2* BP, const double* PD,
+                                                  const dbl2* W) {
+  constexpr int FL = (MODE == GRAD) ? SEP_GRAD : SEP_CE;
+  constexpr bool REG = (FLAGS & F_REG) != 0, OUT = (FLAGS & F_OUT) != 0;
+  static_assert(KJ % 4 == 0, "fours");
+  double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+  for (int jj = 0; jj < KJ; jj += 4) {
+    const dbl2 c[4] = {CS[jj], CS[jj + 1], CS[jj + 2], CS[jj + 3]}, b[4] = {BP[jj], BP[jj + 1], BP[jj + 2], BP[jj + 3]};
+    const double pd[4] = {PD[jj], PD[jj + 1], PD[jj + 2], PD[jj + 3]};
+    const dbl2 wa = W[jj >> 1], wb = W[(jj >> 1) + 1];
+    double v[4];
+    sep_quad_pd_t<FL, REG, OUT, true>(L, c, b, pd, v);
+    a0 = fma(wa.x, v[0], a0); a1 = fma(wa.y, v[1], a1);
+    a0 = fma(wb.x, v[2], a0); a1 = fma(wb.y, v[3], a1);
+  }
+  return a0 + a1;
+}
+
+// Boltzmann-tail Grad lanes with the PD rows: sep_quad_pd_tail_t's fours (w p.dsigma f_eq in two ops)
+template <int MODE, int FLAGS, int KJ>
+__device__ __forceinline__ double sep_phi_wsum_pd_tail(const SepLane& L, const dbl2* CS, const dbl2* BP, const double* PD,
+                                                       const dbl2* W) {
+  constexpr int FL = (MODE == GRAD) ? SEP_GRAD : SEP_CE;
+  constexpr bool REG = (FLAGS & F_REG) != 0, OUT = (FLAGS & F_OUT) != 0;
+  static_assert(KJ % 4 == 0, "fours");
+  double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+  for (int jj = 0; jj < KJ; jj += 4) {
+    const dbl2 c[4] = {CS[jj], CS[jj + 1], CS[jj + 2], CS[jj + 3]}, b[4] = {BP[jj], BP[jj + 1], BP[jj + 2], BP[jj + 3]};
+    const double pd[4] = {PD[jj], PD[jj + 1], PD[jj + 2], PD[jj + 3]};
+    const dbl2 wa = W[jj >> 1], wb = W[(jj >> 1) + 1];
+    double v[4] = {0.0, 0.0, 0.0, 0.0};
+    sep_quad_pd_tail_t<FL, REG, OUT>(L, c, b, pd, v);
+    a0 = fma(wa.x, v[0], a0); a1 = fma(wa.y, v[1], a1);
+    a0 = fma(wb.x, v[2], a0); a1 = fma(wb.y, v[3], a1);
+  }
+  return a0 + a1;
+}
+
+// mod_phi_wsum with the per-(cell, phi) {PDm, Qv} rows (IS3D_DNDX_PDM): p.dsigma |renorm| = fma(Dw, PDm, D0), one op
+// where the lane's linear form took two (the k_spectra table launch's form; Dw PDm = Dc pc + Ds ps to rounding)
+template <int FLAGS, bool CLAMP, int KJ>
+__device__ __forceinline__ double mod_phi_wsum_mw(const ModLane& M, const dbl2* CS, const dbl2* MW, const dbl2* W) {
+  constexpr bool OUT = (FLAGS & F_OUT) != 0;
+  static_assert(KJ % 4 == 0, "fours");
+  double a0 = 0.0, a1 = 0.0;
+#pragma unroll IS3D_DNDX_MOD_UNROLL
+  for (int jj = 0; jj < KJ; jj += 4) {
+    const dbl2 c[4] = {CS[jj], CS[jj + 1], CS[jj + 2], CS[jj + 3]};
+    const dbl2 mw[4] = {MW[jj], MW[jj + 1], MW[jj + 2], MW[jj + 3]};
+    const dbl2 wa = W[jj >> 1], wb = W[(jj >> 1) + 1];
+    double X[4], num[4], q[4], rq[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) X[i] = fma(M.Ec, c[i].x, fma(M.Es, c[i].y, M.E0 + mw[i].y));
+    mod_nq4<CLAMP>(M, X, num, q);
+    mod_quad_rq(q, rq);
+    double v[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      const double pds = fma(M.Dw, mw[i].x, M.D0);
+      const double g = pds * (num[i] * rq[i]);
+      v[i] = (OUT && pds <= 0.0) ? 0.0 : g;
+    }
+    a0 = fma(wa.x, v[0], a0); a1 = fma(wa.y, v[1], a1);
+    a0 = fma(wb.x, v[2], a0); a1 = fma(wb.y, v[3], a1);
+  }
+  return a0 + a1;
+}
+
 template <int FLAGS, bool CLAMP, int KJ>
 __device__ __forceinline__ double mod_phi_wsum(const ModLane& M, const dbl2* CS, const dbl2* QV, const dbl2* W) {
   constexpr bool OUT = (FLAGS & F_OUT) != 0;
@@ -1294,7 +1377,9 @@ __global__ __launch_bounds__(kBlock, (dndx_waves_f<MODE, FLAGS>())) void k_dndx(
   dbl2* s_bp = (dbl2*)(s_w + nphp);                       // [kTile][nphp] {b', Phi} of the current pT
   // (none in the modified launch, which builds only the tables its lanes read: IS3D_MOD_TABLES)
   double* s_qv = (double*)(s_bp + ((MODMAIN && IS3D_MOD_TABLES) ? 0 : kTile * nphp));   // [kTile][nphp] Qv (modified path)
-  double* s_red = s_qv + kTile * nphp;                    // [kTile][kBlock] per-lane cell sums
+  // the modified launch's rows are {PDm, Qv} pairs with IS3D_DNDX_PDM
+  constexpr bool MW = MODMAIN && IS3D_DNDX_PDM && KJ % 4 == 0;
+  double* s_red = s_qv + (MW ? 2 : 1) * kTile * nphp;     // [kTile][kBlock] per-lane cell sums
   double* s_grid = s_red + kTile * kBlock;                // y[nk] | eta[nl] | eta_w[nl]
   // y-term rows without the Y_MU2 / Y_MU slots (kYRowLY): two more doubles per row took config 2's Grad
   // launch past the LDS of three workgroups per CU (k_dndx 647 -> 784 ms)
@@ -1391,7 +1476,16 @@ __global__ __launch_bounds__(kBlock, (dndx_waves_f<MODE, FLAGS>())) void k_dndx(
           }
         }
         if constexpr (!(MODMAIN && IS3D_MOD_TABLES)) s_bp[t * nphp + j] = v;
-        if (MODE >= PTM) s_qv[t * nphp + j] = qv;
+        if constexpr (dndx_pd<MODE>() && KJ % 4 == 0) {
+          dbl2 c; c.x = pT * s_trig[j].x; c.y = pT * s_trig[j].y;
+          s_qv[t * nphp + j] = (j < A.nphi && R[R_KIND] != 0.0) ? sep_pd(R, c, v.x) : 0.0;   // PD rows (sep_pd)
+        } else if constexpr (MW) {
+          dbl2 m; m.x = 0.0; m.y = qv;
+          if (j < A.nphi && R[R_KIND] == 2.0) { dbl2 c; c.x = pT * s_trig[j].x; c.y = pT * s_trig[j].y; m.x = modpdm(R, c); }
+          ((dbl2*)s_qv)[t * nphp + j] = m;
+        } else if (MODE >= PTM) {
+          s_qv[t * nphp + j] = qv;
+        }
       }
       __syncthreads();
       if (!active) continue;
@@ -1423,6 +1517,13 @@ __global__ __launch_bounds__(kBlock, (dndx_waves_f<MODE, FLAGS>())) void k_dndx(
             constexpr bool TL = IS3D_TAIL_DNDX && MODE == GRAD;
             sep_setup(sep_flavor(MODE), R, Y, mT, mT2, m2, mTb, pT, sign, baryon, s_etab, L, TL ? 2 : 0, 0, true);
             if (L.skip) continue;
+            constexpr bool PDL = dndx_pd<MODE>() && KJ % 4 == 0;
+            const double* PDr = s_qv + t * nphp + j0;
+            if constexpr (PDL) {
+              if (TL && L.tail) cell += sep_phi_wsum_pd_tail<MODE, FLAGS, KJ>(L, s_cs + j0, BP, PDr, W);
+              else if (L.fast) cell += sep_phi_wsum_pd<MODE, FLAGS, KJ>(L, s_cs + j0, BP, PDr, W);
+              else cell += sep_phi_wsum<MODE, FLAGS, false, KJ>(L, s_cs + j0, BP, W);
+            } else
             if (TL && L.tail) cell += sep_phi_wsum_tail<MODE, FLAGS, KJ>(L, s_cs + j0, BP, W);
             else cell += L.fast ? sep_phi_wsum<MODE, FLAGS, true, KJ>(L, s_cs + j0, BP, W)
                                 : sep_phi_wsum<MODE, FLAGS, false, KJ>(L, s_cs + j0, BP, W);
@@ -1431,9 +1532,15 @@ __global__ __launch_bounds__(kBlock, (dndx_waves_f<MODE, FLAGS>())) void k_dndx(
             ModLane M;
             mod_setup(R, Y, mT, m2, pT, sign, baryon, rn_abs, s_etab, M, false);
             if (M.skip) continue;
-            const dbl2* QV = (const dbl2*)(s_qv + t * nphp + j0);
-            cell += M.clamp ? mod_phi_wsum<FLAGS, true, KJ>(M, s_cs + j0, QV, W)
-                            : mod_phi_wsum<FLAGS, false, KJ>(M, s_cs + j0, QV, W);
+            if constexpr (MW) {
+              const dbl2* MWr = (const dbl2*)s_qv + t * nphp + j0;
+              cell += M.clamp ? mod_phi_wsum_mw<FLAGS, true, KJ>(M, s_cs + j0, MWr, W)
+                              : mod_phi_wsum_mw<FLAGS, false, KJ>(M, s_cs + j0, MWr, W);
+            } else {
+              const dbl2* QV = (const dbl2*)(s_qv + t * nphp + j0);
+              cell += M.clamp ? mod_phi_wsum<FLAGS, true, KJ>(M, s_cs + j0, QV, W)
+                              : mod_phi_wsum<FLAGS, false, KJ>(M, s_cs + j0, QV, W);
+            }
           }
         }
         s_red[t * kBlock + tid] = fma(wpT, cell, s_red[t * kBlock + tid]);
