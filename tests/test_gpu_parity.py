@@ -189,6 +189,46 @@ def test_full_size_properties(mode):
     assert np.abs(d[~m] - 2.0 * full[~m]).max(initial=0.0) <= 1e-300
 
 
+@pytest.mark.parametrize("mode", [1, 2, 3, 4, 5])
+def test_config3_full_size_properties(mode):
+    """BASELINE config 3 at full size: config 2's surface and grid with shear + bulk + baryon on (the bench's flags: PTB
+    without baryon terms, as bench.py runs it), every delta-f mode -- the F_BY scalar-table launches of Grad / RTA-CE,
+    the modified launches with baryon chemistry (e^chem folded out of the table lanes) and PTMA's warm-start chain at
+    10^5 cells.  Additive over a cell split and invariant under a permutation (not PTMA: its chain warm-starts each
+    cell from the previous one, so a split or a reordering moves the Newton starting points), and bit-exact 2x under
+    dsigma -> 2 dsigma (the Newton solve does not see dsigma)."""
+    baryon = mode != 4
+    s = synth.as_read(synth.surface(100000, seed=7, dimension=3, baryon=True, full3d=True))
+    flags = dict(include_baryon=1, include_baryondiff_deltaf=1) if baryon else {}
+    spec = make_spec(hrg_eos=2, chosen="smash", df_mode=mode, dimension=3, pT="pT48", phi="phi32", y="y21", **flags)
+    e = build_engine(spec, s)
+    full = e.calculate_spectra()
+    n = len(s["tau"])
+    parts = None
+    if mode != 5:
+        h = n // 2 + 777
+        e.set_surface({k: np.ascontiguousarray(v[:h]) for k, v in s.items()})
+        a = e.calculate_spectra()
+        e.set_surface({k: np.ascontiguousarray(v[h:]) for k, v in s.items()})
+        b = e.calculate_spectra()
+        perm = np.random.default_rng(3).permutation(n)
+        e.set_surface({k: np.ascontiguousarray(v[perm]) for k, v in s.items()})
+        parts = (a + b, e.calculate_spectra())
+    s2 = dict(s)
+    for k in ("dat", "dax", "day", "dan"):
+        s2[k] = 2.0 * s[k]
+    e.set_surface(s2)
+    d = e.calculate_spectra()
+    e.close()
+    assert np.isfinite(full).all() and (full != 0).sum() > 0.5 * full.size
+    if parts is not None:
+        assert _rel(parts[0], full) < TOL
+        assert _rel(parts[1], full) < TOL
+    m = np.abs(full) > 1e-290
+    assert np.array_equal(d[m], 2.0 * full[m])
+    assert np.abs(d[~m] - 2.0 * full[~m]).max(initial=0.0) <= 1e-300
+
+
 @pytest.mark.parametrize("phi", ["phi_default", "phi24", "phi32", "phi48"])
 @pytest.mark.parametrize("dim,mode", [(2, 1), (3, 2), (2, 3), (3, 5)])
 def test_phi_grid_blocks(phi, dim, mode):
