@@ -55,10 +55,13 @@ def test_dndx_baryon_flags(mode):
     check(run_gpu(spec, s), O.dndx(spec, s, carry=0, return_cells=True))
 
 
-def test_dndx_smash_many_lane_groups():
-    # 444 species: 7 species groups of 64 mass-sorted species, 21 y tasks over 4 slots
+@pytest.mark.parametrize("mode", [2, 3, 4])
+def test_dndx_smash_many_lane_groups(mode):
+    # 444 species: 7 species groups of 64 mass-sorted species, 21 y tasks over 4 slots; 70 cells end in a ragged record
+    # tile of the 8-cell separable launches and of the modified launch's 4-cell tiles (its per-(cell, species) PTM
+    # renorm rows and {PDm, Qv} rows, round 6)
     s = synth.as_read(synth.surface(70, seed=34, dimension=3))
-    spec = make_spec(hrg_eos=2, chosen="smash", df_mode=2, dimension=3, pT="pT48", phi="phi32")
+    spec = make_spec(hrg_eos=2, chosen="smash", df_mode=mode, dimension=3, pT="pT48", phi="phi32")
     check(run_gpu(spec, s), O.dndx(spec, s, threads=8, carry=0, omp_threads=8, return_cells=True))
 
 
